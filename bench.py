@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""bench.py — frames/sec of the CNN-TDNN fwd+bwd training step on MI355X.
+
+Metric (BASELINE.json): frames/sec CNN-TDNN fwd+bwd, 40-dim x 1500-frame egs,
+1/2/4/8 MI355X. One step = forward + backward + gradient all-reduce (N > 1) +
+SGD over one minibatch of 64 synthetic egs (96,000 frames) per GPU, on the
+pinned synthetic 17-TDNN-F model (configs/cnn_tdnn_17f.xconfig).
+Inputs are resident in HBM before the timed region.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RCCL all-reduce of the flat fp32
+gradient). Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+# torch first: kfp16's libraries then bind to the same HIP runtime (kfp16.hip_runtimes)
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kaldi-fp16_amd", "python"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "frames/sec CNN-TDNN fwd+bwd, 40-dim×1500-frame egs, 1/2/4/8 MI355X"
+PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16 MFMA (MI355X_MICROARCH.md)
+FRAMES_PER_EG = 1500
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--egs", type=int, default=64, help="egs per GPU")
+    p.add_argument("--xconfig", default="cnn_tdnn_17f.xconfig")
+    p.add_argument("--lr", type=float, default=1e-4)
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-frames", type=int, default=1500)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-prof", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(xcfg, params, bns, frames, threads):
+    """The C oracle (a port of the reference's CNN-TDNN math) timed on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from kfp16 import synth
+    try:
+        oracle.build(native=True)
+        oracle.lib(native=True)
+    except Exception:
+        oracle.lib()
+    tp = {k: synth.trunc_fp16(v) for k, v in params.items()}
+    on = oracle.OracleNet(xcfg, tp, bns, round_mode=oracle.ROUND_FUSED, threads=threads)
+    feats = synth.make_features(frames, 40).astype(np.float32)
+    og = (np.random.default_rng(5).standard_normal((frames, 3080)) * 0.02).astype(np.float16).astype(np.float32)
+    t0 = time.perf_counter()
+    on.forward(feats)
+    on.backward(og)
+    dt = time.perf_counter() - t0
+    on.close()
+    return {"value": round(frames / dt, 2), "unit": "frames/sec", "cores": threads, "kind": "port",
+            "sample": f"C oracle fwd+bwd of cnn_tdnn_17f on {frames} frames (1 eg), fp32 math, "
+                      f"{threads} threads, {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    import kfp16
+    from kfp16 import synth
+    kfp16.check(kfp16.core.bridge_gpu_init(local), "bridge_gpu_init")
+    stream = torch.cuda.current_stream()
+    kfp16.set_stream(stream.cuda_stream)
+    kfp16.assert_single_hip_runtime()
+
+    T = a.egs * FRAMES_PER_EG
+    xcfg = synth.load_xconfig(a.xconfig)
+    net = kfp16.Network(xcfg, max_frames=T)
+    params, bns = synth.init_network(net, seed=42)        # identical replicas on every rank
+    grad = torch.zeros(net.num_params, dtype=torch.float32, device="cuda")
+    net.bind_grad_buffer(grad.data_ptr())
+
+    feats = synth.make_features(T, 40, seed=1234 + rank)   # this rank's shard of egs
+    fbuf = torch.from_numpy(feats.view(np.int16)).to("cuda")
+    P = net.layers[-1][3]
+    # output gradient of the chain objective's shape: non-zero only on the
+    # subsampled frames (leftCtx 30, stride 3), as TrainStep scatters it
+    og = np.zeros((T, P), np.float16)
+    rows = np.concatenate([np.arange(30, FRAMES_PER_EG, 3) + e * FRAMES_PER_EG for e in range(a.egs)])
+    og[rows] = (np.random.default_rng(99 + rank).standard_normal((len(rows), P)) * 0.02).astype(np.float16)
+    gbuf = torch.from_numpy(og.view(np.int16)).to("cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        net.forward(fbuf.data_ptr(), T)
+        net.backward(gbuf.data_ptr())
+        if world > 1:
+            dist.all_reduce(grad)
+            grad.mul_(1.0 / world)
+        net.sgd(a.lr, a.momentum)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not a.no_prof:
+        kfp16.core.kf_prof_reset()
+        kfp16.core.kf_prof_enable(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kfp16.core.kf_prof_enable(0)
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    prof = {}
+    if not a.no_prof:
+        for cls, name in ((0, "gemm_fused"), (1, "gemm_wgrad")):
+            n, ms, fl = kfp16.prof_collect(cls)
+            prof[name] = (n, ms, fl)
+        kfp16.core.kf_prof_reset()
+
+    if rank == 0:
+        ms_step = elapsed / a.steps * 1e3
+        frames = T * world * a.steps
+        value = frames / elapsed
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+            "data": "synthetic",
+            "config": {"workload": "cnn_tdnn_17f train step (fwd+bwd+SGD), 64 egs x 1500 frames per GPU",
+                       "xconfig": a.xconfig, "egs_per_gpu": a.egs, "frames_per_eg": FRAMES_PER_EG,
+                       "global_batch_egs": a.egs * world, "parallelism": f"dp{world}",
+                       "output_grad": "synthetic fp16 on subsampled frames (chain objective not in step)"},
+        }
+        if prof:
+            dom = max(prof, key=lambda k: prof[k][1])
+            n, ms, fl = prof[dom]
+            ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+            out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP16_TFLOPS,
+                               "unit": "TFLOP/s", "frac": round(ach / PEAK_FP16_TFLOPS, 4), "traffic": None,
+                               "kernel": dom, "launches": n, "kernel_ms_per_step": round(ms / a.steps, 3),
+                               "all_gemm_tflops": round(sum(v[2] for v in prof.values()) /
+                                                        (sum(v[1] for v in prof.values()) * 1e-3) / 1e12, 2)}
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, a.cpu_threads)
+        print(json.dumps(out), flush=True)
+    net.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,77 @@
+/*
+ * kf_nnet.h — C-ABI of this build's host layer: the C++ restatement of the
+ * reference's Go packages internal/nnet (xconfig.go, layers.go, model.go,
+ * forward.go, network_backward.go, train_step.go) and internal/gpu
+ * (optimize.go), running on the MI355X kernels of kf_ops.h.
+ *
+ * The reference's host code is Go; no Go toolchain exists in this image, so the
+ * host layer is C++. The entry points below are the
+ * Network / Trainer API of internal/nnet flattened into C:
+ *   nnet_create        <- BuildModelFromString (model.go:31) + NewNetwork (forward.go:111)
+ *   nnet_forward       <- Network.Forward (forward.go:148)
+ *   nnet_backward      <- Network.Backward (network_backward.go:94)
+ *   nnet_sgd           <- SGDOptimizer.Update for every parameter (optimize.go:95)
+ *   nnet_train_step    <- TrainStep (train_step.go:142) with the chain objective
+ * Errors: NULL / -1 with the text in nnet_last_error() (thread-local).
+ */
+#ifndef KALDI_FP16_AMD_KF_NNET_H
+#define KALDI_FP16_AMD_KF_NNET_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct KfNet KfNet;
+
+/* layer type codes reported by nnet_layer_info (xconfig.go:18-30 order) */
+enum {
+    NNET_INPUT = 0, NNET_IDCT, NNET_LINEAR, NNET_BATCHNORM, NNET_SPECAUGMENT,
+    NNET_COMBINE_FEATURE_MAPS, NNET_CONV_RELU_BN, NNET_TDNNF, NNET_ATTENTION,
+    NNET_PREFINAL, NNET_OUTPUT
+};
+
+const char *nnet_last_error(void);
+
+/* parse + resolve an xconfig and allocate weights/activations for max_frames */
+KfNet *nnet_create(const char *xconfig_text, int max_frames);
+/* parse + resolve only, no device work: "name type in out" per layer, then
+ * "params N"; returns the bytes needed (incl. NUL) or -1 */
+int nnet_parse_summary(const char *xconfig_text, char *out, int outlen);
+void nnet_free(KfNet *net);
+
+int nnet_num_layers(const KfNet *net);  /* excluding input layers */
+int nnet_layer_info(const KfNet *net, int idx, char *name, int namelen, int *type, int *in_dim,
+                    int *out_dim);
+/* trainable parameters: flat fp32 master / fp16 working / fp32 grad / fp32 velocity */
+long long nnet_num_params(const KfNet *net);
+int nnet_num_param_tensors(const KfNet *net);
+int nnet_param_info(const KfNet *net, int idx, char *name, int namelen, int *rows, int *cols,
+                    long long *offset);
+/* host fp32 values in the flat layout; stored fp16 by truncation
+ * (internal/gpu/tensor.go:158-173) and the master copy = that fp16 value
+ * (optimize.go:52-70 via ops_fp16_to_fp32) */
+int nnet_set_params(KfNet *net, const float *host_flat);
+int nnet_get_params(const KfNet *net, float *host_flat); /* fp32 master */
+/* which = 0: the layer's (first) BatchNorm, 1: prefinal's second BatchNorm */
+int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean, const float *var,
+                const float *gamma, const float *beta, float eps, float target_rms);
+
+/* forward on T frames of fp16 features already in device memory */
+int nnet_forward(KfNet *net, const void *features_dev, int T);
+/* device pointer of a layer's output activation (fp16 [rows x cols]) */
+const void *nnet_activation(const KfNet *net, const char *layer, int *rows, int *cols);
+/* backward from the fp16 gradient of the chain output [T x num_pdfs] */
+int nnet_backward(KfNet *net, const void *out_grad_dev);
+float *nnet_grad_buffer(KfNet *net);   /* device fp32 [num_params] */
+/* use caller-owned device memory (>= num_params fp32) as the gradient buffer */
+int nnet_bind_grad_buffer(KfNet *net, float *dev);
+float *nnet_master_buffer(KfNet *net); /* device fp32 [num_params] */
+void *nnet_weight_buffer(KfNet *net);  /* device fp16 [num_params] */
+int nnet_sgd(KfNet *net, float lr, float momentum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,140 @@
+/*
+ * kf_ops.h — MI355X extension of the kaldi-fp16 C-ABI: fused, implicitly
+ * addressed FP16 MFMA GEMMs and the few multi-tensor kernels the CNN-TDNN
+ * training step needs. Nothing here replaces a reference symbol; these entry
+ * points are what this build's host layer (the C++ mirror of internal/nnet and
+ * internal/gpu, see kf_nnet.h) calls so that the splice / im2col / epilogue
+ * work the reference does as separate kernels and host round trips
+ * (internal/nnet/forward.go:418-790, internal/gpu/backward_ops.go:162-253)
+ * happens inside one GEMM launch. Plain C types only; no torch, no HIP types.
+ *
+ * Operand addressing (KfOperand). An operand is a logical row-major matrix
+ * Op[r][c] (r < nrows, c < ncols) whose 8-element column chunks are fetched
+ * from memory by this rule (all counts in elements):
+ *   part p = c / part_width, kk = c % part_width      (nparts parts)
+ *   t = r / hout, h = r % hout                         (hout = 1 for TDNN rows)
+ *   if edge_t[p] >= 0 and t == edge_t[p]: read edge_ptr[p][kk]
+ *   st = t + dt[p]; outside [0, T): clamp (tpolicy=KF_CLAMP) or zero (KF_ZERO)
+ *   shn = h*hmul + dh[p]; zero unless shn % hdiv == 0; sh = shn / hdiv,
+ *   zero unless 0 <= sh < hsrc
+ *   value = base[st*ld + sh*part_width + kk]
+ * With nparts=1, hout=1, dt=0 this is a plain [nrows x ncols] matrix with
+ * leading dimension ld. The same rule expresses the TDNN time splice
+ * (forward.go:699-790: dt = {-s, 0} clamp, or {0, +s} clamp), the conv im2col
+ * (forward.go:435-456: dt x dh cross product, hmul = subsample, zero pad),
+ * and their transposes used by the input-gradient GEMMs.
+ *
+ * Orientation: an operand is "k-contiguous" when its columns run along the
+ * GEMM reduction index (row-major A[M][K], or B stored [N][K]); otherwise its
+ * rows run along the reduction (A stored [K][M], B stored [K][N]).
+ */
+#ifndef KALDI_FP16_AMD_KF_OPS_H
+#define KALDI_FP16_AMD_KF_OPS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KF_MAX_PARTS 9
+#define KF_ZERO 0
+#define KF_CLAMP 1
+
+typedef struct {
+    const void *base;  /* fp16 */
+    long long ld;      /* elements between consecutive source rows */
+    int nrows, ncols;  /* logical shape of Op */
+    int kcontig;       /* 1: columns are the reduction index */
+    int nparts, part_width;
+    int T, hout, hsrc, hmul, hdiv, tpolicy;
+    int dt[KF_MAX_PARTS];
+    int dh[KF_MAX_PARTS];
+    int edge_t[KF_MAX_PARTS];
+    const void *edge_ptr[KF_MAX_PARTS];
+} KfOperand;
+
+/*
+ * Fused epilogue, applied per output element (m, n) to the fp32 accumulator:
+ *   v = alpha*acc (+ beta*out[m][n]) (+ bias[n])
+ *   if relu: mask_out bit (m*ldo+n) = v > 0; v = max(v, 0)
+ *   if scale: v = v*scale[n] + shift[n]          (frozen BatchNorm, folded)
+ *   if resid: v += resid_alpha * resid[m][n]     (TDNN-F bypass / grad bypass)
+ *   out[m][n] = rne_fp16(v)                       (when out != NULL)
+ *   if out2: out2[m][n] = rne_fp16(v * scale2[n] * bit(mask_in, m*ldo2+n))
+ * Masks are bit-packed in the linear element order of the tensor they describe
+ * (bit i of byte i/8), so producer and consumer may tile differently.
+ */
+typedef struct {
+    void *out;
+    long long ldo;
+    float alpha, beta;
+    const void *bias;      /* fp16 [N] or NULL */
+    int relu;
+    uint8_t *mask_out;     /* or NULL */
+    const float *scale;    /* fp32 [N] or NULL */
+    const float *shift;    /* fp32 [N] (required with scale) */
+    const void *resid;     /* fp16, or NULL */
+    long long ldr;
+    float resid_alpha;
+    void *out2;            /* fp16, or NULL */
+    long long ldo2;
+    const float *scale2;   /* fp32 [N] or NULL (= 1) */
+    const uint8_t *mask_in;/* or NULL (= all ones) */
+} KfEpilogue;
+
+/* current stream for every launch made by this library on the calling thread
+ * (NULL = legacy default stream, the reference's behaviour) */
+void kf_set_stream(void *hip_stream);
+void *kf_get_stream(void);
+
+/* C[M x N] = epilogue(A . B^T-style contraction over K) */
+int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
+                  const KfEpilogue *epi);
+
+/*
+ * Weight-gradient GEMM with the reduction split over workgroups:
+ *   dW[M x N] (fp32, leading dim ldw) (+)= sum_r A(r, m) * B(r, n)
+ * bias_grad[N] (fp32, optional) (+)= sum_r B(r, n).
+ * accumulate=0 overwrites, 1 adds. Deterministic (slab reduction, no atomics).
+ */
+int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW,
+                  long long ldw, float *bias_grad, int accumulate);
+
+/* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols */
+int kf_rows_sum(void *edge, const void *src, long long ld, int r0, int r1, int cols);
+
+/* ---- non-MFMA layer pieces (csrc/layers.hip) ---- */
+/* y[T x N] = x[T x K] . M[K x N], K <= 64, N % 8 == 0 (IDCT, forward.go:317-330) */
+int kf_small_gemm(const void *x, int ldx, const void *M, void *y, int ldy, int T, int K, int N);
+/* y = rne(x*scale[d] + shift[d]) on [rows x D] (frozen BatchNorm, folded) */
+int kf_bn_apply(const void *x, void *y, long long rows, int D, const float *scale,
+                const float *shift);
+/* conv-relu-batchnorm with one input filter (im2col K = noff), fused epilogue;
+ * y [(T*hout) x fout], mask bits in the same element order */
+int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
+                       const int *dh, const void *x, const void *W, const void *bias,
+                       const float *scale, const float *shift, void *y, uint8_t *mask);
+/* its weight / bias gradient (fp32, overwritten), deterministic */
+int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
+                     const int *dh, const void *x, const void *dz, float *dW, float *db);
+/* one-launch SGD over a flat parameter set: v = mom*v + g; w32 -= lr*v; w16 = rne(w32) */
+int kf_sgd_flat(float *w32, void *w16, const float *g, float *v, float lr, float mom,
+                long long n);
+int kf_f32_to_f16_flat(const float *src, void *dst, long long n);
+const char *kf_layers_last_error(void);
+
+/* optional HIP-event timing of every GEMM launch on the current stream
+ * (class 0 = kf_gemm_fused, 1 = kf_gemm_wgrad); collect sums since reset */
+void kf_prof_enable(int on);
+int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
+void kf_prof_reset(void);
+
+const char *kf_last_error(void);
+void kf_clear_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

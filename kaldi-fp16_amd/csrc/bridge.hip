@@ -1,0 +1,223 @@
+// bridge.hip — device / memory / transfer entry points (include/bridge.h).
+// Behaviour follows the reference's cpp/cuda/bridge.cu:38-334; device work is
+// issued on the library's current stream (kf_set_stream) and every call that
+// hands data back to the host synchronises, as the reference's blocking
+// cudaMemcpy calls do.
+#include "kf_common.h"
+#include "../../include/bridge.h"
+#include "../../include/kf_ops.h"
+
+KF_DECLARE_ERR(bridge)
+
+// ---------------------------------------------------------------------------
+// stream + workspace shared by all modules of the library
+// ---------------------------------------------------------------------------
+static __thread hipStream_t g_stream = nullptr;
+hipStream_t kf_stream() { return g_stream; }
+extern "C" void kf_set_stream(void *s) { g_stream = (hipStream_t)s; }
+extern "C" void *kf_get_stream(void) { return (void *)g_stream; }
+
+namespace {
+struct Slot {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+constexpr int kMaxDev = 16, kMaxSlot = 8;
+Slot g_ws[kMaxDev][kMaxSlot];
+}  // namespace
+
+void *kf_workspace(size_t bytes, int slot) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDev || slot < 0 || slot >= kMaxSlot) return nullptr;
+    Slot &s = g_ws[dev][slot];
+    if (s.bytes >= bytes && s.ptr) return s.ptr;
+    // growing a slot is an allocation point: never inside a captured region
+    if (s.ptr) {
+        hipStreamSynchronize(g_stream);
+        hipFree(s.ptr);
+        s.ptr = nullptr;
+        s.bytes = 0;
+    }
+    size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    if (hipMalloc(&s.ptr, want) != hipSuccess) {
+        s.ptr = nullptr;
+        return nullptr;
+    }
+    s.bytes = want;
+    return s.ptr;
+}
+
+__global__ void k_f16_to_f32(float *dst, const h16 *src, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) dst[i] = h2f(src[i]);
+}
+__global__ void k_f32_to_f16(h16 *dst, const float *src, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (; i < n; i += stride) dst[i] = f2h(src[i]);
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static int copy_sync(void *dst, const void *src, size_t bytes, hipMemcpyKind kind,
+                     const char *what, size_t count) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, g_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(g_stream);
+    if (e != hipSuccess) {
+        bridge_set_error("hipMemcpy %s (%zu): %s", what, count, hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+extern "C" {
+
+const char *bridge_last_error(void) { return bridge_err_.get(); }
+void bridge_clear_error(void) { bridge_err_.clear(); }
+
+int bridge_gpu_init(int device_id) {
+    hipError_t e = hipSetDevice(device_id);
+    if (e != hipSuccess) {
+        bridge_set_error("hipSetDevice(%d): %s", device_id, hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int bridge_gpu_get_free_memory(size_t *free_bytes, size_t *total_bytes) {
+    hipError_t e = hipMemGetInfo(free_bytes, total_bytes);
+    if (e != hipSuccess) {
+        bridge_set_error("hipMemGetInfo: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int bridge_gpu_sync(void) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        bridge_set_error("hipDeviceSynchronize: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+void *bridge_gpu_malloc(size_t bytes) {
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        bridge_set_error("hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+void bridge_gpu_free(void *ptr) {
+    if (ptr) hipFree(ptr);
+}
+
+void *bridge_host_alloc(size_t bytes) {
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        bridge_set_error("hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+        return nullptr;
+    }
+    return p;
+}
+
+void bridge_host_free(void *ptr) {
+    if (ptr) hipHostFree(ptr);
+}
+
+int bridge_transfer_fp16(void *dst_device, const uint16_t *src_host, size_t count) {
+    return copy_sync(dst_device, src_host, count * 2, hipMemcpyHostToDevice, "FP16 H2D", count);
+}
+int bridge_read_fp16(uint16_t *dst_host, const void *src_device, size_t count) {
+    return copy_sync(dst_host, src_device, count * 2, hipMemcpyDeviceToHost, "FP16 D2H", count);
+}
+int bridge_transfer_int32(void *dst_device, const int32_t *src_host, size_t count) {
+    return copy_sync(dst_device, src_host, count * 4, hipMemcpyHostToDevice, "int32 H2D", count);
+}
+int bridge_transfer_float32(void *dst_device, const float *src_host, size_t count) {
+    return copy_sync(dst_device, src_host, count * 4, hipMemcpyHostToDevice, "float32 H2D",
+                     count);
+}
+
+int bridge_batch_alloc(int total_frames, int feat_dim, int batch_size, int ivec_dim,
+                       int num_states, int num_arcs, GPUBatchPtrs *out) {
+    memset(out, 0, sizeof(*out));
+    out->features_bytes = align256((size_t)total_frames * feat_dim * 2);
+    out->ivectors_bytes = align256((size_t)batch_size * ivec_dim * 2);
+    out->csr_rowptr_bytes = align256((size_t)(num_states + 1) * 4);
+    out->csr_colidx_bytes = align256((size_t)num_arcs * 4);
+    out->csr_labels_bytes = align256((size_t)num_arcs * 4);
+    out->csr_weights_bytes = align256((size_t)num_arcs * 4);
+    out->total_bytes = out->features_bytes + out->ivectors_bytes + out->csr_rowptr_bytes +
+                       out->csr_colidx_bytes + out->csr_labels_bytes + out->csr_weights_bytes;
+    hipError_t e = hipMalloc(&out->d_buffer, out->total_bytes);
+    if (e != hipSuccess) {
+        bridge_set_error("hipMalloc combined (%zu bytes): %s", out->total_bytes,
+                         hipGetErrorString(e));
+        out->d_buffer = nullptr;
+        return -1;
+    }
+    char *b = (char *)out->d_buffer;
+    size_t off = 0;
+    out->d_features = b + off;
+    off += out->features_bytes;
+    out->d_ivectors = b + off;
+    off += out->ivectors_bytes;
+    out->d_csr_row_ptr = b + off;
+    off += out->csr_rowptr_bytes;
+    out->d_csr_col_idx = b + off;
+    off += out->csr_colidx_bytes;
+    out->d_csr_labels = b + off;
+    off += out->csr_labels_bytes;
+    out->d_csr_weights = b + off;
+    return 0;
+}
+
+int bridge_batch_transfer(const GPUBatchPtrs *ptrs, const void *host_buf, size_t total_bytes) {
+    return copy_sync(ptrs->d_buffer, host_buf, total_bytes, hipMemcpyHostToDevice, "batch",
+                     total_bytes);
+}
+
+void bridge_batch_free(GPUBatchPtrs *ptrs) {
+    if (ptrs && ptrs->d_buffer) {
+        hipFree(ptrs->d_buffer);
+        memset(ptrs, 0, sizeof(*ptrs));
+    }
+}
+
+void bridge_gpu_memset(void *ptr, int value, size_t bytes) {
+    hipMemsetAsync(ptr, value, bytes, g_stream);
+}
+
+int bridge_fp16_to_fp32_gpu(float *dst_device, const void *src_device, size_t count) {
+    if (count == 0) return 0;
+    k_f16_to_f32<<<kf_blocks(count, 256, 8192), 256, 0, g_stream>>>(dst_device,
+                                                                    (const h16 *)src_device, count);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        bridge_set_error("fp16_to_fp32 kernel: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+int bridge_fp32_to_fp16_gpu(void *dst_device, const float *src_device, size_t count) {
+    if (count == 0) return 0;
+    k_f32_to_f16<<<kf_blocks(count, 256, 8192), 256, 0, g_stream>>>((h16 *)dst_device,
+                                                                    src_device, count);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        bridge_set_error("fp32_to_fp16 kernel: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+}  // extern "C"

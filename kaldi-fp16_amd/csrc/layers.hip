@@ -1,0 +1,270 @@
+// layers.hip — the few CNN-TDNN pieces that are not MFMA-shaped:
+//   * IDCT (K = 40 dense, forward.go:317-330) — a register dot per output group;
+//   * the first conv layer, whose input has one filter so im2col K = 9
+//     (forward.go:418-524 with num-filters-in = 1): direct 9-tap kernel with the
+//     bias / ReLU / mask / BatchNorm epilogue fused, and its weight gradient as a
+//     deterministic two-pass reduction;
+//   * the flat multi-tensor SGD with fp32 master weights
+//     (backward_wrappers.cu:129-142 applied to every parameter in one launch).
+// All are HBM-bound; every lane moves 16-byte vectors.
+#include "kf_common.h"
+#include "../../include/kf_ops.h"
+
+KF_DECLARE_ERR(lay)
+
+static int lay_check(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        lay_set_error("%s: %s", what, hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+extern "C" const char *kf_layers_last_error(void) { return lay_err_.get(); }
+
+// y[t][j..j+7] = sum_k x[t][k] * M[k][j..j+7]; K <= 64, N % 8 == 0, M fp16 [K x N]
+__global__ void k_small_gemm(const h16 *x, int ldx, const h16 *Mw, h16 *y, int ldy, int T, int K,
+                             int N) {
+    __shared__ float sm[64 * 64];
+    for (int i = threadIdx.x; i < K * N; i += blockDim.x) sm[i] = h2f(Mw[i]);
+    __syncthreads();
+    const int groups = N / 8;
+    const long long total = (long long)T * groups;
+    for (long long it = (long long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+         it += (long long)gridDim.x * blockDim.x) {
+        const int t = (int)(it / groups), g = (int)(it - (long long)t * groups);
+        float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const h16 *xr = x + (long long)t * ldx;
+        for (int k = 0; k < K; ++k) {
+            const float xv = h2f(xr[k]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[e] += xv * sm[k * N + 8 * g + e];
+        }
+        half8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2h(acc[e]);
+        store_h8(y + (long long)t * ldy + 8 * g, o);
+    }
+}
+
+// first conv layer, one input filter: x [T x hin], out [(t*hout+h) x fout]
+struct ConvC1 {
+    int T, hin, hout, sub, fout, noff;
+    int dt[9], dh[9];
+};
+
+__global__ void k_conv_c1_fwd(ConvC1 c, const h16 *x, const h16 *W, const h16 *bias,
+                              const float *scale, const float *shift, h16 *y, uint8_t *mask) {
+    __shared__ float sw[9 * 256];
+    __shared__ float sb[256];
+    for (int i = threadIdx.x; i < c.noff * c.fout; i += blockDim.x) sw[i] = h2f(W[i]);
+    for (int i = threadIdx.x; i < c.fout; i += blockDim.x) sb[i] = bias ? h2f(bias[i]) : 0.f;
+    __syncthreads();
+    const int groups = c.fout / 8;
+    const long long total = (long long)c.T * c.hout * groups;
+    for (long long it = (long long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
+         it += (long long)gridDim.x * blockDim.x) {
+        const long long row = it / groups;
+        const int g = (int)(it - row * groups);
+        const int t = (int)(row / c.hout), h = (int)(row - (long long)t * c.hout);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = sb[8 * g + e];
+        for (int o = 0; o < c.noff; ++o) {
+            const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
+            if (ts < 0 || ts >= c.T || hs < 0 || hs >= c.hin) continue;
+            const float xv = h2f(x[(long long)ts * c.hin + hs]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += xv * sw[o * c.fout + 8 * g + e];
+        }
+        unsigned bits = 0;
+        half8 out;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float a = v[e];
+            if (a > 0.f) bits |= 1u << e;
+            else a = 0.f;
+            if (scale) a = fmaf(a, scale[8 * g + e], shift[8 * g + e]);
+            out[e] = f2h(a);
+        }
+        const long long idx = row * c.fout + 8 * g;
+        store_h8(y + idx, out);
+        if (mask) mask[idx >> 3] = (uint8_t)bits;
+    }
+}
+
+// partial dW / db of the 1-filter conv: each block reduces a contiguous range of
+// rows into slab[block][noff+1][fout] (row noff = bias), fixed order (deterministic)
+__global__ void k_conv_c1_wgrad(ConvC1 c, const h16 *x, const h16 *dz, float *slab,
+                                int rows_per_block) {
+    const int f = threadIdx.x % c.fout;
+    const int rg = threadIdx.x / c.fout, nrg = blockDim.x / c.fout;
+    const long long rows = (long long)c.T * c.hout;
+    const long long r0 = (long long)blockIdx.x * rows_per_block;
+    const long long r1 = min(rows, r0 + rows_per_block);
+    float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (long long r = r0 + rg; r < r1; r += nrg) {
+        const float g = h2f(dz[r * c.fout + f]);
+        const int t = (int)(r / c.hout), h = (int)(r - (long long)t * c.hout);
+#pragma unroll
+        for (int o = 0; o < 9; ++o) {
+            if (o >= c.noff) break;
+            const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
+            if (ts < 0 || ts >= c.T || hs < 0 || hs >= c.hin) continue;
+            acc[o] += g * h2f(x[(long long)ts * c.hin + hs]);
+        }
+        acc[9] += g;
+    }
+    __shared__ float red[256 * 10];
+#pragma unroll
+    for (int o = 0; o < 10; ++o) red[o * 256 + threadIdx.x] = acc[o];
+    __syncthreads();
+    if (rg == 0) {
+        float *out = slab + (long long)blockIdx.x * (c.noff + 1) * c.fout;
+        for (int o = 0; o <= c.noff; ++o) {
+            const int src = o == c.noff ? 9 : o;
+            float s = 0.f;
+            for (int k = 0; k < nrg; ++k) s += red[src * 256 + k * c.fout + f];
+            out[o * c.fout + f] = s;
+        }
+    }
+}
+
+__global__ void k_conv_c1_reduce(const float *slab, int nblk, int n, float *dW, float *db,
+                                 int wcount) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += slab[(long long)b * n + i];
+    if (i < wcount) dW[i] = s;
+    else if (db) db[i - wcount] = s;
+}
+
+// flat SGD with momentum and fp32 master weights; fp32 gradient
+__global__ void k_sgd_flat(float *w32, h16 *w16, const float *g, float *v, float lr, float mom,
+                           long long n) {
+    const long long n4 = n / 4;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * blockDim.x) {
+        float4v gv = reinterpret_cast<const float4v *>(g)[i];
+        float4v vv = reinterpret_cast<float4v *>(v)[i];
+        float4v wv = reinterpret_cast<float4v *>(w32)[i];
+        half4 hv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            vv[e] = mom * vv[e] + gv[e];
+            wv[e] = wv[e] - lr * vv[e];
+            hv[e] = f2h(wv[e]);
+        }
+        reinterpret_cast<float4v *>(v)[i] = vv;
+        reinterpret_cast<float4v *>(w32)[i] = wv;
+        reinterpret_cast<half4 *>(w16)[i] = hv;
+    }
+    for (long long i = n4 * 4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const float vv = mom * v[i] + g[i];
+        v[i] = vv;
+        w32[i] -= lr * vv;
+        w16[i] = f2h(w32[i]);
+    }
+}
+
+// fp16 <- fp32 for a flat parameter set (master -> working copy)
+__global__ void k_f32_to_f16_flat(const float *s, h16 *d, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        d[i] = f2h(s[i]);
+}
+
+// fused frozen BatchNorm on a [rows x D] fp16 tensor (y = x*scale + shift)
+__global__ void k_bn_apply(const h16 *x, h16 *y, long long rows, int D, const float *scale,
+                           const float *shift) {
+    const long long total = rows * D;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int d = (int)(i % D);
+        y[i] = f2h(fmaf(h2f(x[i]), scale[d], shift[d]));
+    }
+}
+
+extern "C" {
+
+int kf_small_gemm(const void *x, int ldx, const void *Mw, void *y, int ldy, int T, int K, int N) {
+    if (K > 64 || N > 64 || N % 8) {
+        lay_set_error("small_gemm: K=%d N=%d unsupported", K, N);
+        return -1;
+    }
+    if (T <= 0) return 0;
+    k_small_gemm<<<kf_blocks((long long)T * (N / 8), 256, 4096), 256, 0, kf_stream()>>>(
+        (const h16 *)x, ldx, (const h16 *)Mw, (h16 *)y, ldy, T, K, N);
+    return lay_check("small_gemm");
+}
+
+int kf_bn_apply(const void *x, void *y, long long rows, int D, const float *scale,
+                const float *shift) {
+    if (rows <= 0) return 0;
+    k_bn_apply<<<kf_blocks(rows * D, 256, 8192), 256, 0, kf_stream()>>>(
+        (const h16 *)x, (h16 *)y, rows, D, scale, shift);
+    return lay_check("bn_apply");
+}
+
+int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
+                       const int *dh, const void *x, const void *W, const void *bias,
+                       const float *scale, const float *shift, void *y, uint8_t *mask) {
+    if (noff > 9 || fout % 8 || fout > 256) {
+        lay_set_error("conv_c1_forward: noff=%d fout=%d unsupported", noff, fout);
+        return -1;
+    }
+    ConvC1 c{T, hin, hout, sub, fout, noff, {0}, {0}};
+    for (int i = 0; i < noff; ++i) {
+        c.dt[i] = dt[i];
+        c.dh[i] = dh[i];
+    }
+    const long long total = (long long)T * hout * (fout / 8);
+    k_conv_c1_fwd<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
+        c, (const h16 *)x, (const h16 *)W, (const h16 *)bias, scale, shift, (h16 *)y, mask);
+    return lay_check("conv_c1_forward");
+}
+
+int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
+                     const int *dh, const void *x, const void *dz, float *dW, float *db) {
+    if (noff > 9 || fout > 256 || 256 % fout) {
+        lay_set_error("conv_c1_wgrad: noff=%d fout=%d unsupported", noff, fout);
+        return -1;
+    }
+    ConvC1 c{T, hin, hout, sub, fout, noff, {0}, {0}};
+    for (int i = 0; i < noff; ++i) {
+        c.dt[i] = dt[i];
+        c.dh[i] = dh[i];
+    }
+    const long long rows = (long long)T * hout;
+    int nblk = 1024;
+    int rpb = (int)((rows + nblk - 1) / nblk);
+    if (rpb < 64) rpb = 64;
+    nblk = (int)((rows + rpb - 1) / rpb);
+    const int n = (noff + 1) * fout;
+    float *slab = (float *)kf_workspace((size_t)nblk * n * 4, 2);
+    if (!slab) {
+        lay_set_error("conv_c1_wgrad: workspace");
+        return -1;
+    }
+    k_conv_c1_wgrad<<<nblk, 256, 0, kf_stream()>>>(c, (const h16 *)x, (const h16 *)dz, slab, rpb);
+    k_conv_c1_reduce<<<(n + 255) / 256, 256, 0, kf_stream()>>>(slab, nblk, n, dW, db, noff * fout);
+    return lay_check("conv_c1_wgrad");
+}
+
+int kf_sgd_flat(float *w32, void *w16, const float *g, float *v, float lr, float mom,
+                long long n) {
+    if (n <= 0) return 0;
+    k_sgd_flat<<<kf_blocks(n / 4 + 1, 256, 8192), 256, 0, kf_stream()>>>(w32, (h16 *)w16, g, v, lr,
+                                                                        mom, n);
+    return lay_check("sgd_flat");
+}
+
+int kf_f32_to_f16_flat(const float *src, void *dst, long long n) {
+    if (n <= 0) return 0;
+    k_f32_to_f16_flat<<<kf_blocks(n, 256, 8192), 256, 0, kf_stream()>>>(src, (h16 *)dst, n);
+    return lay_check("f32_to_f16_flat");
+}
+
+}  // extern "C"

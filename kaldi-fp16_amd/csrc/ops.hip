@@ -1,0 +1,414 @@
+// ops.hip — reference ABI compute ops (include/ops.h) on gfx950.
+// Semantics follow cpp/cuda/ops.cu:26-643 and cpp/cuda/backward_wrappers.cu:41-291:
+// fp16 in, fp32 math, one round-to-nearest-even fp16 store. Kernels are
+// grid-stride loops over 8-element (16-byte) vectors with a scalar tail, so
+// they run at HBM rate for any count (the reference uses one thread per
+// element and 2-byte accesses).
+#include "kf_common.h"
+#include "../../include/ops.h"
+#include "../../include/kf_ops.h"
+
+KF_DECLARE_ERR(ops)
+
+int kf_ops_gemm_impl(int M, int N, int K, float alpha, const void *A, int lda, const void *B,
+                     int ldb, float beta, void *C, int ldc, char *err, size_t errlen);
+
+static int ops_check(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        ops_set_error("%s: %s", what, hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+static inline bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+// Generic element-wise driver: f(i, ...) applied per element; vector path when
+// all pointers are 16-byte aligned.
+#define GRID_STRIDE(i, n)                                                          \
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (n); \
+         i += (long long)gridDim.x * blockDim.x)
+
+// ------------------------------- activations -------------------------------
+enum { ACT_RELU, ACT_SIGMOID, ACT_TANH, ACT_CLIPPED };
+
+__device__ __forceinline__ float act_apply(int kind, float x, float ceil_) {
+    switch (kind) {
+        case ACT_RELU: return x < 0.f ? 0.f : x;
+        case ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+        case ACT_TANH: return tanhf(x);
+        default: return fmaxf(0.f, fminf(x, ceil_));
+    }
+}
+
+__global__ void k_act(h16 *d, long long n, int kind, float ceil_, int vec) {
+    if (vec) {
+        GRID_STRIDE(i, n / 8) {
+            half8 v = load_h8(d + 8 * i);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = f2h(act_apply(kind, (float)v[e], ceil_));
+            store_h8(d + 8 * i, v);
+        }
+        GRID_STRIDE(i, n % 8) {
+            long long j = n / 8 * 8 + i;
+            d[j] = f2h(act_apply(kind, h2f(d[j]), ceil_));
+        }
+    } else {
+        GRID_STRIDE(i, n) d[i] = f2h(act_apply(kind, h2f(d[i]), ceil_));
+    }
+}
+
+static int run_act(void *data, int count, int kind, float c, const char *name) {
+    if (count < 0) {
+        ops_set_error("%s: negative count", name);
+        return -1;
+    }
+    if (count == 0) return 0;
+    k_act<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
+        (h16 *)data, count, kind, c, aligned16(data));
+    return ops_check(name);
+}
+
+// ------------------------------- softmax -----------------------------------
+// one 256-thread block per row; true max via wave/block reduction
+__device__ __forceinline__ float block_reduce(float v, bool is_max, float *sh) {
+    for (int o = 32; o > 0; o >>= 1) {
+        float w = __shfl_xor(v, o);
+        v = is_max ? fmaxf(v, w) : v + w;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) sh[wid] = v;
+    __syncthreads();
+    const int nw = blockDim.x >> 6;
+    float r = sh[0];
+    for (int i = 1; i < nw; ++i) r = is_max ? fmaxf(r, sh[i]) : r + sh[i];
+    return r;
+}
+
+__global__ void k_softmax(h16 *data, int cols, int logmode) {
+    __shared__ float sh[16];
+    h16 *row = data + (long long)blockIdx.x * cols;
+    float mx = -INFINITY;
+    for (int j = threadIdx.x; j < cols; j += blockDim.x) mx = fmaxf(mx, h2f(row[j]));
+    mx = block_reduce(mx, true, sh);
+    float s = 0.f;
+    for (int j = threadIdx.x; j < cols; j += blockDim.x) s += expf(h2f(row[j]) - mx);
+    s = block_reduce(s, false, sh);
+    if (logmode) {
+        const float lse = mx + logf(s);
+        for (int j = threadIdx.x; j < cols; j += blockDim.x) row[j] = f2h(h2f(row[j]) - lse);
+    } else {
+        const float inv = 1.f / s;
+        for (int j = threadIdx.x; j < cols; j += blockDim.x)
+            row[j] = f2h(expf(h2f(row[j]) - mx) * inv);
+    }
+}
+
+// ------------------------------- batchnorm ---------------------------------
+__global__ void k_bn(h16 *x, long long total, int D, const float *mean, const float *var,
+                     const float *gamma, const float *beta, float target_rms, float eps,
+                     int rms) {
+    GRID_STRIDE(i, total) {
+        const int d = (int)(i % D);
+        const float norm = (h2f(x[i]) - mean[d]) / sqrtf(var[d] + eps);
+        x[i] = f2h(rms ? norm * target_rms : gamma[d] * norm + beta[d]);
+    }
+}
+
+__global__ void k_bn_bwd(const h16 *go, h16 *gi, const float *gamma, const float *var,
+                         float eps, long long total, int cols) {
+    GRID_STRIDE(i, total) {
+        const int d = (int)(i % cols);
+        gi[i] = f2h(h2f(go[i]) * (gamma[d] / sqrtf(var[d] + eps)));
+    }
+}
+
+// ------------------------------- element-wise ------------------------------
+__global__ void k_add_scaled(h16 *dst, const h16 *src, long long n, float a, float b, int vec) {
+    if (vec) {
+        GRID_STRIDE(i, n / 8) {
+            half8 d = load_h8(dst + 8 * i), s = load_h8(src + 8 * i);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d[e] = f2h(a * (float)s[e] + b * (float)d[e]);
+            store_h8(dst + 8 * i, d);
+        }
+        GRID_STRIDE(i, n % 8) {
+            long long j = n / 8 * 8 + i;
+            dst[j] = f2h(a * h2f(src[j]) + b * h2f(dst[j]));
+        }
+    } else {
+        GRID_STRIDE(i, n) dst[i] = f2h(a * h2f(src[i]) + b * h2f(dst[i]));
+    }
+}
+
+__global__ void k_fill(h16 *dst, long long n, float v) {
+    const h16 hv = f2h(v);
+    GRID_STRIDE(i, n) dst[i] = hv;
+}
+
+__global__ void k_concat_cols(h16 *dst, int T, int dst_cols, const h16 *src, int src_cols,
+                              int off) {
+    GRID_STRIDE(i, (long long)T * src_cols) {
+        const long long t = i / src_cols, c = i - t * src_cols;
+        dst[t * dst_cols + off + c] = src[i];
+    }
+}
+
+__global__ void k_slice_cols(h16 *dst, int T, int dst_cols, const h16 *src, int src_cols,
+                             int off) {
+    GRID_STRIDE(i, (long long)T * dst_cols) {
+        const long long t = i / dst_cols, c = i - t * dst_cols;
+        dst[i] = src[t * src_cols + off + c];
+    }
+}
+
+__global__ void k_combine_fm(h16 *out, const h16 *in, int T, int total, int H, int nf1,
+                             int nf2) {
+    GRID_STRIDE(i, (long long)T * total) {
+        const long long t = i / total;
+        const int d = (int)(i - t * total);
+        const int nf = nf1 + nf2, h = d / nf, f = d - h * nf;
+        const long long src = f < nf1 ? t * total + (long long)h * nf1 + f
+                                      : t * total + (long long)H * nf1 + (long long)h * nf2 + (f - nf1);
+        out[i] = in[src];
+    }
+}
+
+__global__ void k_subsample_rows(h16 *dst, const h16 *src, int out_rows, int cols, int stride,
+                                 int off) {
+    GRID_STRIDE(i, (long long)out_rows * cols) {
+        const long long r = i / cols, c = i - r * cols;
+        dst[i] = src[(off + r * stride) * cols + c];
+    }
+}
+
+__global__ void k_act_bwd(const h16 *x, h16 *g, long long n, int kind) {
+    GRID_STRIDE(i, n) {
+        const float xv = h2f(x[i]), gv = h2f(g[i]);
+        float r;
+        if (kind == ACT_RELU) r = xv > 0.f ? gv : 0.f;
+        else if (kind == ACT_SIGMOID) r = gv * xv * (1.f - xv);
+        else r = gv * (1.f - xv * xv);
+        g[i] = f2h(r);
+    }
+}
+
+// tiled transpose through LDS (dst[N x M] = src[M x N]^T), coalesced both ways
+__global__ void k_transpose(const h16 *src, h16 *dst, int M, int N) {
+    __shared__ h16 tile[64][65];
+    const int bx = blockIdx.x * 64, by = blockIdx.y * 64;
+    for (int r = threadIdx.y; r < 64; r += blockDim.y) {
+        const int m = by + r, n = bx + threadIdx.x;
+        if (m < M && n < N) tile[r][threadIdx.x] = src[(long long)m * N + n];
+    }
+    __syncthreads();
+    for (int r = threadIdx.y; r < 64; r += blockDim.y) {
+        const int n = bx + r, m = by + threadIdx.x;
+        if (m < M && n < N) dst[(long long)n * M + m] = tile[threadIdx.x][r];
+    }
+}
+
+__global__ void k_h2f(const h16 *s, float *d, long long n) { GRID_STRIDE(i, n) d[i] = h2f(s[i]); }
+
+__global__ void k_sgd(float *w32, h16 *w16, const h16 *g, float *v, float lr, float mom,
+                      long long n) {
+    GRID_STRIDE(i, n) {
+        const float vv = mom * v[i] + h2f(g[i]);
+        v[i] = vv;
+        const float w = w32[i] - lr * vv;
+        w32[i] = w;
+        w16[i] = f2h(w);
+    }
+}
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+const char *ops_last_error(void) { return ops_err_.get(); }
+void ops_clear_error(void) { ops_err_.clear(); }
+
+int ops_gemm(void *handle, int M, int N, int K, float alpha, const void *A, int lda,
+             const void *B, int ldb, float beta, void *C, int ldc) {
+    (void)handle;
+    char err[512];
+    if (kf_ops_gemm_impl(M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, err, sizeof err)) {
+        ops_set_error("%s", err);
+        return -1;
+    }
+    return 0;
+}
+
+int ops_gemm_strided(void *handle, int M, int N, int K, float alpha, const void *A, int lda,
+                     int64_t strideA, const void *B, int ldb, int64_t strideB, float beta,
+                     void *C, int ldc, int64_t strideC, int batch_count) {
+    (void)handle;
+    char err[512];
+    for (int b = 0; b < batch_count; ++b) {
+        if (kf_ops_gemm_impl(M, N, K, alpha, (const h16 *)A + b * strideA, lda,
+                             (const h16 *)B + b * strideB, ldb, beta, (h16 *)C + b * strideC,
+                             ldc, err, sizeof err)) {
+            ops_set_error("strided batch %d: %s", b, err);
+            return -1;
+        }
+    }
+    return 0;
+}
+
+int ops_relu(void *data, int count) { return run_act(data, count, ACT_RELU, 0.f, "relu kernel"); }
+int ops_sigmoid(void *data, int count) { return run_act(data, count, ACT_SIGMOID, 0.f, "sigmoid"); }
+int ops_tanh_act(void *data, int count) { return run_act(data, count, ACT_TANH, 0.f, "tanh"); }
+int ops_clipped_relu(void *data, int count, float ceiling) {
+    return run_act(data, count, ACT_CLIPPED, ceiling, "clipped_relu");
+}
+
+int ops_softmax(void *data, int rows, int cols) {
+    if (rows <= 0 || cols <= 0) return 0;
+    k_softmax<<<rows, 256, 0, kf_stream()>>>((h16 *)data, cols, 0);
+    return ops_check("softmax kernel");
+}
+int ops_log_softmax(void *data, int rows, int cols) {
+    if (rows <= 0 || cols <= 0) return 0;
+    k_softmax<<<rows, 256, 0, kf_stream()>>>((h16 *)data, cols, 1);
+    return ops_check("log_softmax kernel");
+}
+
+int ops_batchnorm_forward(void *x, int T, int D, const float *mean, const float *var,
+                          const float *gamma, const float *beta, float epsilon) {
+    long long total = (long long)T * D;
+    if (total <= 0) return 0;
+    k_bn<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>((h16 *)x, total, D, mean, var,
+                                                              gamma, beta, 1.f, epsilon, 0);
+    return ops_check("batchnorm kernel");
+}
+int ops_batchnorm_forward_rms(void *x, int T, int D, const float *mean, const float *var,
+                              float target_rms, float epsilon) {
+    long long total = (long long)T * D;
+    if (total <= 0) return 0;
+    k_bn<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
+        (h16 *)x, total, D, mean, var, nullptr, nullptr, target_rms, epsilon, 1);
+    return ops_check("batchnorm rms kernel");
+}
+
+int ops_add_scaled(void *dst, const void *src, int count, float alpha, float beta) {
+    if (count <= 0) return 0;
+    k_add_scaled<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
+        (h16 *)dst, (const h16 *)src, count, alpha, beta, aligned16(dst) && aligned16(src));
+    return ops_check("add_scaled");
+}
+int ops_add(void *dst, const void *src, int count) {
+    return ops_add_scaled(dst, src, count, 1.f, 1.f);
+}
+int ops_copy(void *dst, const void *src, int count) {
+    if (count <= 0) return 0;
+    hipError_t e = hipMemcpyAsync(dst, src, (size_t)count * 2, hipMemcpyDeviceToDevice, kf_stream());
+    if (e != hipSuccess) {
+        ops_set_error("copy: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+int ops_fill(void *dst, int count, float val) {
+    if (count <= 0) return 0;
+    k_fill<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((h16 *)dst, count, val);
+    return ops_check("fill");
+}
+
+int ops_concat_cols(void *dst, int T, int dst_cols, const void *src, int src_cols,
+                    int dst_col_offset) {
+    if ((long long)T * src_cols <= 0) return 0;
+    if (dst_col_offset < 0 || dst_col_offset + src_cols > dst_cols) {
+        ops_set_error("concat_cols: offset %d + %d > %d", dst_col_offset, src_cols, dst_cols);
+        return -1;
+    }
+    k_concat_cols<<<kf_blocks((long long)T * src_cols, 256, 8192), 256, 0, kf_stream()>>>(
+        (h16 *)dst, T, dst_cols, (const h16 *)src, src_cols, dst_col_offset);
+    return ops_check("concat_cols");
+}
+int ops_slice_cols(const void *src, int T, int src_cols, void *dst, int dst_cols,
+                   int src_col_offset) {
+    if ((long long)T * dst_cols <= 0) return 0;
+    if (src_col_offset < 0 || src_col_offset + dst_cols > src_cols) {
+        ops_set_error("slice_cols: offset %d + %d > %d", src_col_offset, dst_cols, src_cols);
+        return -1;
+    }
+    k_slice_cols<<<kf_blocks((long long)T * dst_cols, 256, 8192), 256, 0, kf_stream()>>>(
+        (h16 *)dst, T, dst_cols, (const h16 *)src, src_cols, src_col_offset);
+    return ops_check("slice_cols");
+}
+
+int ops_combine_feature_maps(void *data, int T, int total_dim, int height, int nf1, int nf2) {
+    const long long total = (long long)T * total_dim;
+    if (total <= 0) return 0;
+    if ((long long)height * (nf1 + nf2) != total_dim) {
+        ops_set_error("combine_feature_maps: height*(nf1+nf2)=%d != %d", height * (nf1 + nf2),
+                      total_dim);
+        return -1;
+    }
+    void *tmp = kf_workspace(total * 2, 1);
+    if (!tmp) {
+        ops_set_error("combine alloc: out of memory");
+        return -1;
+    }
+    hipMemcpyAsync(tmp, data, total * 2, hipMemcpyDeviceToDevice, kf_stream());
+    k_combine_fm<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
+        (h16 *)data, (const h16 *)tmp, T, total_dim, height, nf1, nf2);
+    return ops_check("combine_feature_maps");
+}
+
+void ops_subsample_rows(void *dst, const void *src, int in_rows, int cols, int stride,
+                        int row_offset) {
+    if (stride <= 0) return;
+    const int out_rows = (in_rows - row_offset + stride - 1) / stride;
+    if (out_rows <= 0 || cols <= 0) return;
+    k_subsample_rows<<<kf_blocks((long long)out_rows * cols, 256, 8192), 256, 0, kf_stream()>>>(
+        (h16 *)dst, (const h16 *)src, out_rows, cols, stride, row_offset);
+}
+
+int ops_relu_backward(const void *x, void *grad, int count) {
+    if (count <= 0) return 0;
+    k_act_bwd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)x, (h16 *)grad,
+                                                                    count, ACT_RELU);
+    return ops_check("relu_backward");
+}
+int ops_sigmoid_backward(const void *out, void *grad, int count) {
+    if (count <= 0) return 0;
+    k_act_bwd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>(
+        (const h16 *)out, (h16 *)grad, count, ACT_SIGMOID);
+    return ops_check("sigmoid_backward");
+}
+int ops_tanh_backward(const void *out, void *grad, int count) {
+    if (count <= 0) return 0;
+    k_act_bwd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)out,
+                                                                    (h16 *)grad, count, ACT_TANH);
+    return ops_check("tanh_backward");
+}
+int ops_transpose(const void *src, void *dst, int M, int N) {
+    if (M <= 0 || N <= 0) return 0;
+    dim3 grid((N + 63) / 64, (M + 63) / 64);
+    k_transpose<<<grid, dim3(64, 4), 0, kf_stream()>>>((const h16 *)src, (h16 *)dst, M, N);
+    return ops_check("transpose");
+}
+int ops_batchnorm_backward(const void *grad_out, void *grad_in, const float *gamma,
+                           const float *variance, float eps, int rows, int cols) {
+    const long long total = (long long)rows * cols;
+    if (total <= 0) return 0;
+    k_bn_bwd<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
+        (const h16 *)grad_out, (h16 *)grad_in, gamma, variance, eps, total, cols);
+    return ops_check("batchnorm_backward");
+}
+int ops_fp16_to_fp32(const void *src, float *dst, int count) {
+    if (count <= 0) return 0;
+    k_h2f<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)src, dst, count);
+    return ops_check("fp16_to_fp32");
+}
+int ops_sgd_update(float *w_fp32, void *w_fp16, const void *grad_fp16, float *velocity,
+                   float lr, float momentum, int count) {
+    if (count <= 0) return 0;
+    k_sgd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>(
+        w_fp32, (h16 *)w_fp16, (const h16 *)grad_fp16, velocity, lr, momentum, count);
+    return ops_check("sgd_update");
+}
+
+}  // extern "C"

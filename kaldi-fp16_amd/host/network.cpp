@@ -1,0 +1,1008 @@
+// network.cpp — Network / backward / SGD of the C++ host layer.
+//
+// Restates internal/nnet/forward.go (Network.Forward and the per-layer
+// forward functions), internal/nnet/network_backward.go (Network.Backward) and
+// internal/gpu/optimize.go (SGDOptimizer) on top of the MI355X C-ABI:
+//   * every dense product is one kf_gemm_fused / kf_gemm_wgrad launch whose
+//     operand addressing does the TDNN splice (forward.go:699-790) and the conv
+//     im2col (forward.go:435-456) implicitly, with bias / ReLU / BatchNorm /
+//     bypass fused into the epilogue;
+//   * backward is the exact gradient of that forward (the reference's
+//     backwardTDNNF / backwardPrefinal are not);
+//   * all trainable parameters live in one flat fp32 master / fp16 working /
+//     fp32 gradient / fp32 velocity allocation, so the optimiser is one launch
+//     and the data-parallel gradient exchange is one contiguous buffer.
+// Memory comes from the bridge_* ABI, as the Go layer does (internal/gpu/tensor.go).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+
+#include "nnet_host.h"
+
+using kf::Layer;
+using kf::LayerType;
+
+static __thread char g_nnet_err[1024];
+static void set_err(const std::string &s) { snprintf(g_nnet_err, sizeof g_nnet_err, "%s", s.c_str()); }
+extern "C" const char *nnet_last_error(void) { return g_nnet_err[0] ? g_nnet_err : nullptr; }
+
+namespace {
+
+struct ParamRef {
+    std::string name;
+    int rows, cols;
+    long long off;
+};
+
+struct NetLayer {
+    Layer L;
+    int input = -1;  // index into layers, -1 = network input (features)
+    int pW = -1, pb = -1, pW2 = -1, pb2 = -1;
+    std::vector<int> dt, dh;  // conv: cross product of offsets (Kaldi)
+    float *bn_scale = nullptr, *bn_shift = nullptr;    // device, expanded to out width
+    float *bn2_scale = nullptr, *bn2_shift = nullptr;  // prefinal small BN
+    std::vector<float> hbn[4], hbn2[4];                // host mean,var,gamma,beta
+    float bn_eps = 1e-3f, bn_rms = 1.f, bn2_eps = 1e-3f, bn2_rms = 1.f;
+    bool has_bn2 = false;
+    void *act = nullptr;      // fp16 [maxT x out_dim] (or alias of the input for spec-augment)
+    bool act_alias = false;
+    uint8_t *mask = nullptr;  // relu bits
+    void *aux = nullptr;      // tdnnf bottleneck / prefinal big
+    void *idct = nullptr;     // fp16 [D x D]
+    bool bypass = false;
+    bool needs_dx = false;
+};
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+KfOperand op_base(const void *p, long long ld, int rows, int cols, int kcontig) {
+    KfOperand d;
+    memset(&d, 0, sizeof d);
+    d.base = p;
+    d.ld = ld;
+    d.nrows = rows;
+    d.ncols = cols;
+    d.kcontig = kcontig;
+    d.nparts = 1;
+    d.part_width = cols;
+    d.T = rows;
+    d.hout = 1;
+    d.hsrc = 1;
+    d.hmul = 0;
+    d.hdiv = 1;
+    d.tpolicy = KF_ZERO;
+    for (int i = 0; i < KF_MAX_PARTS; ++i) d.edge_t[i] = -1;
+    return d;
+}
+// [x(t+dt0) | x(t+dt1)] over T rows of width d (forward.go:699-790)
+KfOperand op_splice(const void *p, int T, int d, int dt0, int dt1, int policy, int kcontig) {
+    KfOperand o = op_base(p, d, T, 2 * d, kcontig);
+    o.nparts = 2;
+    o.part_width = d;
+    o.dt[0] = dt0;
+    o.dt[1] = dt1;
+    o.tpolicy = policy;
+    return o;
+}
+// im2col of a conv layer input [T x hin*fin] -> rows (t,h) < T*hout, cols (o,f)
+KfOperand op_im2col(const NetLayer &nl, const void *x, int T, int kcontig) {
+    const Layer &L = nl.L;
+    const int noff = (int)nl.dt.size();
+    KfOperand o = op_base(x, (long long)L.hin * L.fin, T * L.hout, noff * L.fin, kcontig);
+    o.nparts = noff;
+    o.part_width = L.fin;
+    o.T = T;
+    o.hout = L.hout;
+    o.hsrc = L.hin;
+    o.hmul = L.hsub;
+    o.hdiv = 1;
+    o.tpolicy = KF_ZERO;
+    for (int i = 0; i < noff; ++i) {
+        o.dt[i] = nl.dt[i];
+        o.dh[i] = nl.dh[i];
+    }
+    return o;
+}
+// transpose-conv gather of dz [(t,h) x fout]: rows (t',h') < T*hin, cols (o,n)
+KfOperand op_col2im(const NetLayer &nl, const void *dz, int T) {
+    const Layer &L = nl.L;
+    const int noff = (int)nl.dt.size();
+    KfOperand o = op_base(dz, (long long)L.hout * L.fout, T * L.hin, noff * L.fout, 1);
+    o.nparts = noff;
+    o.part_width = L.fout;
+    o.T = T;
+    o.hout = L.hin;
+    o.hsrc = L.hout;
+    o.hmul = 1;
+    o.hdiv = L.hsub;
+    o.tpolicy = KF_ZERO;
+    for (int i = 0; i < noff; ++i) {
+        o.dt[i] = -nl.dt[i];
+        o.dh[i] = -nl.dh[i];
+    }
+    return o;
+}
+// weights W[nparts*rows x width] read as B'[j][(p, n)] = W[p*rows + j][n]
+KfOperand op_wrows(const void *W, int nparts, int rows, int width) {
+    KfOperand o = op_base(W, width, rows, nparts * width, 1);
+    o.nparts = nparts;
+    o.part_width = width;
+    o.T = nparts * rows;
+    for (int p = 0; p < nparts; ++p) o.dt[p] = p * rows;
+    return o;
+}
+KfEpilogue epi0() {
+    KfEpilogue e;
+    memset(&e, 0, sizeof e);
+    e.alpha = 1.f;
+    return e;
+}
+
+}  // namespace
+
+struct KfNet {
+    std::vector<Layer> all;
+    std::vector<NetLayer> layers;
+    int feat_dim = 0, max_T = 0, T = 0;
+    const void *features = nullptr;
+    long long nparams = 0;
+    std::vector<ParamRef> params;
+    float *master = nullptr, *grad = nullptr, *vel = nullptr;
+    void *w16 = nullptr;
+    void *dz[2] = {nullptr, nullptr}, *g[2] = {nullptr, nullptr};
+    void *dbott = nullptr, *edge = nullptr;
+    size_t edge_half = 0;
+    std::vector<void *> allocs;
+
+    void *dalloc(size_t bytes) {
+        void *p = bridge_gpu_malloc(bytes ? bytes : 16);
+        if (p) allocs.push_back(p);
+        return p;
+    }
+    ~KfNet() {
+        for (void *p : allocs) bridge_gpu_free(p);
+    }
+};
+
+namespace {
+
+inline void *wptr(KfNet *net, int pi) {
+    return pi < 0 ? nullptr : (char *)net->w16 + net->params[pi].off * 2;
+}
+inline float *gptr(KfNet *net, int pi) { return pi < 0 ? nullptr : net->grad + net->params[pi].off; }
+
+bool ck(int rc, const char *what) {
+    if (rc != 0) {
+        const char *e = kf_last_error();
+        if (!e) e = kf_layers_last_error();
+        if (!e) e = ops_last_error();
+        set_err(std::string(what) + ": " + (e ? e : "failed"));
+        return false;
+    }
+    return true;
+}
+
+// makeIDCTMatrix, forward.go:1190-1210
+std::vector<float> idct_matrix(int dim, double lifter) {
+    std::vector<float> m((size_t)dim * dim);
+    for (int i = 0; i < dim; ++i)
+        for (int j = 0; j < dim; ++j) {
+            double v = cos(M_PI * j * (i + 0.5) / dim);
+            v *= j == 0 ? sqrt(1.0 / dim) : sqrt(2.0 / dim);
+            if (lifter > 0 && j > 0) v *= 1.0 + (lifter / 2.0) * sin(M_PI * j / lifter);
+            m[(size_t)i * dim + j] = (float)v;
+        }
+    return m;
+}
+
+// truncating fp32 -> fp16, internal/gpu/tensor.go:158-173 (weights enter this way)
+uint16_t f32_to_f16_trunc(float f) {
+    uint32_t bits;
+    memcpy(&bits, &f, 4);
+    uint16_t sign = (uint16_t)((bits >> 16) & 0x8000u);
+    int exp = (int)((bits >> 23) & 0xFF) - 127;
+    uint32_t frac = bits & 0x7FFFFFu;
+    if (exp > 15) return sign | 0x7C00u;
+    if (exp < -14) return sign;
+    return (uint16_t)(sign | (uint16_t)((exp + 15) << 10) | (uint16_t)(frac >> 13));
+}
+float f16_to_f32(uint16_t h) {
+    uint32_t sign = (uint32_t)(h & 0x8000u) << 16, exp = (h >> 10) & 0x1Fu, frac = h & 0x3FFu;
+    uint32_t bits;
+    if (exp == 0) {
+        if (frac == 0) bits = sign;
+        else {
+            exp = 1;
+            while (!(frac & 0x400u)) {
+                frac <<= 1;
+                exp--;
+            }
+            frac &= 0x3FFu;
+            bits = sign | ((uint32_t)(127 - 15 + (int)exp) << 23) | (frac << 13);
+        }
+    } else if (exp == 31) {
+        bits = sign | 0x7F800000u | (frac << 13);
+    } else {
+        bits = sign | ((exp - 15 + 127) << 23) | (frac << 13);
+    }
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+
+int add_param(KfNet *net, const std::string &name, int rows, int cols) {
+    ParamRef p{name, rows, cols, net->nparams};
+    net->params.push_back(p);
+    net->nparams += (long long)align_up((size_t)rows * cols, 64);
+    return (int)net->params.size() - 1;
+}
+
+// fold frozen BN into per-column scale/shift, expanded to `width` columns by
+// repeating the `dim` pattern (conv layers: width = hout*fout, dim = fout)
+bool upload_bn(KfNet *net, const std::vector<float> *h, float eps, float rms, int dim, int width,
+               float *&dscale, float *&dshift) {
+    std::vector<float> sc(width), sh(width);
+    for (int c = 0; c < width; ++c) {
+        int d = c % dim;
+        float inv = 1.0f / sqrtf(h[1][d] + eps);
+        float s = rms != 1.0f ? rms * inv : h[2][d] * inv;
+        sc[c] = s;
+        sh[c] = (rms != 1.0f ? 0.f : h[3][d]) - h[0][d] * s;
+    }
+    if (!dscale) {
+        dscale = (float *)net->dalloc(width * 4);
+        dshift = (float *)net->dalloc(width * 4);
+        if (!dscale || !dshift) return false;
+    }
+    return bridge_transfer_float32(dscale, sc.data(), width) == 0 &&
+           bridge_transfer_float32(dshift, sh.data(), width) == 0;
+}
+
+void identity_bn(std::vector<float> *h, int dim) {  // identityBN, forward.go:1172-1187
+    h[0].assign(dim, 0.f);
+    h[1].assign(dim, 1.f);
+    h[2].assign(dim, 1.f);
+    h[3].assign(dim, 0.f);
+}
+
+bool is_trainable(LayerType t) {
+    return t == LayerType::ConvReluBN || t == LayerType::TDNNF || t == LayerType::Linear ||
+           t == LayerType::Prefinal || t == LayerType::Output;
+}
+
+}  // namespace
+
+extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
+    g_nnet_err[0] = 0;
+    std::unique_ptr<KfNet> net(new KfNet);
+    std::vector<kf::LayerConfig> cfgs;
+    std::string err;
+    if (!kf::ParseXConfig(xconfig_text ? xconfig_text : "", cfgs, err) ||
+        !kf::ResolveLayers(cfgs, net->all, err)) {
+        set_err("parse xconfig: " + err);
+        return nullptr;
+    }
+    if (max_frames <= 0) {
+        set_err("max_frames must be positive");
+        return nullptr;
+    }
+    net->max_T = max_frames;
+    std::map<std::string, int> index;  // layer name -> index in net->layers (-1 = input)
+    for (const Layer &L : net->all) {
+        if (L.type == LayerType::Input) {
+            if (net->feat_dim && net->feat_dim != L.out_dim) {
+                set_err("multiple input layers are not supported (ivector Append: SURVEY §8d)");
+                return nullptr;
+            }
+            net->feat_dim = L.out_dim;
+            index[L.name] = -1;
+            continue;
+        }
+        NetLayer nl;
+        nl.L = L;
+        if (L.input.kind == kf::InputRef::Append || L.input_names.size() != 1) {
+            set_err("layer " + L.name + ": Append inputs are not in the fused path yet");
+            return nullptr;
+        }
+        auto it = index.find(L.input_names[0]);
+        if (it == index.end()) {
+            set_err("layer " + L.name + ": input not found");
+            return nullptr;
+        }
+        nl.input = it->second;
+        const int din = L.in_dim, dout = L.out_dim;
+        const std::string &n = L.name;
+        switch (L.type) {
+            case LayerType::IDCT:
+                if (din != dout || din > 64 || din % 8) {
+                    set_err("idct-layer " + n + ": dim must equal input dim, <= 64, multiple of 8");
+                    return nullptr;
+                }
+                break;
+            case LayerType::Batchnorm:
+                identity_bn(nl.hbn, dout);
+                nl.bn_rms = (float)L.target_rms;
+                break;
+            case LayerType::ConvReluBN: {
+                if (L.hin <= 0 || L.fin <= 0 || L.fin * L.hin != din || L.fout % 8) {
+                    set_err("conv layer " + n + ": inconsistent height-in / filters");
+                    return nullptr;
+                }
+                for (int a : L.time_offsets)
+                    for (int b : L.height_offsets) {
+                        nl.dt.push_back(a);
+                        nl.dh.push_back(b);
+                    }
+                if (nl.dt.empty() || nl.dt.size() > KF_MAX_PARTS) {
+                    set_err("conv layer " + n + ": need 1..9 (time x height) offsets");
+                    return nullptr;
+                }
+                if (L.fin != 1 && L.fin % 32) {
+                    set_err("conv layer " + n + ": num-filters-in must be 1 or a multiple of 32");
+                    return nullptr;
+                }
+                const int K = (int)nl.dt.size() * L.fin;
+                nl.pW = add_param(net.get(), n + ".W", K, L.fout);
+                nl.pb = add_param(net.get(), n + ".Bias", 1, L.fout);
+                identity_bn(nl.hbn, L.fout);
+                break;
+            }
+            case LayerType::TDNNF: {
+                const int s = L.time_stride, bn = L.bottleneck;
+                if (bn % 32 || din % 32 || dout % 8) {
+                    set_err("tdnnf layer " + n + ": dims must be multiples of 32");
+                    return nullptr;
+                }
+                nl.pW = add_param(net.get(), n + ".LinearW", s > 0 ? 2 * din : din, bn);
+                nl.pW2 = add_param(net.get(), n + ".AffineW", s > 0 ? 2 * bn : bn, dout);
+                nl.pb2 = add_param(net.get(), n + ".AffineBias", 1, dout);
+                nl.bypass = L.bypass_scale > 0 && din == dout;
+                identity_bn(nl.hbn, dout);
+                break;
+            }
+            case LayerType::Linear:
+                nl.pW = add_param(net.get(), n + ".W", din, dout);
+                break;
+            case LayerType::Prefinal:
+                nl.pW = add_param(net.get(), n + ".BigW", din, L.big_dim);
+                nl.pb = add_param(net.get(), n + ".BigBias", 1, L.big_dim);
+                nl.pW2 = add_param(net.get(), n + ".SmallW", L.big_dim, L.small_dim);
+                identity_bn(nl.hbn, L.big_dim);
+                identity_bn(nl.hbn2, L.small_dim);
+                nl.has_bn2 = true;
+                break;
+            case LayerType::Output:
+                if (L.include_log_softmax) {
+                    // the xent branch (log-softmax output) is a "next" row
+                }
+                nl.pW = add_param(net.get(), n + ".W", din, dout);
+                nl.pb = add_param(net.get(), n + ".Bias", 1, dout);
+                break;
+            case LayerType::SpecAugment:
+            case LayerType::CombineFeatureMaps:
+                break;
+            default:
+                set_err("layer " + n + ": type not supported on the MI355X path");
+                return nullptr;
+        }
+        index[L.name] = (int)net->layers.size();
+        net->layers.push_back(nl);
+    }
+    if (net->layers.empty()) {
+        set_err("no layers");
+        return nullptr;
+    }
+    // which layers need an input gradient (a trainable layer lies below them)
+    for (size_t i = 0; i < net->layers.size(); ++i) {
+        bool need = false;
+        for (int cur = net->layers[i].input; cur >= 0; cur = net->layers[cur].input)
+            if (is_trainable(net->layers[cur].L.type)) need = true;
+        net->layers[i].needs_dx = need;
+    }
+    // flat parameter storage
+    const long long P = net->nparams > 0 ? net->nparams : 64;
+    net->master = (float *)net->dalloc(P * 4);
+    net->grad = (float *)net->dalloc(P * 4);
+    net->vel = (float *)net->dalloc(P * 4);
+    net->w16 = net->dalloc(P * 2);
+    if (!net->master || !net->grad || !net->vel || !net->w16) {
+        set_err("alloc params: " + std::string(bridge_last_error() ? bridge_last_error() : ""));
+        return nullptr;
+    }
+    bridge_gpu_memset(net->master, 0, P * 4);
+    bridge_gpu_memset(net->grad, 0, P * 4);
+    bridge_gpu_memset(net->vel, 0, P * 4);
+    bridge_gpu_memset(net->w16, 0, P * 2);
+    // activations, masks, BN params
+    const size_t T = (size_t)max_frames;
+    size_t maxw = 16;
+    for (auto &nl : net->layers) {
+        const Layer &L = nl.L;
+        const int dout = L.out_dim;
+        maxw = std::max(maxw, (size_t)std::max(L.in_dim, dout));
+        if (L.type == LayerType::SpecAugment) {
+            nl.act_alias = true;
+        } else {
+            nl.act = net->dalloc(T * dout * 2);
+            if (!nl.act) {
+                set_err("alloc activation " + L.name);
+                return nullptr;
+            }
+        }
+        int mwidth = 0;
+        if (L.type == LayerType::ConvReluBN || L.type == LayerType::TDNNF) mwidth = dout;
+        if (L.type == LayerType::Prefinal) mwidth = L.big_dim;
+        if (mwidth) nl.mask = (uint8_t *)net->dalloc(align_up(T * mwidth / 8 + 16, 256));
+        if (L.type == LayerType::TDNNF) nl.aux = net->dalloc(T * L.bottleneck * 2);
+        if (L.type == LayerType::Prefinal) {
+            nl.aux = net->dalloc(T * L.big_dim * 2);
+            maxw = std::max(maxw, (size_t)L.big_dim);
+        }
+        if (L.type == LayerType::IDCT) {
+            auto m = idct_matrix(dout, L.cepstral_lifter);
+            std::vector<uint16_t> h(m.size());
+            for (size_t i = 0; i < m.size(); ++i) h[i] = f32_to_f16_trunc(m[i]);
+            nl.idct = net->dalloc(h.size() * 2);
+            if (bridge_transfer_fp16(nl.idct, h.data(), h.size())) {
+                set_err("upload idct");
+                return nullptr;
+            }
+        }
+        if (L.type == LayerType::Batchnorm &&
+            !upload_bn(net.get(), nl.hbn, nl.bn_eps, nl.bn_rms, dout, dout, nl.bn_scale, nl.bn_shift))
+            return nullptr;
+        if (L.type == LayerType::ConvReluBN &&
+            !upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, L.fout, dout, nl.bn_scale, nl.bn_shift))
+            return nullptr;
+        if (L.type == LayerType::TDNNF &&
+            !upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, dout, dout, nl.bn_scale, nl.bn_shift))
+            return nullptr;
+        if (L.type == LayerType::Prefinal &&
+            (!upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, L.big_dim, L.big_dim, nl.bn_scale,
+                        nl.bn_shift) ||
+             !upload_bn(net.get(), nl.hbn2, nl.bn2_eps, 1.f, L.small_dim, L.small_dim,
+                        nl.bn2_scale, nl.bn2_shift)))
+            return nullptr;
+    }
+    for (int i = 0; i < 2; ++i) {
+        net->dz[i] = net->dalloc(T * maxw * 2);
+        net->g[i] = net->dalloc(T * maxw * 2);
+    }
+    net->dbott = net->dalloc(T * maxw * 2);
+    net->edge_half = align_up(maxw * 2, 256);
+    net->edge = net->dalloc(net->edge_half * 2);
+    if (!net->dz[0] || !net->dz[1] || !net->g[0] || !net->g[1] || !net->dbott || !net->edge) {
+        set_err("alloc backward scratch");
+        return nullptr;
+    }
+    return net.release();
+}
+
+extern "C" void nnet_free(KfNet *net) { delete net; }
+
+extern "C" int nnet_num_layers(const KfNet *net) { return (int)net->layers.size(); }
+
+extern "C" int nnet_layer_info(const KfNet *net, int idx, char *name, int namelen, int *type,
+                               int *in_dim, int *out_dim) {
+    if (idx < 0 || idx >= (int)net->layers.size()) return -1;
+    const Layer &L = net->layers[idx].L;
+    if (name && namelen > 0) snprintf(name, namelen, "%s", L.name.c_str());
+    if (type) *type = (int)L.type;
+    if (in_dim) *in_dim = L.in_dim;
+    if (out_dim) *out_dim = L.out_dim;
+    return 0;
+}
+
+extern "C" long long nnet_num_params(const KfNet *net) { return net->nparams; }
+extern "C" int nnet_num_param_tensors(const KfNet *net) { return (int)net->params.size(); }
+extern "C" int nnet_param_info(const KfNet *net, int idx, char *name, int namelen, int *rows,
+                               int *cols, long long *offset) {
+    if (idx < 0 || idx >= (int)net->params.size()) return -1;
+    const ParamRef &p = net->params[idx];
+    if (name && namelen > 0) snprintf(name, namelen, "%s", p.name.c_str());
+    if (rows) *rows = p.rows;
+    if (cols) *cols = p.cols;
+    if (offset) *offset = p.off;
+    return 0;
+}
+
+extern "C" int nnet_set_params(KfNet *net, const float *host) {
+    const long long P = net->nparams;
+    std::vector<uint16_t> h(P, 0);
+    std::vector<float> m(P, 0.f);
+    for (const ParamRef &p : net->params)
+        for (long long i = 0; i < (long long)p.rows * p.cols; ++i) {
+            uint16_t v = f32_to_f16_trunc(host[p.off + i]);
+            h[p.off + i] = v;
+            m[p.off + i] = f16_to_f32(v);
+        }
+    if (bridge_transfer_fp16(net->w16, h.data(), P) || bridge_transfer_float32(net->master, m.data(), P)) {
+        set_err(std::string("set_params: ") + (bridge_last_error() ? bridge_last_error() : ""));
+        return -1;
+    }
+    bridge_gpu_memset(net->vel, 0, P * 4);
+    return 0;
+}
+
+extern "C" int nnet_get_params(const KfNet *net, float *host) {
+    // D2H through the bridge (fp32 read = 2x fp16 count on a 4-byte aligned buffer)
+    std::vector<uint16_t> tmp(net->nparams * 2);
+    if (bridge_read_fp16(tmp.data(), net->master, net->nparams * 2)) {
+        set_err("get_params");
+        return -1;
+    }
+    memcpy(host, tmp.data(), net->nparams * 4);
+    return 0;
+}
+
+extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean,
+                           const float *var, const float *gamma, const float *beta, float eps,
+                           float target_rms) {
+    for (auto &nl : net->layers) {
+        if (nl.L.name != layer) continue;
+        const Layer &L = nl.L;
+        int dim, width;
+        std::vector<float> *h;
+        if (which == 1) {
+            if (L.type != LayerType::Prefinal) break;
+            dim = width = L.small_dim;
+            h = nl.hbn2;
+            nl.bn2_eps = eps;
+            nl.bn2_rms = target_rms;
+        } else {
+            if (L.type == LayerType::ConvReluBN) {
+                dim = L.fout;
+                width = L.out_dim;
+            } else if (L.type == LayerType::Prefinal) {
+                dim = width = L.big_dim;
+            } else if (L.type == LayerType::TDNNF || L.type == LayerType::Batchnorm) {
+                dim = width = L.out_dim;
+            } else {
+                break;
+            }
+            h = nl.hbn;
+            nl.bn_eps = eps;
+            nl.bn_rms = target_rms;
+        }
+        h[0].assign(mean, mean + dim);
+        h[1].assign(var, var + dim);
+        h[2].assign(gamma, gamma + dim);
+        h[3].assign(beta, beta + dim);
+        if (which == 1) return upload_bn(net, h, eps, target_rms, dim, width, nl.bn2_scale, nl.bn2_shift) ? 0 : -1;
+        return upload_bn(net, h, eps, target_rms, dim, width, nl.bn_scale, nl.bn_shift) ? 0 : -1;
+    }
+    set_err(std::string("set_bn: no BatchNorm '") + std::to_string(which) + "' on layer " + layer);
+    return -1;
+}
+
+static const void *act_of(KfNet *net, int idx) {
+    if (idx < 0) return net->features;
+    NetLayer &nl = net->layers[idx];
+    return nl.act_alias ? act_of(net, nl.input) : nl.act;
+}
+
+// ---------------------------------------------------------------------------
+// forward (Network.Forward, forward.go:148-202)
+// ---------------------------------------------------------------------------
+extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
+    if (T <= 0 || T > net->max_T) {
+        set_err("forward: T=" + std::to_string(T) + " outside (0, max_frames]");
+        return -1;
+    }
+    net->T = T;
+    net->features = features;
+    for (size_t li = 0; li < net->layers.size(); ++li) {
+        NetLayer &nl = net->layers[li];
+        const Layer &L = nl.L;
+        const void *x = act_of(net, nl.input);
+        const int din = L.in_dim, dout = L.out_dim;
+        switch (L.type) {
+            case LayerType::IDCT:
+                if (!ck(kf_small_gemm(x, din, nl.idct, nl.act, dout, T, din, dout), "idct")) return -1;
+                break;
+            case LayerType::Batchnorm:
+                if (!ck(kf_bn_apply(x, nl.act, T, dout, nl.bn_scale, nl.bn_shift), "batchnorm")) return -1;
+                break;
+            case LayerType::SpecAugment:
+                break;  // pass-through (forward.go:225-231, masking is a TODO there too)
+            case LayerType::CombineFeatureMaps:
+                if (!ck(ops_copy(nl.act, x, T * dout), "combine copy") ||
+                    !ck(ops_combine_feature_maps(nl.act, T, dout, L.height, L.nf1, L.nf2), "combine"))
+                    return -1;
+                break;
+            case LayerType::ConvReluBN: {
+                if (L.fin == 1) {
+                    if (!ck(kf_conv_c1_forward(T, L.hin, L.hout, L.hsub, L.fout, (int)nl.dt.size(),
+                                               nl.dt.data(), nl.dh.data(), x, wptr(net, nl.pW),
+                                               wptr(net, nl.pb), nl.bn_scale, nl.bn_shift, nl.act,
+                                               nl.mask),
+                            "conv c1"))
+                        return -1;
+                    break;
+                }
+                const int K = (int)nl.dt.size() * L.fin;
+                KfOperand A = op_im2col(nl, x, T, 1);
+                KfOperand B = op_base(wptr(net, nl.pW), L.fout, K, L.fout, 0);
+                KfEpilogue E = epi0();
+                E.out = nl.act;
+                E.ldo = L.fout;
+                E.bias = wptr(net, nl.pb);
+                E.relu = 1;
+                E.mask_out = nl.mask;
+                E.scale = nl.bn_scale;
+                E.shift = nl.bn_shift;
+                if (!ck(kf_gemm_fused(T * L.hout, L.fout, K, &A, &B, &E), "conv")) return -1;
+                break;
+            }
+            case LayerType::TDNNF: {
+                const int s = L.time_stride, bn = L.bottleneck;
+                const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
+                KfOperand A = s > 0 ? op_splice(x, T, din, -s, 0, KF_CLAMP, 1) : op_base(x, din, T, din, 1);
+                KfOperand B = op_base(wptr(net, nl.pW), bn, klin, bn, 0);
+                KfEpilogue E = epi0();
+                E.out = nl.aux;
+                E.ldo = bn;
+                if (!ck(kf_gemm_fused(T, bn, klin, &A, &B, &E), "tdnnf linear")) return -1;
+                KfOperand A2 = s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 1)
+                                     : op_base(nl.aux, bn, T, bn, 1);
+                KfOperand B2 = op_base(wptr(net, nl.pW2), dout, kaff, dout, 0);
+                KfEpilogue E2 = epi0();
+                E2.out = nl.act;
+                E2.ldo = dout;
+                E2.bias = wptr(net, nl.pb2);
+                E2.relu = 1;
+                E2.mask_out = nl.mask;
+                E2.scale = nl.bn_scale;
+                E2.shift = nl.bn_shift;
+                if (nl.bypass) {
+                    E2.resid = x;
+                    E2.ldr = din;
+                    E2.resid_alpha = (float)L.bypass_scale;
+                }
+                if (!ck(kf_gemm_fused(T, dout, kaff, &A2, &B2, &E2), "tdnnf affine")) return -1;
+                break;
+            }
+            case LayerType::Linear: {
+                KfOperand A = op_base(x, din, T, din, 1);
+                KfOperand B = op_base(wptr(net, nl.pW), dout, din, dout, 0);
+                KfEpilogue E = epi0();
+                E.out = nl.act;
+                E.ldo = dout;
+                if (!ck(kf_gemm_fused(T, dout, din, &A, &B, &E), "linear")) return -1;
+                break;
+            }
+            case LayerType::Prefinal: {
+                const int big = L.big_dim, small = L.small_dim;
+                KfOperand A = op_base(x, din, T, din, 1);
+                KfOperand B = op_base(wptr(net, nl.pW), big, din, big, 0);
+                KfEpilogue E = epi0();
+                E.out = nl.aux;
+                E.ldo = big;
+                E.bias = wptr(net, nl.pb);
+                E.relu = 1;
+                E.mask_out = nl.mask;
+                E.scale = nl.bn_scale;
+                E.shift = nl.bn_shift;
+                if (!ck(kf_gemm_fused(T, big, din, &A, &B, &E), "prefinal big")) return -1;
+                KfOperand A2 = op_base(nl.aux, big, T, big, 1);
+                KfOperand B2 = op_base(wptr(net, nl.pW2), small, big, small, 0);
+                KfEpilogue E2 = epi0();
+                E2.out = nl.act;
+                E2.ldo = small;
+                if (nl.has_bn2) {
+                    E2.scale = nl.bn2_scale;
+                    E2.shift = nl.bn2_shift;
+                }
+                if (!ck(kf_gemm_fused(T, small, big, &A2, &B2, &E2), "prefinal small")) return -1;
+                break;
+            }
+            case LayerType::Output: {
+                KfOperand A = op_base(x, din, T, din, 1);
+                KfOperand B = op_base(wptr(net, nl.pW), dout, din, dout, 0);
+                KfEpilogue E = epi0();
+                E.out = nl.act;
+                E.ldo = dout;
+                E.bias = wptr(net, nl.pb);
+                if (!ck(kf_gemm_fused(T, dout, din, &A, &B, &E), "output")) return -1;
+                if (L.include_log_softmax && !ck(ops_log_softmax(nl.act, T, dout), "log_softmax"))
+                    return -1;
+                break;
+            }
+            default:
+                set_err("forward: unsupported layer " + L.name);
+                return -1;
+        }
+    }
+    return 0;
+}
+
+extern "C" const void *nnet_activation(const KfNet *cnet, const char *layer, int *rows, int *cols) {
+    KfNet *net = const_cast<KfNet *>(cnet);
+    for (size_t i = 0; i < net->layers.size(); ++i)
+        if (net->layers[i].L.name == layer) {
+            if (rows) *rows = net->T;
+            if (cols) *cols = net->layers[i].L.out_dim;
+            return act_of(net, (int)i);
+        }
+    set_err(std::string("no layer ") + layer);
+    return nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// backward (Network.Backward, network_backward.go:94-143) — exact gradients
+// ---------------------------------------------------------------------------
+namespace {
+
+// Epilogue of an input-gradient GEMM that produces the gradient of layer P
+// (the input of the layer being back-propagated). v = acc (+ bypass * g_cur):
+//   g_P = rne(v) when P itself has a bypass (its own input gradient needs it)
+//   dz_P = rne(v * bnscale_P * mask_P) for relu+BN layers, rne(v*bn2scale) for prefinal
+bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
+    E = epi0();
+    NetLayer &pl = net->layers[P];
+    const Layer &L = pl.L;
+    const int w = L.out_dim;
+    E.ldo2 = w;
+    E.out2 = dz_out;
+    switch (L.type) {
+        case LayerType::TDNNF:
+            E.scale2 = pl.bn_scale;
+            E.mask_in = pl.mask;
+            if (pl.bypass) {
+                E.out = g_out;
+                E.ldo = w;
+            }
+            return true;
+        case LayerType::ConvReluBN:
+            E.scale2 = pl.bn_scale;
+            E.mask_in = pl.mask;
+            return true;
+        case LayerType::Prefinal:
+            if (pl.has_bn2) E.scale2 = pl.bn2_scale;
+            return true;
+        case LayerType::Linear:
+            return true;
+        default:
+            set_err("backward: gradient into layer " + L.name + " is not supported");
+            return false;
+    }
+}
+
+}  // namespace
+
+extern "C" int nnet_backward(KfNet *net, const void *out_grad) {
+    const int T = net->T;
+    if (T <= 0) {
+        set_err("backward before forward");
+        return -1;
+    }
+    const int n = (int)net->layers.size();
+    // the top layer must be the chain output
+    const void *dz = out_grad;  // gradient w.r.t. pre-activation of the current layer
+    const void *gcur = out_grad;  // stored gradient w.r.t. the current layer's output
+    int flip = 0;
+    for (int li = n - 1; li >= 0; li = net->layers[li].input) {
+        NetLayer &nl = net->layers[li];
+        const Layer &L = nl.L;
+        const int din = L.in_dim, dout = L.out_dim;
+        const void *x = act_of(net, nl.input);
+        const bool want_dx = nl.needs_dx && nl.input >= 0;
+        void *dz_next = net->dz[flip], *g_next = net->g[flip];
+        KfEpilogue E;
+        if (want_dx && !dx_epilogue(net, nl.input, dz_next, g_next, E)) return -1;
+        if (nl.bypass) {
+            E.resid = gcur;
+            E.ldr = dout;
+            E.resid_alpha = (float)L.bypass_scale;
+        }
+        switch (L.type) {
+            case LayerType::Output:
+            case LayerType::Linear: {
+                KfOperand A = op_base(x, din, T, din, 0);
+                KfOperand B = op_base(dz, dout, T, dout, 0);
+                if (!ck(kf_gemm_wgrad(din, dout, T, &A, &B, gptr(net, nl.pW), dout, gptr(net, nl.pb), 0),
+                        "wgrad"))
+                    return -1;
+                if (want_dx) {
+                    KfOperand A2 = op_base(dz, dout, T, dout, 1);
+                    KfOperand B2 = op_base(wptr(net, nl.pW), dout, din, dout, 1);
+                    if (!ck(kf_gemm_fused(T, din, dout, &A2, &B2, &E), "dgrad")) return -1;
+                }
+                break;
+            }
+            case LayerType::Prefinal: {
+                const int big = L.big_dim, small = L.small_dim;
+                // dz = gradient at the small (BN2) pre-activation
+                KfOperand A = op_base(nl.aux, big, T, big, 0);
+                KfOperand B = op_base(dz, small, T, small, 0);
+                if (!ck(kf_gemm_wgrad(big, small, T, &A, &B, gptr(net, nl.pW2), small, nullptr, 0),
+                        "prefinal small wgrad"))
+                    return -1;
+                void *dzbig = net->dbott;
+                KfEpilogue E1 = epi0();
+                E1.out2 = dzbig;
+                E1.ldo2 = big;
+                E1.scale2 = nl.bn_scale;
+                E1.mask_in = nl.mask;
+                KfOperand A1 = op_base(dz, small, T, small, 1);
+                KfOperand B1 = op_base(wptr(net, nl.pW2), small, big, small, 1);
+                if (!ck(kf_gemm_fused(T, big, small, &A1, &B1, &E1), "prefinal small dgrad")) return -1;
+                KfOperand A3 = op_base(x, din, T, din, 0);
+                KfOperand B3 = op_base(dzbig, big, T, big, 0);
+                if (!ck(kf_gemm_wgrad(din, big, T, &A3, &B3, gptr(net, nl.pW), big, gptr(net, nl.pb), 0),
+                        "prefinal big wgrad"))
+                    return -1;
+                if (want_dx) {
+                    KfOperand A4 = op_base(dzbig, big, T, big, 1);
+                    KfOperand B4 = op_base(wptr(net, nl.pW), big, din, big, 1);
+                    if (!ck(kf_gemm_fused(T, din, big, &A4, &B4, &E), "prefinal big dgrad")) return -1;
+                }
+                break;
+            }
+            case LayerType::TDNNF: {
+                const int s = L.time_stride, bn = L.bottleneck;
+                const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
+                // affine weight / bias gradient: splice+(bott)^T . dz
+                KfOperand A = s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 0)
+                                    : op_base(nl.aux, bn, T, bn, 0);
+                KfOperand B = op_base(dz, dout, T, dout, 0);
+                if (!ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
+                        "tdnnf affine wgrad"))
+                    return -1;
+                // bottleneck gradient: transpose of the [0, +s] clamped splice
+                void *dbott = net->dbott;
+                KfEpilogue E1 = epi0();
+                E1.out = dbott;
+                E1.ldo = bn;
+                if (s > 0) {
+                    void *edge = net->edge;
+                    if (!ck(kf_rows_sum(edge, dz, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout), "edge"))
+                        return -1;
+                    KfOperand A1 = op_splice(dz, T, dout, 0, -s, KF_ZERO, 1);
+                    A1.edge_t[1] = T - 1;
+                    A1.edge_ptr[1] = edge;
+                    KfOperand B1 = op_wrows(wptr(net, nl.pW2), 2, bn, dout);
+                    if (!ck(kf_gemm_fused(T, bn, 2 * dout, &A1, &B1, &E1), "tdnnf affine dgrad"))
+                        return -1;
+                } else {
+                    KfOperand A1 = op_base(dz, dout, T, dout, 1);
+                    KfOperand B1 = op_base(wptr(net, nl.pW2), dout, bn, dout, 1);
+                    if (!ck(kf_gemm_fused(T, bn, dout, &A1, &B1, &E1), "tdnnf affine dgrad")) return -1;
+                }
+                // linear weight gradient: splice-(x)^T . dbott
+                KfOperand A2 = s > 0 ? op_splice(x, T, din, -s, 0, KF_CLAMP, 0)
+                                     : op_base(x, din, T, din, 0);
+                KfOperand B2 = op_base(dbott, bn, T, bn, 0);
+                if (!ck(kf_gemm_wgrad(klin, bn, T, &A2, &B2, gptr(net, nl.pW), bn, nullptr, 0),
+                        "tdnnf linear wgrad"))
+                    return -1;
+                if (want_dx) {
+                    // input gradient: transpose of the [-s, 0] clamped splice
+                    if (s > 0) {
+                        void *edge = (char *)net->edge + net->edge_half;
+                        if (!ck(kf_rows_sum(edge, dbott, bn, 0, s + 1 < T ? s + 1 : T, bn), "edge"))
+                            return -1;
+                        KfOperand A3 = op_splice(dbott, T, bn, s, 0, KF_ZERO, 1);
+                        A3.edge_t[0] = 0;
+                        A3.edge_ptr[0] = edge;
+                        KfOperand B3 = op_wrows(wptr(net, nl.pW), 2, din, bn);
+                        if (!ck(kf_gemm_fused(T, din, 2 * bn, &A3, &B3, &E), "tdnnf linear dgrad"))
+                            return -1;
+                    } else {
+                        KfOperand A3 = op_base(dbott, bn, T, bn, 1);
+                        KfOperand B3 = op_base(wptr(net, nl.pW), bn, din, bn, 1);
+                        if (!ck(kf_gemm_fused(T, din, bn, &A3, &B3, &E), "tdnnf linear dgrad")) return -1;
+                    }
+                }
+                break;
+            }
+            case LayerType::ConvReluBN: {
+                const int noff = (int)nl.dt.size();
+                if (L.fin == 1) {
+                    if (!ck(kf_conv_c1_wgrad(T, L.hin, L.hout, L.hsub, L.fout, noff, nl.dt.data(),
+                                             nl.dh.data(), x, dz, gptr(net, nl.pW), gptr(net, nl.pb)),
+                            "conv c1 wgrad"))
+                        return -1;
+                } else {
+                    KfOperand A = op_im2col(nl, x, T, 0);
+                    KfOperand B = op_base(dz, L.fout, T * L.hout, L.fout, 0);
+                    if (!ck(kf_gemm_wgrad(noff * L.fin, L.fout, T * L.hout, &A, &B, gptr(net, nl.pW),
+                                          L.fout, gptr(net, nl.pb), 0),
+                            "conv wgrad"))
+                        return -1;
+                }
+                if (want_dx) {
+                    if (L.fin == 1) {
+                        set_err("conv " + L.name + ": input gradient of a 1-filter conv not supported");
+                        return -1;
+                    }
+                    KfOperand A2 = op_col2im(nl, dz, T);
+                    KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
+                    E.ldo2 = L.fin;  // dz of the input conv layer viewed as [(t,h) x fin]
+                    if (E.out) E.ldo = L.fin;
+                    if (!ck(kf_gemm_fused(T * L.hin, L.fin, noff * L.fout, &A2, &B2, &E), "conv dgrad"))
+                        return -1;
+                }
+                break;
+            }
+            case LayerType::Batchnorm:
+            case LayerType::IDCT:
+            case LayerType::SpecAugment:
+            case LayerType::CombineFeatureMaps:
+                if (want_dx) {
+                    set_err("backward through " + L.name + " into trainable layers is not supported");
+                    return -1;
+                }
+                break;
+            default:
+                set_err("backward: unsupported layer " + L.name);
+                return -1;
+        }
+        if (!want_dx) break;  // nothing trainable below
+        dz = dz_next;
+        gcur = g_next;
+        flip ^= 1;
+    }
+    return 0;
+}
+
+extern "C" float *nnet_grad_buffer(KfNet *net) { return net->grad; }
+extern "C" float *nnet_master_buffer(KfNet *net) { return net->master; }
+extern "C" void *nnet_weight_buffer(KfNet *net) { return net->w16; }
+
+extern "C" int nnet_sgd(KfNet *net, float lr, float momentum) {
+    return ck(kf_sgd_flat(net->master, net->w16, net->grad, net->vel, lr, momentum, net->nparams),
+              "sgd")
+               ? 0
+               : -1;
+}
+
+// Parse + resolve only (no device work): one line per layer
+// "name type in_dim out_dim" followed by "params N". Returns bytes needed, -1 on error.
+extern "C" int nnet_parse_summary(const char *xconfig_text, char *out, int outlen) {
+    std::vector<kf::LayerConfig> cfgs;
+    std::vector<Layer> layers;
+    std::string err;
+    if (!kf::ParseXConfig(xconfig_text ? xconfig_text : "", cfgs, err) ||
+        !kf::ResolveLayers(cfgs, layers, err)) {
+        set_err("parse xconfig: " + err);
+        return -1;
+    }
+    std::string s;
+    long long nparams = 0;
+    for (const Layer &L : layers) {
+        s += L.name + " " + std::to_string((int)L.type) + " " + std::to_string(L.in_dim) + " " +
+             std::to_string(L.out_dim) + "\n";
+        switch (L.type) {
+            case LayerType::ConvReluBN:
+                nparams += (long long)L.time_offsets.size() * L.height_offsets.size() * L.fin * L.fout + L.fout;
+                break;
+            case LayerType::TDNNF: {
+                int k = L.time_stride > 0 ? 2 : 1;
+                nparams += (long long)k * L.in_dim * L.bottleneck + (long long)k * L.bottleneck * L.out_dim + L.out_dim;
+                break;
+            }
+            case LayerType::Linear: nparams += (long long)L.in_dim * L.out_dim; break;
+            case LayerType::Prefinal:
+                nparams += (long long)L.in_dim * L.big_dim + L.big_dim + (long long)L.big_dim * L.small_dim;
+                break;
+            case LayerType::Output: nparams += (long long)L.in_dim * L.out_dim + L.out_dim; break;
+            default: break;
+        }
+    }
+    s += "params " + std::to_string(nparams) + "\n";
+    if (out && outlen > 0) snprintf(out, outlen, "%s", s.c_str());
+    return (int)s.size() + 1;
+}
+
+// Use caller-owned device memory (>= num_params fp32) as the gradient buffer,
+// e.g. a torch tensor handed to the data-parallel all-reduce.
+extern "C" int nnet_bind_grad_buffer(KfNet *net, float *dev) {
+    if (!dev) {
+        set_err("bind_grad_buffer: null");
+        return -1;
+    }
+    net->grad = dev;
+    return 0;
+}

@@ -1,0 +1,299 @@
+"""kfp16 — Python binding of the MI355X kaldi-fp16 core.
+
+Thin ctypes layer over the C-ABI libraries built in ``kaldi-fp16_amd/lib``:
+``libkaldi_fp16.so`` (bridge_* / ops_* / chain_* / den_* / kf_* kernels) and
+``libkaldi_fp16_nnet.so`` (the C++ host layer restating internal/nnet).
+Tests and bench.py drive the product through this module; nothing here
+computes anything itself. If the HIP libraries are missing, importing this
+module raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.normpath(os.path.join(_HERE, "..", "..", "lib"))
+INCDIR = os.path.normpath(os.path.join(_HERE, "..", "..", "..", "include"))
+
+
+class KfError(RuntimeError):
+    pass
+
+
+def _load(name):
+    path = os.path.join(LIBDIR, name)
+    if not os.path.exists(path):
+        raise ImportError(
+            f"kfp16: {path} is missing — build the HIP libraries first "
+            "(python -c 'import __graft_entry__ as g; g.build()'); there is no CPU fallback")
+    return C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
+core = _load("libkaldi_fp16.so")
+nnet = _load("libkaldi_fp16_nnet.so")
+
+_vp, _i, _f, _ll, _sz = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_size_t
+
+
+def _sig(lib, name, res, *args):
+    fn = getattr(lib, name)
+    fn.restype = res
+    fn.argtypes = list(args)
+    return fn
+
+
+# ---------------------------------------------------------------- bridge_*
+for _n in ("bridge_last_error", "ops_last_error", "kf_last_error", "nnet_last_error"):
+    _sig(core if not _n.startswith("nnet") else nnet, _n, C.c_char_p)
+_sig(core, "bridge_clear_error", None)
+_sig(core, "bridge_gpu_init", _i, _i)
+_sig(core, "bridge_gpu_sync", _i)
+_sig(core, "bridge_gpu_get_free_memory", _i, C.POINTER(_sz), C.POINTER(_sz))
+_sig(core, "bridge_gpu_malloc", _vp, _sz)
+_sig(core, "bridge_gpu_free", None, _vp)
+_sig(core, "bridge_transfer_fp16", _i, _vp, _vp, _sz)
+_sig(core, "bridge_read_fp16", _i, _vp, _vp, _sz)
+_sig(core, "bridge_transfer_int32", _i, _vp, _vp, _sz)
+_sig(core, "bridge_transfer_float32", _i, _vp, _vp, _sz)
+_sig(core, "bridge_gpu_memset", None, _vp, _i, _sz)
+_sig(core, "bridge_fp16_to_fp32_gpu", _i, _vp, _vp, _sz)
+_sig(core, "bridge_fp32_to_fp16_gpu", _i, _vp, _vp, _sz)
+_sig(core, "kf_set_stream", None, _vp)
+_sig(core, "kf_get_stream", _vp)
+_sig(core, "ops_gemm", _i, _vp, _i, _i, _i, _f, _vp, _i, _vp, _i, _f, _vp, _i)
+_sig(core, "ops_cublas_create", _vp)
+_sig(core, "ops_cublas_destroy", None, _vp)
+
+# ---------------------------------------------------------------- nnet_*
+_sig(nnet, "nnet_create", _vp, C.c_char_p, _i)
+_sig(nnet, "nnet_free", None, _vp)
+_sig(nnet, "nnet_parse_summary", _i, C.c_char_p, C.c_char_p, _i)
+_sig(nnet, "nnet_num_layers", _i, _vp)
+_sig(nnet, "nnet_layer_info", _i, _vp, _i, C.c_char_p, _i, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i))
+_sig(nnet, "nnet_num_params", _ll, _vp)
+_sig(nnet, "nnet_num_param_tensors", _i, _vp)
+_sig(nnet, "nnet_param_info", _i, _vp, _i, C.c_char_p, _i, C.POINTER(_i), C.POINTER(_i), C.POINTER(_ll))
+_sig(nnet, "nnet_set_params", _i, _vp, _vp)
+_sig(nnet, "nnet_get_params", _i, _vp, _vp)
+_sig(nnet, "nnet_set_bn", _i, _vp, C.c_char_p, _i, _vp, _vp, _vp, _vp, _f, _f)
+_sig(nnet, "nnet_forward", _i, _vp, _vp, _i)
+_sig(nnet, "nnet_activation", _vp, _vp, C.c_char_p, C.POINTER(_i), C.POINTER(_i))
+_sig(nnet, "nnet_backward", _i, _vp, _vp)
+_sig(nnet, "nnet_grad_buffer", _vp, _vp)
+_sig(nnet, "nnet_master_buffer", _vp, _vp)
+_sig(nnet, "nnet_weight_buffer", _vp, _vp)
+_sig(nnet, "nnet_sgd", _i, _vp, _f, _f)
+_sig(nnet, "nnet_bind_grad_buffer", _i, _vp, _vp)
+_sig(core, "kf_prof_enable", None, _i)
+_sig(core, "kf_prof_collect", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double))
+_sig(core, "kf_prof_reset", None)
+
+
+def _err(lib_fn):
+    s = lib_fn()
+    return s.decode() if s else "unknown error"
+
+
+def check(rc, what="kfp16"):
+    if rc != 0:
+        msgs = [m for m in (core.kf_last_error(), core.ops_last_error(), core.bridge_last_error(),
+                            nnet.nnet_last_error()) if m]
+        raise KfError(f"{what}: " + "; ".join(m.decode() for m in msgs))
+
+
+# ---------------------------------------------------------------- device buffers
+class DeviceBuffer:
+    """Owning device allocation made through bridge_gpu_malloc."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self.ptr = core.bridge_gpu_malloc(max(self.nbytes, 16))
+        if not self.ptr:
+            raise KfError("bridge_gpu_malloc: " + _err(core.bridge_last_error))
+
+    def free(self):
+        if self.ptr:
+            core.bridge_gpu_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def upload_fp16(arr: np.ndarray) -> DeviceBuffer:
+    a = np.ascontiguousarray(arr, dtype=np.float16)
+    buf = DeviceBuffer(a.nbytes)
+    check(core.bridge_transfer_fp16(buf.ptr, a.ctypes.data, a.size), "upload_fp16")
+    buf.shape = a.shape
+    return buf
+
+
+def upload_f32(arr: np.ndarray) -> DeviceBuffer:
+    a = np.ascontiguousarray(arr, dtype=np.float32)
+    buf = DeviceBuffer(a.nbytes)
+    check(core.bridge_transfer_float32(buf.ptr, a.ctypes.data, a.size), "upload_f32")
+    buf.shape = a.shape
+    return buf
+
+
+def read_fp16(ptr, shape) -> np.ndarray:
+    out = np.empty(shape, dtype=np.float16)
+    check(core.bridge_read_fp16(out.ctypes.data, ptr, out.size), "read_fp16")
+    return out
+
+
+def read_f32(ptr, shape) -> np.ndarray:
+    out = np.empty(shape, dtype=np.float32)
+    # bridge has no fp32 read: read the bytes as twice as many fp16 words
+    check(core.bridge_read_fp16(out.ctypes.data, ptr, out.size * 2), "read_f32")
+    return out
+
+
+def hip_runtimes():
+    """Paths of every HIP runtime mapped into this process (must be exactly one:
+    import torch BEFORE kfp16 when both are used, so both bind torch's copy)."""
+    with open("/proc/self/maps") as f:
+        return sorted({l.split()[-1] for l in f if "libamdhip64" in l})
+
+
+def assert_single_hip_runtime():
+    libs = hip_runtimes()
+    if len(libs) > 1:
+        raise KfError(f"two HIP runtimes loaded {libs}: import torch before kfp16")
+
+
+def prof_collect(cls: int):
+    n, ms, fl = _ll(), C.c_double(), C.c_double()
+    core.kf_prof_collect(cls, C.byref(n), C.byref(ms), C.byref(fl))
+    return n.value, ms.value, fl.value
+
+
+def set_stream(stream_handle) -> None:
+    core.kf_set_stream(C.c_void_p(stream_handle) if stream_handle else None)
+
+
+def sync() -> None:
+    check(core.bridge_gpu_sync(), "sync")
+
+
+# ---------------------------------------------------------------- network
+class Network:
+    """internal/nnet Network (forward.go:15-21) behind the nnet_* C-ABI."""
+
+    def __init__(self, xconfig: str, max_frames: int):
+        self.h = nnet.nnet_create(xconfig.encode(), int(max_frames))
+        if not self.h:
+            raise KfError("nnet_create: " + _err(nnet.nnet_last_error))
+        self.max_frames = int(max_frames)
+        self.layers = []
+        name = C.create_string_buffer(256)
+        ty, di, do = _i(), _i(), _i()
+        for i in range(nnet.nnet_num_layers(self.h)):
+            nnet.nnet_layer_info(self.h, i, name, 256, C.byref(ty), C.byref(di), C.byref(do))
+            self.layers.append((name.value.decode(), ty.value, di.value, do.value))
+        self.num_params = nnet.nnet_num_params(self.h)
+        self.params = {}
+        r, c, off = _i(), _i(), _ll()
+        for i in range(nnet.nnet_num_param_tensors(self.h)):
+            nnet.nnet_param_info(self.h, i, name, 256, C.byref(r), C.byref(c), C.byref(off))
+            self.params[name.value.decode()] = (r.value, c.value, off.value)
+        self.T = 0
+
+    def close(self):
+        if getattr(self, "h", None):
+            nnet.nnet_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # parameters --------------------------------------------------------
+    def flat_params(self, named: dict) -> np.ndarray:
+        flat = np.zeros(self.num_params, dtype=np.float32)
+        for k, (r, c, off) in self.params.items():
+            flat[off:off + r * c] = np.asarray(named[k], dtype=np.float32).reshape(-1)
+        return flat
+
+    def unflatten(self, flat: np.ndarray) -> dict:
+        return {k: flat[off:off + r * c].reshape(r, c) for k, (r, c, off) in self.params.items()}
+
+    def set_params(self, named: dict):
+        flat = self.flat_params(named)
+        check(nnet.nnet_set_params(self.h, flat.ctypes.data), "nnet_set_params")
+
+    def get_params(self) -> dict:
+        flat = np.empty(self.num_params, dtype=np.float32)
+        check(nnet.nnet_get_params(self.h, flat.ctypes.data), "nnet_get_params")
+        return self.unflatten(flat)
+
+    def set_bn(self, layer, which, mean, var, gamma, beta, eps=1e-3, target_rms=1.0):
+        arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (mean, var, gamma, beta)]
+        check(nnet.nnet_set_bn(self.h, layer.encode(), which, *[a.ctypes.data for a in arrs],
+                               float(eps), float(target_rms)), "nnet_set_bn")
+
+    # compute -----------------------------------------------------------
+    def forward(self, features_ptr, T: int):
+        check(nnet.nnet_forward(self.h, features_ptr, int(T)), "nnet_forward")
+        self.T = int(T)
+
+    def activation(self, layer: str):
+        r, c = _i(), _i()
+        p = nnet.nnet_activation(self.h, layer.encode(), C.byref(r), C.byref(c))
+        if not p:
+            raise KfError("nnet_activation: " + _err(nnet.nnet_last_error))
+        return p, r.value, c.value
+
+    def read_activation(self, layer: str) -> np.ndarray:
+        p, r, c = self.activation(layer)
+        return read_fp16(p, (r, c))
+
+    def backward(self, out_grad_ptr):
+        check(nnet.nnet_backward(self.h, out_grad_ptr), "nnet_backward")
+
+    @property
+    def grad_ptr(self):
+        return nnet.nnet_grad_buffer(self.h)
+
+    @property
+    def master_ptr(self):
+        return nnet.nnet_master_buffer(self.h)
+
+    def read_grads(self) -> dict:
+        return self.unflatten(read_f32(self.grad_ptr, (self.num_params,)))
+
+    def bind_grad_buffer(self, ptr):
+        check(nnet.nnet_bind_grad_buffer(self.h, ptr), "nnet_bind_grad_buffer")
+
+    def sgd(self, lr: float, momentum: float):
+        check(nnet.nnet_sgd(self.h, float(lr), float(momentum)), "nnet_sgd")
+
+
+def parse_summary(xconfig: str):
+    """Host-layer xconfig resolution without touching the device."""
+    n = nnet.nnet_parse_summary(xconfig.encode(), None, 0)
+    if n < 0:
+        raise KfError("nnet_parse_summary: " + _err(nnet.nnet_last_error))
+    buf = C.create_string_buffer(n)
+    nnet.nnet_parse_summary(xconfig.encode(), buf, n)
+    lines = buf.value.decode().strip().splitlines()
+    layers = [(a, int(b), int(c), int(d)) for a, b, c, d in (l.split() for l in lines[:-1])]
+    return layers, int(lines[-1].split()[1])
+
+
+def read_header_symbols(header: str):
+    """Function names declared in include/<header> (for the ABI export test)."""
+    import re
+    text = open(os.path.join(INCDIR, header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    names = re.findall(r"\b([a-z][a-z0-9_]*)\s*\([^;{]*\)\s*;", text)
+    return sorted(set(n for n in names if not n.startswith(("sizeof", "typedef"))))

@@ -1,0 +1,120 @@
+"""Synthetic model / egs generator pinned by SURVEY.md §8d and BASELINE.md §2.
+
+The reference's real model, egs and den.fst live outside its repository, so the
+benchmark and the parity tests run on this fixed synthetic setup:
+  * weights: Xavier-normal sqrt(2/(fan_in+fan_out)) from default_rng(42) in
+    parameter order (the reference's randTensor, forward.go:1161-1168), stored
+    fp16 by truncation on upload (internal/gpu/tensor.go:158-173);
+  * biases U(-0.05, 0.05) from default_rng(43) (the reference zero-initialises;
+    non-zero biases exercise the bias path);
+  * frozen BatchNorm: mean ~ N(0, 0.1^2), var ~ U(0.5, 2), gamma 1, beta 0,
+    eps 1e-3 (identityBN's eps, forward.go:1185) from default_rng(44);
+  * features x ~ N(0, 1) from default_rng(1234), fp16 round-to-nearest-even
+    (internal/fp16/fp16.go:12-70, applied by TransferBatch).
+Pure numpy; no device work.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+CONFIG_DIR = os.path.normpath(os.path.join(os.path.dirname(__file__), "..", "..", "..", "configs"))
+
+
+def load_xconfig(name: str) -> str:
+    with open(os.path.join(CONFIG_DIR, name)) as f:
+        return f.read()
+
+
+def make_params(param_shapes: dict, seed: int = 42, bias_seed: int = 43) -> dict:
+    """param_shapes: name -> (rows, cols) in the network's parameter order."""
+    rw = np.random.default_rng(seed)
+    rb = np.random.default_rng(bias_seed)
+    out = {}
+    for name, (r, c, *_rest) in param_shapes.items():
+        if name.endswith("Bias"):
+            out[name] = rb.uniform(-0.05, 0.05, size=(r, c)).astype(np.float32)
+        else:
+            scale = np.sqrt(2.0 / (r + c))
+            out[name] = (rw.standard_normal((r, c)) * scale).astype(np.float32)
+    return out
+
+
+def bn_layers(layers):
+    """(layer name, which, dim) for every frozen BatchNorm of the network."""
+    res = []
+    for name, ty, din, dout in layers:
+        if ty in (3,):  # batchnorm-component
+            res.append((name, 0, dout))
+    return res
+
+
+def make_bn(dim: int, rng) -> tuple:
+    mean = rng.normal(0.0, 0.1, size=dim).astype(np.float32)
+    var = rng.uniform(0.5, 2.0, size=dim).astype(np.float32)
+    return mean, var, np.ones(dim, np.float32), np.zeros(dim, np.float32)
+
+
+def bn_specs(net_layers, conv_fout: dict, prefinal_dims: dict):
+    """Every BatchNorm (layer, which, dim) in the order the generator draws them."""
+    specs = []
+    for name, ty, din, dout in net_layers:
+        if ty == 3:            # batchnorm-component
+            specs.append((name, 0, dout))
+        elif ty == 6:          # conv-relu-batchnorm: per filter
+            specs.append((name, 0, conv_fout[name]))
+        elif ty == 7:          # tdnnf
+            specs.append((name, 0, dout))
+        elif ty == 9:          # prefinal: big then small
+            big, small = prefinal_dims[name]
+            specs.append((name, 0, big))
+            specs.append((name, 1, small))
+    return specs
+
+
+def make_bn_all(specs, seed: int = 44) -> dict:
+    rng = np.random.default_rng(seed)
+    return {(name, which): make_bn(dim, rng) for name, which, dim in specs}
+
+
+def make_features(T: int, dim: int, seed: int = 1234) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal((T, dim)).astype(np.float32).astype(np.float16)
+
+
+def layer_dims(net):
+    """Recover per-layer structural dims from the network's parameter shapes."""
+    conv_fout, prefinal = {}, {}
+    for name, ty, din, dout in net.layers:
+        if ty == 6:
+            conv_fout[name] = net.params[name + ".W"][1]
+        if ty == 9:
+            prefinal[name] = (net.params[name + ".BigW"][1], dout)
+    return conv_fout, prefinal
+
+
+def init_network(net, seed: int = 42):
+    """Draw synthetic weights + BN statistics and load them into `net`.
+    Returns (params dict fp32 pre-truncation, bn dict)."""
+    params = make_params(net.params, seed=seed)
+    net.set_params(params)
+    conv_fout, prefinal = layer_dims(net)
+    bns = make_bn_all(bn_specs(net.layers, conv_fout, prefinal))
+    for (name, which), (m, v, g, b) in bns.items():
+        net.set_bn(name, which, m, v, g, b, eps=1e-3, target_rms=1.0)
+    return params, bns
+
+
+def trunc_fp16(a: np.ndarray) -> np.ndarray:
+    """internal/gpu/tensor.go:158-173 truncating fp32->fp16, returned as fp32 values."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    bits = a.view(np.uint32)
+    sign = ((bits >> 16) & 0x8000).astype(np.uint16)
+    exp = ((bits >> 23) & 0xFF).astype(np.int32) - 127
+    frac = bits & 0x7FFFFF
+    h = np.where(exp > 15, sign | 0x7C00,
+                 np.where(exp < -14, sign,
+                          sign | ((np.clip(exp, -14, 15) + 15).astype(np.uint16) << 10)
+                          | (frac >> 13).astype(np.uint16))).astype(np.uint16)
+    return h.view(np.float16).astype(np.float32)

@@ -1,0 +1,630 @@
+/*
+ * kf_oracle.c — CPU restatement of the reference's CNN-TDNN forward/backward.
+ *
+ * TEST INFRASTRUCTURE ONLY (see kf_oracle.h). It follows the reference's own
+ * materialising formulation — explicit time splices (forward.go:699-790),
+ * explicit im2col patches (forward.go:435-456), dense fp32-accumulated GEMMs
+ * (ops.cu:381-392) — so it shares no addressing code with the MI355X kernels
+ * that compute the same quantities implicitly.
+ *
+ * Deliberate differences from the reference's *buggy* pieces:
+ *   - conv offsets are Kaldi's cross product (time x height), output layout is
+ *     height-major [h*F + f] (Kaldi), not the reference's zipped offsets and
+ *     filter-major reorder (forward.go:442-444, :499-508);
+ *   - backward is the exact gradient of the forward (the reference's
+ *     backwardTDNNF / backwardPrefinal are inconsistent with their forward,
+ *     network_backward.go:336-463, :549-656).
+ */
+#include "kf_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------- */
+/* fp16 conversions                                                          */
+/* ------------------------------------------------------------------------- */
+static inline uint32_t f2u(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+static inline float u2f(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+/* IEEE round-to-nearest-even, as internal/fp16/fp16.go:12-70 */
+uint16_t orc_f32_to_f16_rne(float f) {
+    uint32_t b = f2u(f);
+    uint32_t sign = (b >> 31) & 1u;
+    int exp = (int)((b >> 23) & 0xFF);
+    uint32_t frac = b & 0x7FFFFFu;
+    if (exp == 255) {
+        if (frac == 0) return (uint16_t)(sign << 15 | 0x7C00u);
+        return (uint16_t)(sign << 15 | 0x7C00u | (frac >> 13));
+    }
+    if (exp > 142) return (uint16_t)(sign << 15 | 0x7C00u);
+    if (exp > 112) {
+        uint32_t e = (uint32_t)(exp - 112);
+        uint32_t round = frac & 0x1FFFu;
+        frac >>= 13;
+        if (round > 0x1000u || (round == 0x1000u && (frac & 1u))) {
+            frac++;
+            if (frac > 0x3FFu) {
+                frac = 0;
+                e++;
+                if (e > 30) return (uint16_t)(sign << 15 | 0x7C00u);
+            }
+        }
+        return (uint16_t)(sign << 15 | e << 10 | frac);
+    }
+    if (exp > 101) {
+        unsigned shift = (unsigned)(113 - exp);
+        frac |= 0x800000u;
+        uint32_t round = frac & ((1u << (shift + 13)) - 1u);
+        uint32_t half = 1u << (shift + 12);
+        frac >>= (shift + 13);
+        if (round > half || (round == half && (frac & 1u))) frac++;
+        return (uint16_t)(sign << 15 | frac);
+    }
+    return (uint16_t)(sign << 15);
+}
+
+/* truncating conversion used for weights, internal/gpu/tensor.go:158-173 */
+uint16_t orc_f32_to_f16_trunc(float f) {
+    uint32_t bits = f2u(f);
+    uint16_t sign = (uint16_t)((bits >> 16) & 0x8000u);
+    int exp = (int)((bits >> 23) & 0xFF) - 127;
+    uint32_t frac = bits & 0x7FFFFFu;
+    if (exp > 15) return sign | 0x7C00u;
+    if (exp < -14) return sign;
+    return (uint16_t)(sign | (uint16_t)((exp + 15) << 10) | (uint16_t)(frac >> 13));
+}
+
+/* internal/fp16/fp16.go:73-110 */
+float orc_f16_to_f32(uint16_t h) {
+    uint32_t sign = (uint32_t)(h >> 15) & 1u;
+    uint32_t exp = (uint32_t)(h >> 10) & 0x1Fu;
+    uint32_t frac = (uint32_t)h & 0x3FFu;
+    if (exp == 31) return u2f(sign << 31 | 0x7F800000u | (frac << 13));
+    if (exp == 0) {
+        if (frac == 0) return u2f(sign << 31);
+        while ((frac & 0x400u) == 0) {
+            frac <<= 1;
+            exp--;
+        }
+        frac &= 0x3FFu;
+        exp++;
+        return u2f(sign << 31 | (exp + 112) << 23 | frac << 13);
+    }
+    return u2f(sign << 31 | (exp + 112) << 23 | frac << 13);
+}
+
+static inline float rh(float x) { return orc_f16_to_f32(orc_f32_to_f16_rne(x)); }
+
+void orc_round_f16(float *x, long long n) {
+    for (long long i = 0; i < n; ++i) x[i] = rh(x[i]);
+}
+
+/* ------------------------------------------------------------------------- */
+/* threading: rows split over threads like gotorch's matmulParallel          */
+/* ------------------------------------------------------------------------- */
+static int g_threads = 1;
+void orc_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+int orc_get_threads(void) { return g_threads; }
+
+typedef void (*range_fn)(void *ctx, int lo, int hi);
+typedef struct {
+    range_fn fn;
+    void *ctx;
+    int lo, hi;
+} job_t;
+static void *job_run(void *p) {
+    job_t *j = (job_t *)p;
+    j->fn(j->ctx, j->lo, j->hi);
+    return NULL;
+}
+static void parallel_for(int n, range_fn fn, void *ctx) {
+    int nt = g_threads;
+    if (nt > n) nt = n;
+    if (nt <= 1) {
+        fn(ctx, 0, n);
+        return;
+    }
+    pthread_t th[256];
+    job_t jobs[256];
+    if (nt > 256) nt = 256;
+    int chunk = (n + nt - 1) / nt;
+    int used = 0;
+    for (int i = 0; i < nt; ++i) {
+        int lo = i * chunk, hi = lo + chunk < n ? lo + chunk : n;
+        if (lo >= hi) break;
+        jobs[i].fn = fn;
+        jobs[i].ctx = ctx;
+        jobs[i].lo = lo;
+        jobs[i].hi = hi;
+        pthread_create(&th[i], NULL, job_run, &jobs[i]);
+        used++;
+    }
+    for (int i = 0; i < used; ++i) pthread_join(th[i], NULL);
+}
+
+/* C = A . B  (NN), A [MxK], B [KxN] */
+typedef struct {
+    int M, N, K;
+    const float *A, *B;
+    float *C;
+} mm_t;
+static void mm_nn_rows(void *p, int lo, int hi) {
+    mm_t *m = (mm_t *)p;
+    for (int i = lo; i < hi; ++i) {
+        float *c = m->C + (size_t)i * m->N;
+        memset(c, 0, sizeof(float) * (size_t)m->N);
+        const float *a = m->A + (size_t)i * m->K;
+        for (int k = 0; k < m->K; ++k) {
+            const float av = a[k];
+            if (av == 0.f) continue;
+            const float *b = m->B + (size_t)k * m->N;
+            for (int j = 0; j < m->N; ++j) c[j] += av * b[j];
+        }
+    }
+}
+void orc_matmul(int M, int N, int K, const float *A, const float *B, float *C) {
+    mm_t m = {M, N, K, A, B, C};
+    parallel_for(M, mm_nn_rows, &m);
+}
+/* C = A . B^T, A [MxK], B [NxK] */
+static void mm_nt_rows(void *p, int lo, int hi) {
+    mm_t *m = (mm_t *)p;
+    for (int i = lo; i < hi; ++i) {
+        const float *a = m->A + (size_t)i * m->K;
+        for (int j = 0; j < m->N; ++j) {
+            const float *b = m->B + (size_t)j * m->K;
+            float s = 0.f;
+            for (int k = 0; k < m->K; ++k) s += a[k] * b[k];
+            m->C[(size_t)i * m->N + j] = s;
+        }
+    }
+}
+static void matmul_nt(int M, int N, int K, const float *A, const float *B, float *C) {
+    mm_t m = {M, N, K, A, B, C};
+    parallel_for(M, mm_nt_rows, &m);
+}
+/* C[MxN] = A^T . B, A [K x M], B [K x N]  (weight gradients; K = frames) */
+static void mm_tn_rows(void *p, int lo, int hi) {
+    mm_t *m = (mm_t *)p;
+    for (int i = lo; i < hi; ++i) memset(m->C + (size_t)i * m->N, 0, sizeof(float) * (size_t)m->N);
+    for (int k = 0; k < m->K; ++k) {
+        const float *a = m->A + (size_t)k * m->M;
+        const float *b = m->B + (size_t)k * m->N;
+        for (int i = lo; i < hi; ++i) {
+            const float av = a[i];
+            if (av == 0.f) continue;
+            float *c = m->C + (size_t)i * m->N;
+            for (int j = 0; j < m->N; ++j) c[j] += av * b[j];
+        }
+    }
+}
+static void matmul_tn(int M, int N, int K, const float *A, const float *B, float *C) {
+    mm_t m = {M, N, K, A, B, C};
+    parallel_for(M, mm_tn_rows, &m);
+}
+
+/* ------------------------------------------------------------------------- */
+/* layer pieces                                                              */
+/* ------------------------------------------------------------------------- */
+static void *xalloc(size_t n) {
+    void *p = calloc(n ? n : 1, 1);
+    return p;
+}
+
+/* ops.cu:171-204 */
+static inline float bn_apply(const OrcBN *bn, int d, float v) {
+    float norm = (v - bn->mean[d]) / sqrtf(bn->var[d] + bn->eps);
+    if (bn->target_rms != 1.0f) return norm * bn->target_rms;
+    return bn->gamma[d] * norm + bn->beta[d];
+}
+static inline float bn_scale(const OrcBN *bn, int d) {
+    if (bn->target_rms != 1.0f) return bn->target_rms / sqrtf(bn->var[d] + bn->eps);
+    return bn->gamma[d] / sqrtf(bn->var[d] + bn->eps);
+}
+
+/* spliceBackward forward.go:699-741: [x(max(t-s,0)) | x(t)] */
+static float *splice_minus(const float *x, int T, int d, int s) {
+    float *o = (float *)xalloc(sizeof(float) * (size_t)T * 2 * d);
+    for (int t = 0; t < T; ++t) {
+        int tp = t - s < 0 ? 0 : t - s;
+        memcpy(o + (size_t)t * 2 * d, x + (size_t)tp * d, sizeof(float) * d);
+        memcpy(o + (size_t)t * 2 * d + d, x + (size_t)t * d, sizeof(float) * d);
+    }
+    return o;
+}
+/* spliceForward forward.go:745-790: [x(t) | x(min(t+s,T-1))] */
+static float *splice_plus(const float *x, int T, int d, int s) {
+    float *o = (float *)xalloc(sizeof(float) * (size_t)T * 2 * d);
+    for (int t = 0; t < T; ++t) {
+        int tp = t + s > T - 1 ? T - 1 : t + s;
+        memcpy(o + (size_t)t * 2 * d, x + (size_t)t * d, sizeof(float) * d);
+        memcpy(o + (size_t)t * 2 * d + d, x + (size_t)tp * d, sizeof(float) * d);
+    }
+    return o;
+}
+/* im2col forward.go:435-456, Kaldi cross product of offsets, zero padding */
+static float *im2col(const OrcLayer *L, const float *x, int T) {
+    const int pd = L->noff * L->fin;
+    float *p = (float *)xalloc(sizeof(float) * (size_t)T * L->hout * pd);
+    for (int t = 0; t < T; ++t)
+        for (int h = 0; h < L->hout; ++h) {
+            float *row = p + ((size_t)t * L->hout + h) * pd;
+            for (int o = 0; o < L->noff; ++o) {
+                int ts = t + L->toff[o], hs = h * L->sub + L->hoff[o];
+                if (ts < 0 || ts >= T || hs < 0 || hs >= L->hin) continue;
+                memcpy(row + (size_t)o * L->fin, x + (size_t)ts * L->hin * L->fin + (size_t)hs * L->fin,
+                       sizeof(float) * L->fin);
+            }
+        }
+    return p;
+}
+static void col2im_add(const OrcLayer *L, const float *dp, int T, float *dx) {
+    const int pd = L->noff * L->fin;
+    for (int t = 0; t < T; ++t)
+        for (int h = 0; h < L->hout; ++h) {
+            const float *row = dp + ((size_t)t * L->hout + h) * pd;
+            for (int o = 0; o < L->noff; ++o) {
+                int ts = t + L->toff[o], hs = h * L->sub + L->hoff[o];
+                if (ts < 0 || ts >= T || hs < 0 || hs >= L->hin) continue;
+                float *d = dx + (size_t)ts * L->hin * L->fin + (size_t)hs * L->fin;
+                for (int f = 0; f < L->fin; ++f) d[f] += row[(size_t)o * L->fin + f];
+            }
+        }
+}
+
+/* relu + BN (+ bias) epilogue; R mode rounds after every reference op */
+static void bias_relu_bn(float *z, int rows, int D, const float *bias, const OrcBN *bn,
+                         uint8_t *mask, int mode, int relu) {
+    for (long long i = 0; i < (long long)rows * D; ++i) {
+        int d = (int)(i % D);
+        float v = z[i];
+        if (mode == ORC_ROUND_REF) v = rh(v); /* cuBLAS fp16 output */
+        if (bias) {
+            v += bias[d];
+            if (mode == ORC_ROUND_REF) v = rh(v);
+        }
+        if (relu) {
+            if (mask) mask[i] = v > 0.f;
+            if (!(v > 0.f)) v = 0.f;
+        }
+        if (bn && bn->mean) {
+            v = bn_apply(bn, d, v);
+            if (mode == ORC_ROUND_REF) v = rh(v);
+        }
+        z[i] = v;
+    }
+}
+
+static int layer_needs_dx(const OrcNet *net, int li) {
+    /* does any trainable layer lie below li on its input chain? */
+    int cur = net->layers[li].input;
+    while (cur >= 0) {
+        int ty = net->layers[cur].type;
+        if (ty == ORC_CONV || ty == ORC_TDNNF || ty == ORC_LINEAR || ty == ORC_PREFINAL ||
+            ty == ORC_OUTPUT)
+            return 1;
+        cur = net->layers[cur].input;
+    }
+    return 0;
+}
+
+static void alloc_net(OrcNet *net) {
+    int n = net->nlayers;
+    net->act = (float **)xalloc(sizeof(float *) * n);
+    net->mask = (uint8_t **)xalloc(sizeof(uint8_t *) * n);
+    net->aux = (float **)xalloc(sizeof(float *) * n);
+    net->gW = (float **)xalloc(sizeof(float *) * n);
+    net->gb = (float **)xalloc(sizeof(float *) * n);
+    net->gW2 = (float **)xalloc(sizeof(float *) * n);
+    net->gb2 = (float **)xalloc(sizeof(float *) * n);
+    net->gact = (float **)xalloc(sizeof(float *) * n);
+}
+
+int orc_net_forward(OrcNet *net, const float *features) {
+    const int T = net->T, mode = net->round_mode;
+    if (!net->act) alloc_net(net);
+    for (int li = 0; li < net->nlayers; ++li) {
+        const OrcLayer *L = &net->layers[li];
+        const float *x = L->input < 0 ? features : net->act[L->input];
+        const int din = L->in_dim, dout = L->out_dim;
+        float *y = (float *)xalloc(sizeof(float) * (size_t)T * dout);
+        switch (L->type) {
+            case ORC_IDCT:
+                orc_matmul(T, dout, din, x, L->W, y);
+                if (mode) orc_round_f16(y, (long long)T * dout);
+                break;
+            case ORC_BATCHNORM:
+                for (long long i = 0; i < (long long)T * dout; ++i) y[i] = bn_apply(&L->bn, (int)(i % dout), x[i]);
+                if (mode) orc_round_f16(y, (long long)T * dout);
+                break;
+            case ORC_CONV: {
+                float *p = im2col(L, x, T);
+                orc_matmul(T * L->hout, L->fout, L->noff * L->fin, p, L->W, y);
+                free(p);
+                net->mask[li] = (uint8_t *)xalloc((size_t)T * dout);
+                bias_relu_bn(y, T * L->hout, L->fout, L->b, &L->bn, net->mask[li], mode, 1);
+                if (mode) orc_round_f16(y, (long long)T * dout);
+                break;
+            }
+            case ORC_TDNNF: {
+                const int s = L->stride, bn = L->bn_dim;
+                const float *lin_in = x;
+                float *tmp = NULL;
+                if (s > 0) lin_in = tmp = splice_minus(x, T, din, s);
+                float *bott = (float *)xalloc(sizeof(float) * (size_t)T * bn);
+                orc_matmul(T, bn, s > 0 ? 2 * din : din, lin_in, L->W, bott);
+                free(tmp);
+                if (mode) orc_round_f16(bott, (long long)T * bn);
+                const float *aff_in = bott;
+                tmp = NULL;
+                if (s > 0) aff_in = tmp = splice_plus(bott, T, bn, s);
+                orc_matmul(T, dout, s > 0 ? 2 * bn : bn, aff_in, L->W2, y);
+                free(tmp);
+                net->mask[li] = (uint8_t *)xalloc((size_t)T * dout);
+                bias_relu_bn(y, T, dout, L->b2, &L->bn, net->mask[li], mode, 1);
+                if (L->bypass > 0.f && din == dout) {
+                    for (long long i = 0; i < (long long)T * dout; ++i) {
+                        float v = y[i] + L->bypass * x[i];
+                        y[i] = mode == ORC_ROUND_REF ? rh(v) : v;
+                    }
+                }
+                if (mode) orc_round_f16(y, (long long)T * dout);
+                net->aux[li] = bott;
+                break;
+            }
+            case ORC_LINEAR:
+                orc_matmul(T, dout, din, x, L->W, y);
+                if (mode) orc_round_f16(y, (long long)T * dout);
+                break;
+            case ORC_PREFINAL: {
+                const int big = L->big_dim, small = L->small_dim;
+                float *bg = (float *)xalloc(sizeof(float) * (size_t)T * big);
+                orc_matmul(T, big, din, x, L->W, bg);
+                net->mask[li] = (uint8_t *)xalloc((size_t)T * big);
+                bias_relu_bn(bg, T, big, L->b, &L->bn, net->mask[li], mode, 1);
+                if (mode) orc_round_f16(bg, (long long)T * big);
+                orc_matmul(T, small, big, bg, L->W2, y);
+                bias_relu_bn(y, T, small, NULL, &L->bn2, NULL, mode, 0);
+                if (mode) orc_round_f16(y, (long long)T * small);
+                net->aux[li] = bg;
+                break;
+            }
+            case ORC_OUTPUT:
+                orc_matmul(T, dout, din, x, L->W, y);
+                bias_relu_bn(y, T, dout, L->b, NULL, NULL, mode, 0);
+                if (mode) orc_round_f16(y, (long long)T * dout);
+                break;
+            default:
+                free(y);
+                return -1;
+        }
+        net->act[li] = y;
+    }
+    return 0;
+}
+
+static float *colsum(const float *g, int rows, int D) {
+    float *s = (float *)xalloc(sizeof(float) * D);
+    for (int r = 0; r < rows; ++r)
+        for (int d = 0; d < D; ++d) s[d] += g[(size_t)r * D + d];
+    return s;
+}
+
+/*
+ * Exact backward. v[li] is the fp32 (unrounded) gradient w.r.t. layer li's
+ * output; the MI355X build stores g = rne(v) and dz = rne(v * bnscale * mask),
+ * and this restatement rounds at exactly those tensors in F mode.
+ */
+int orc_net_backward(OrcNet *net, const float *features, const float *out_grad) {
+    const int T = net->T, mode = net->round_mode;
+    const int n = net->nlayers;
+    float **v = (float **)xalloc(sizeof(float *) * n);
+    {
+        const OrcLayer *top = &net->layers[n - 1];
+        v[n - 1] = (float *)xalloc(sizeof(float) * (size_t)T * top->out_dim);
+        memcpy(v[n - 1], out_grad, sizeof(float) * (size_t)T * top->out_dim);
+    }
+    for (int li = n - 1; li >= 0; --li) {
+        const OrcLayer *L = &net->layers[li];
+        if (!v[li]) continue;
+        const int din = L->in_dim, dout = L->out_dim;
+        const float *x = L->input < 0 ? features : net->act[L->input];
+        const int need_dx = layer_needs_dx(net, li);
+        float *g = v[li];
+        /* stored gradient of this layer's output */
+        float *gr = (float *)xalloc(sizeof(float) * (size_t)T * dout);
+        memcpy(gr, g, sizeof(float) * (size_t)T * dout);
+        if (mode) orc_round_f16(gr, (long long)T * dout);
+        net->gact[li] = gr;
+        float *dx = NULL;
+        switch (L->type) {
+            case ORC_OUTPUT:
+            case ORC_LINEAR: {
+                const float *dz = gr;
+                net->gW[li] = (float *)xalloc(sizeof(float) * (size_t)din * dout);
+                matmul_tn(din, dout, T, x, dz, net->gW[li]);
+                if (L->type == ORC_OUTPUT) net->gb[li] = colsum(dz, T, dout);
+                if (need_dx) {
+                    dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
+                    matmul_nt(T, din, dout, dz, L->W, dx); /* W [din x dout] viewed as B^T */
+                }
+                break;
+            }
+            case ORC_CONV: {
+                float *dz = (float *)xalloc(sizeof(float) * (size_t)T * dout);
+                for (long long i = 0; i < (long long)T * dout; ++i) {
+                    int f = (int)(i % L->fout);
+                    dz[i] = net->mask[li][i] ? g[i] * bn_scale(&L->bn, f) : 0.f;
+                }
+                if (mode) orc_round_f16(dz, (long long)T * dout);
+                const int pd = L->noff * L->fin, rows = T * L->hout;
+                float *p = im2col(L, x, T);
+                net->gW[li] = (float *)xalloc(sizeof(float) * (size_t)pd * L->fout);
+                matmul_tn(pd, L->fout, rows, p, dz, net->gW[li]);
+                free(p);
+                net->gb[li] = colsum(dz, rows, L->fout);
+                if (need_dx) {
+                    float *dp = (float *)xalloc(sizeof(float) * (size_t)rows * pd);
+                    matmul_nt(rows, pd, L->fout, dz, L->W, dp);
+                    dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
+                    col2im_add(L, dp, T, dx);
+                    free(dp);
+                }
+                free(dz);
+                break;
+            }
+            case ORC_TDNNF: {
+                const int s = L->stride, bn = L->bn_dim;
+                float *dz = (float *)xalloc(sizeof(float) * (size_t)T * dout);
+                for (long long i = 0; i < (long long)T * dout; ++i) {
+                    int d = (int)(i % dout);
+                    dz[i] = net->mask[li][i] ? g[i] * bn_scale(&L->bn, d) : 0.f;
+                }
+                if (mode) orc_round_f16(dz, (long long)T * dout);
+                const float *bott = net->aux[li];
+                const int kaff = s > 0 ? 2 * bn : bn, klin = s > 0 ? 2 * din : din;
+                float *aff_in = s > 0 ? splice_plus(bott, T, bn, s) : (float *)bott;
+                net->gW2[li] = (float *)xalloc(sizeof(float) * (size_t)kaff * dout);
+                matmul_tn(kaff, dout, T, aff_in, dz, net->gW2[li]);
+                if (s > 0) free(aff_in);
+                net->gb2[li] = colsum(dz, T, dout);
+                float *daff = (float *)xalloc(sizeof(float) * (size_t)T * kaff);
+                matmul_nt(T, kaff, dout, dz, L->W2, daff);
+                float *dbott = (float *)xalloc(sizeof(float) * (size_t)T * bn);
+                for (int t = 0; t < T; ++t)
+                    for (int c = 0; c < bn; ++c) dbott[(size_t)t * bn + c] += daff[(size_t)t * kaff + c];
+                if (s > 0)
+                    for (int t = 0; t < T; ++t) {
+                        int tp = t + s > T - 1 ? T - 1 : t + s;
+                        for (int c = 0; c < bn; ++c)
+                            dbott[(size_t)tp * bn + c] += daff[(size_t)t * kaff + bn + c];
+                    }
+                free(daff);
+                if (mode) orc_round_f16(dbott, (long long)T * bn);
+                float *lin_in = s > 0 ? splice_minus(x, T, din, s) : (float *)x;
+                net->gW[li] = (float *)xalloc(sizeof(float) * (size_t)klin * bn);
+                matmul_tn(klin, bn, T, lin_in, dbott, net->gW[li]);
+                if (s > 0) free(lin_in);
+                if (need_dx) {
+                    float *dlin = (float *)xalloc(sizeof(float) * (size_t)T * klin);
+                    matmul_nt(T, klin, bn, dbott, L->W, dlin);
+                    dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
+                    if (s > 0) {
+                        for (int t = 0; t < T; ++t) {
+                            int tp = t - s < 0 ? 0 : t - s;
+                            for (int c = 0; c < din; ++c) {
+                                dx[(size_t)t * din + c] += dlin[(size_t)t * klin + din + c];
+                                dx[(size_t)tp * din + c] += dlin[(size_t)t * klin + c];
+                            }
+                        }
+                    } else {
+                        memcpy(dx, dlin, sizeof(float) * (size_t)T * din);
+                    }
+                    free(dlin);
+                    if (L->bypass > 0.f && din == dout)
+                        for (long long i = 0; i < (long long)T * din; ++i) dx[i] += L->bypass * gr[i];
+                }
+                free(dbott);
+                free(dz);
+                break;
+            }
+            case ORC_PREFINAL: {
+                const int big = L->big_dim, small = L->small_dim;
+                float *ds = (float *)xalloc(sizeof(float) * (size_t)T * small);
+                for (long long i = 0; i < (long long)T * small; ++i) {
+                    int d = (int)(i % small);
+                    ds[i] = L->bn2.mean ? g[i] * bn_scale(&L->bn2, d) : g[i];
+                }
+                if (mode) orc_round_f16(ds, (long long)T * small);
+                const float *bg = net->aux[li];
+                net->gW2[li] = (float *)xalloc(sizeof(float) * (size_t)big * small);
+                matmul_tn(big, small, T, bg, ds, net->gW2[li]);
+                float *dbig = (float *)xalloc(sizeof(float) * (size_t)T * big);
+                matmul_nt(T, big, small, ds, L->W2, dbig);
+                for (long long i = 0; i < (long long)T * big; ++i) {
+                    int d = (int)(i % big);
+                    dbig[i] = net->mask[li][i] ? dbig[i] * bn_scale(&L->bn, d) : 0.f;
+                }
+                if (mode) orc_round_f16(dbig, (long long)T * big);
+                net->gW[li] = (float *)xalloc(sizeof(float) * (size_t)din * big);
+                matmul_tn(din, big, T, x, dbig, net->gW[li]);
+                net->gb[li] = colsum(dbig, T, big);
+                if (need_dx) {
+                    dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
+                    matmul_nt(T, din, big, dbig, L->W, dx);
+                }
+                free(dbig);
+                free(ds);
+                break;
+            }
+            case ORC_BATCHNORM:
+                if (need_dx) {
+                    dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
+                    for (long long i = 0; i < (long long)T * din; ++i)
+                        dx[i] = g[i] * bn_scale(&L->bn, (int)(i % din));
+                }
+                break;
+            case ORC_IDCT:
+                if (need_dx) {
+                    dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
+                    matmul_nt(T, din, dout, g, L->W, dx);
+                }
+                break;
+            default:
+                break;
+        }
+        if (dx && L->input >= 0) {
+            if (v[L->input]) {
+                for (long long i = 0; i < (long long)T * din; ++i) v[L->input][i] += dx[i];
+                free(dx);
+            } else {
+                v[L->input] = dx;
+            }
+        } else {
+            free(dx);
+        }
+    }
+    for (int i = 0; i < n; ++i) free(v[i]);
+    free(v);
+    return 0;
+}
+
+void orc_net_free(OrcNet *net) {
+    if (!net->act) return;
+    for (int i = 0; i < net->nlayers; ++i) {
+        free(net->act[i]);
+        free(net->mask[i]);
+        free(net->aux[i]);
+        free(net->gW[i]);
+        free(net->gb[i]);
+        free(net->gW2[i]);
+        free(net->gb2[i]);
+        free(net->gact[i]);
+    }
+    free(net->act);
+    free(net->mask);
+    free(net->aux);
+    free(net->gW);
+    free(net->gb);
+    free(net->gW2);
+    free(net->gb2);
+    free(net->gact);
+    net->act = NULL;
+}
+
+void orc_sgd(float *w32, const float *g, float *v, float lr, float mom, long long n) {
+    for (long long i = 0; i < n; ++i) {
+        v[i] = mom * v[i] + g[i];
+        w32[i] -= lr * v[i];
+    }
+}

@@ -1,0 +1,99 @@
+/*
+ * kf_oracle.h — CPU restatement of the reference's CNN-TDNN hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker
+ * (or the timed CPU baseline) — never as the product path.
+ *
+ * Plain C, float32 arithmetic (fp32 accumulation, as cublasGemmEx with
+ * CUBLAS_COMPUTE_32F in cpp/cuda/ops.cu:381-392), with fp16 rounding applied at
+ * tensor boundaries. Two rounding modes:
+ *   ORC_ROUND_FUSED (F): round to fp16 once per stored tensor, where the MI355X
+ *                        build stores fp16 tensors;
+ *   ORC_ROUND_REF   (R): round after every reference op, as the reference's
+ *                        chain of cuBLAS + element-wise kernels does
+ *                        (internal/nnet/forward.go:589-695, ops.cu:26-228).
+ * Parity pinning: see oracle/README in DESIGN.md §Oracle.
+ */
+#ifndef KF_ORACLE_H
+#define KF_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* fp16 conversions */
+uint16_t orc_f32_to_f16_rne(float f);     /* internal/fp16/fp16.go:12-70 */
+uint16_t orc_f32_to_f16_trunc(float f);   /* internal/gpu/tensor.go:158-173 */
+float orc_f16_to_f32(uint16_t h);         /* internal/fp16/fp16.go:73-110 */
+void orc_round_f16(float *x, long long n); /* x = f32(rne(x)) in place */
+void orc_set_threads(int n);
+int orc_get_threads(void);
+
+/* C[MxN] = A[MxK] . B[KxN] (fp32), rows split over threads (go/gotorch/ops.go:49-81) */
+void orc_matmul(int M, int N, int K, const float *A, const float *B, float *C);
+
+enum {
+    ORC_IDCT = 1,
+    ORC_BATCHNORM = 2,
+    ORC_CONV = 3,
+    ORC_TDNNF = 4,
+    ORC_LINEAR = 5,
+    ORC_PREFINAL = 6,
+    ORC_OUTPUT = 7,
+};
+enum { ORC_ROUND_NONE = 0, ORC_ROUND_FUSED = 1, ORC_ROUND_REF = 2 };
+
+typedef struct {
+    const float *mean, *var, *gamma, *beta; /* [dim] */
+    float eps, target_rms;
+} OrcBN;
+
+typedef struct {
+    int type;
+    int input;        /* index of input layer, -1 = features */
+    int in_dim, out_dim;
+    /* conv (forward.go:418-524 with Kaldi cross-product offsets) */
+    int hin, hout, sub, fin, fout, noff;
+    int toff[9], hoff[9];
+    /* tdnnf (forward.go:589-695) */
+    int bn_dim, stride;
+    float bypass;
+    /* prefinal (forward.go:912-968): big then small */
+    int small_dim, big_dim;
+    /* parameters (host fp32, values already fp16-representable) */
+    const float *W;   /* conv [noff*fin x fout]; tdnnf LinearW; linear/output W; prefinal BigW; idct M */
+    const float *b;   /* conv / output bias; prefinal BigBias */
+    const float *W2;  /* tdnnf AffineW; prefinal SmallW */
+    const float *b2;  /* tdnnf AffineBias */
+    OrcBN bn;         /* conv / tdnnf / batchnorm-component / prefinal BN1 */
+    OrcBN bn2;        /* prefinal BN2 (small dim); mean==NULL -> none */
+} OrcLayer;
+
+typedef struct {
+    int nlayers;
+    const OrcLayer *layers;
+    int T;            /* frames */
+    int feat_dim;
+    int round_mode;
+    /* outputs, allocated by the oracle (orc_net_free) */
+    float **act;      /* [nlayers] forward outputs [T x out_dim] */
+    uint8_t **mask;   /* [nlayers] relu masks (1 byte per element) */
+    float **aux;      /* [nlayers] tdnnf bottleneck / prefinal big */
+    float **gW, **gb, **gW2, **gb2; /* [nlayers] parameter gradients (fp32) */
+    float **gact;     /* [nlayers] gradient w.r.t. each layer's output */
+} OrcNet;
+
+int orc_net_forward(OrcNet *net, const float *features);
+/* out_grad [T x out_dim(last)], already fp16-representable */
+int orc_net_backward(OrcNet *net, const float *features, const float *out_grad);
+void orc_net_free(OrcNet *net);
+
+/* v = mom*v + g; w32 -= lr*v (backward_wrappers.cu:129-142) */
+void orc_sgd(float *w32, const float *g, float *v, float lr, float mom, long long n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,282 @@
+"""oracle.py — ctypes driver of the CPU oracle (kf_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, as the checker / CPU baseline. The product path
+never loads it.
+
+It parses the xconfig on its own (a restatement of internal/nnet/xconfig.go's
+key=value grammar and layers.go's dimension rules, independent of the C++ host
+layer under test) and builds the oracle's layer table from named parameters.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+
+
+def build(native: bool = False) -> str:
+    env = dict(os.environ)
+    if native:
+        env["ORACLE_NATIVE"] = "1"
+    subprocess.run(["make", "-s", "-C", HERE], check=True, env=env)
+    return os.path.join(BUILD, "libkforacle_native.so" if native else "libkforacle.so")
+
+
+_lib = None
+
+
+def lib(native: bool = False):
+    global _lib
+    if _lib is None:
+        path = os.path.join(BUILD, "libkforacle_native.so" if native else "libkforacle.so")
+        if not os.path.exists(path):
+            path = build(native)
+        _lib = C.CDLL(path)
+        _lib.orc_f32_to_f16_rne.restype = C.c_uint16
+        _lib.orc_f32_to_f16_rne.argtypes = [C.c_float]
+        _lib.orc_f32_to_f16_trunc.restype = C.c_uint16
+        _lib.orc_f32_to_f16_trunc.argtypes = [C.c_float]
+        _lib.orc_f16_to_f32.restype = C.c_float
+        _lib.orc_f16_to_f32.argtypes = [C.c_uint16]
+        _lib.orc_set_threads.argtypes = [C.c_int]
+        _lib.orc_matmul.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib.orc_net_forward.argtypes = [C.c_void_p, C.c_void_p]
+        _lib.orc_net_backward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib.orc_net_free.argtypes = [C.c_void_p]
+        _lib.orc_sgd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_longlong]
+    return _lib
+
+
+ORC = dict(IDCT=1, BATCHNORM=2, CONV=3, TDNNF=4, LINEAR=5, PREFINAL=6, OUTPUT=7)
+ROUND_NONE, ROUND_FUSED, ROUND_REF = 0, 1, 2
+
+_fp = C.POINTER(C.c_float)
+
+
+class OrcBN(C.Structure):
+    _fields_ = [("mean", _fp), ("var", _fp), ("gamma", _fp), ("beta", _fp),
+                ("eps", C.c_float), ("target_rms", C.c_float)]
+
+
+class OrcLayer(C.Structure):
+    _fields_ = [("type", C.c_int), ("input", C.c_int), ("in_dim", C.c_int), ("out_dim", C.c_int),
+                ("hin", C.c_int), ("hout", C.c_int), ("sub", C.c_int), ("fin", C.c_int),
+                ("fout", C.c_int), ("noff", C.c_int), ("toff", C.c_int * 9), ("hoff", C.c_int * 9),
+                ("bn_dim", C.c_int), ("stride", C.c_int), ("bypass", C.c_float),
+                ("small_dim", C.c_int), ("big_dim", C.c_int),
+                ("W", _fp), ("b", _fp), ("W2", _fp), ("b2", _fp), ("bn", OrcBN), ("bn2", OrcBN)]
+
+
+class OrcNet(C.Structure):
+    _fields_ = [("nlayers", C.c_int), ("layers", C.POINTER(OrcLayer)), ("T", C.c_int),
+                ("feat_dim", C.c_int), ("round_mode", C.c_int),
+                ("act", C.POINTER(_fp)), ("mask", C.POINTER(C.POINTER(C.c_uint8))),
+                ("aux", C.POINTER(_fp)), ("gW", C.POINTER(_fp)), ("gb", C.POINTER(_fp)),
+                ("gW2", C.POINTER(_fp)), ("gb2", C.POINTER(_fp)), ("gact", C.POINTER(_fp))]
+
+
+def parse_xconfig(text: str):
+    """Minimal restatement of xconfig.go + layers.go for the layer kinds in configs/."""
+    layers, dims, prev = [], {}, None
+    for raw in text.splitlines():
+        line = raw.strip()
+        if not line or line.startswith("#"):
+            continue
+        toks = line.split()
+        kind, kv = toks[0], dict(t.split("=", 1) for t in toks[1:] if "=" in t)
+        name = kv.get("name")
+        inp = kv.get("input", prev)
+        if kind == "input":
+            dims[name] = int(kv["dim"])
+            prev = name
+            continue
+        din = dims[inp]
+        L = dict(kind=kind, name=name, input=inp, in_dim=din, kv=kv)
+        if kind == "idct-layer":
+            L["out_dim"] = int(kv.get("dim", din))
+        elif kind == "batchnorm-component":
+            L["out_dim"] = din
+        elif kind == "conv-relu-batchnorm-layer":
+            hin = int(kv["height-in"])
+            L.update(hin=hin, hout=int(kv.get("height-out", hin)), sub=int(kv.get("height-subsample-out", 1)),
+                     fout=int(kv["num-filters-out"]), fin=din // hin,
+                     toffs=[int(x) for x in kv["time-offsets"].split(",")],
+                     hoffs=[int(x) for x in kv["height-offsets"].split(",")])
+            L["out_dim"] = L["hout"] * L["fout"]
+        elif kind == "tdnnf-layer":
+            L.update(out_dim=int(kv["dim"]), bn_dim=int(kv["bottleneck-dim"]),
+                     stride=int(kv.get("time-stride", 3)), bypass=float(kv.get("bypass-scale", 0.66)))
+        elif kind == "linear-component":
+            L["out_dim"] = int(kv["dim"])
+        elif kind == "prefinal-layer":
+            L.update(small_dim=int(kv["small-dim"]), big_dim=int(kv["big-dim"]), out_dim=int(kv["small-dim"]))
+        elif kind == "output-layer":
+            L["out_dim"] = int(kv["dim"])
+        else:
+            raise ValueError(f"oracle: unsupported layer kind {kind}")
+        dims[name] = L["out_dim"]
+        prev = name
+        layers.append(L)
+    return layers
+
+
+def idct_matrix(dim: int, lifter: float) -> np.ndarray:
+    """makeIDCTMatrix, forward.go:1190-1210 (float64 then float32)."""
+    m = np.zeros((dim, dim), np.float64)
+    for i in range(dim):
+        for j in range(dim):
+            v = np.cos(np.pi * j * (i + 0.5) / dim) * (np.sqrt(1.0 / dim) if j == 0 else np.sqrt(2.0 / dim))
+            if lifter > 0 and j > 0:
+                v *= 1.0 + (lifter / 2.0) * np.sin(np.pi * j / lifter)
+            m[i, j] = v
+    return m.astype(np.float32)
+
+
+def trunc_fp16_vals(a):
+    from_bits = np.vectorize(lambda x: lib().orc_f32_to_f16_trunc(float(x)), otypes=[np.uint16])
+    return from_bits(np.asarray(a, np.float32)).view(np.float16).astype(np.float32)
+
+
+class OracleNet:
+    """The CPU restatement of Network.Forward / Backward on given parameters.
+
+    params: name -> fp32 array, already fp16-representable (truncated) values;
+    bns: (layer, which) -> (mean, var, gamma, beta)."""
+
+    def __init__(self, xconfig: str, params: dict, bns: dict, round_mode=ROUND_FUSED, threads=None):
+        self.L = parse_xconfig(xconfig)
+        self.keep = []
+        index = {}
+        arr = (OrcLayer * len(self.L))()
+        for i, L in enumerate(self.L):
+            o = arr[i]
+            o.input = index.get(L["input"], -1)
+            o.in_dim, o.out_dim = L["in_dim"], L["out_dim"]
+            kind = L["kind"]
+            if kind == "idct-layer":
+                o.type = ORC["IDCT"]
+                M = trunc_fp16_vals(idct_matrix(L["out_dim"], float(L["kv"].get("cepstral-lifter", 22))))
+                o.W = self._p(M)
+            elif kind == "batchnorm-component":
+                o.type = ORC["BATCHNORM"]
+                o.bn = self._bn(bns.get((L["name"], 0)), L["out_dim"], float(L["kv"].get("target-rms", 1.0)))
+            elif kind == "conv-relu-batchnorm-layer":
+                o.type = ORC["CONV"]
+                offs = [(a, b) for a in L["toffs"] for b in L["hoffs"]]
+                o.hin, o.hout, o.sub, o.fin, o.fout, o.noff = L["hin"], L["hout"], L["sub"], L["fin"], L["fout"], len(offs)
+                for k, (a, b) in enumerate(offs):
+                    o.toff[k], o.hoff[k] = a, b
+                o.W, o.b = self._p(params[L["name"] + ".W"]), self._p(params[L["name"] + ".Bias"])
+                o.bn = self._bn(bns.get((L["name"], 0)), L["fout"])
+            elif kind == "tdnnf-layer":
+                o.type = ORC["TDNNF"]
+                o.bn_dim, o.stride, o.bypass = L["bn_dim"], L["stride"], L["bypass"]
+                n = L["name"]
+                o.W, o.W2, o.b2 = self._p(params[n + ".LinearW"]), self._p(params[n + ".AffineW"]), self._p(params[n + ".AffineBias"])
+                o.bn = self._bn(bns.get((n, 0)), L["out_dim"])
+            elif kind == "linear-component":
+                o.type = ORC["LINEAR"]
+                o.W = self._p(params[L["name"] + ".W"])
+            elif kind == "prefinal-layer":
+                o.type = ORC["PREFINAL"]
+                n = L["name"]
+                o.small_dim, o.big_dim = L["small_dim"], L["big_dim"]
+                o.W, o.b, o.W2 = self._p(params[n + ".BigW"]), self._p(params[n + ".BigBias"]), self._p(params[n + ".SmallW"])
+                o.bn = self._bn(bns.get((n, 0)), L["big_dim"])
+                if (n, 1) in bns:
+                    o.bn2 = self._bn(bns[(n, 1)], L["small_dim"])
+            elif kind == "output-layer":
+                o.type = ORC["OUTPUT"]
+                o.W, o.b = self._p(params[L["name"] + ".W"]), self._p(params[L["name"] + ".Bias"])
+            index[L["name"]] = i
+        self.arr = arr
+        self.index = index
+        self.round_mode = round_mode
+        if threads:
+            lib().orc_set_threads(int(threads))
+        self.net = None
+
+    def _p(self, a):
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        self.keep.append(a)
+        return a.ctypes.data_as(_fp)
+
+    def _bn(self, spec, dim, target_rms=1.0):
+        if spec is None:
+            spec = (np.zeros(dim, np.float32), np.ones(dim, np.float32), np.ones(dim, np.float32), np.zeros(dim, np.float32))
+        m, v, g, b = spec
+        return OrcBN(self._p(m), self._p(v), self._p(g), self._p(b), 1e-3, target_rms)
+
+    def forward(self, features: np.ndarray):
+        x = np.ascontiguousarray(features, dtype=np.float32)
+        self.x = x
+        if self.net is not None:
+            lib().orc_net_free(C.byref(self.net))
+        self.net = OrcNet()
+        self.net.nlayers = len(self.L)
+        self.net.layers = self.arr
+        self.net.T = x.shape[0]
+        self.net.feat_dim = x.shape[1]
+        self.net.round_mode = self.round_mode
+        rc = lib().orc_net_forward(C.byref(self.net), x.ctypes.data)
+        assert rc == 0
+
+    def act(self, name):
+        i = self.index[name]
+        T, d = self.net.T, self.L[i]["out_dim"]
+        return np.ctypeslib.as_array(self.net.act[i], shape=(T * d,)).reshape(T, d).copy()
+
+    def backward(self, out_grad: np.ndarray):
+        g = np.ascontiguousarray(out_grad, dtype=np.float32)
+        rc = lib().orc_net_backward(C.byref(self.net), self.x.ctypes.data, g.ctypes.data)
+        assert rc == 0
+
+    def grads(self) -> dict:
+        """Gradients keyed by the product's parameter names."""
+        out = {}
+        T = self.net.T
+
+        def get(ptrs, i, n):
+            p = ptrs[i]
+            return None if not p else np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+        for i, L in enumerate(self.L):
+            k, n = L["kind"], L["name"]
+            if k == "conv-relu-batchnorm-layer":
+                K = len(L["toffs"]) * len(L["hoffs"]) * L["fin"]
+                out[n + ".W"] = get(self.net.gW, i, K * L["fout"]).reshape(K, L["fout"])
+                out[n + ".Bias"] = get(self.net.gb, i, L["fout"]).reshape(1, -1)
+            elif k == "tdnnf-layer":
+                s, din, bn, dout = L["stride"], L["in_dim"], L["bn_dim"], L["out_dim"]
+                kl, ka = (2 * din if s > 0 else din), (2 * bn if s > 0 else bn)
+                out[n + ".LinearW"] = get(self.net.gW, i, kl * bn).reshape(kl, bn)
+                out[n + ".AffineW"] = get(self.net.gW2, i, ka * dout).reshape(ka, dout)
+                out[n + ".AffineBias"] = get(self.net.gb2, i, dout).reshape(1, -1)
+            elif k == "linear-component":
+                out[n + ".W"] = get(self.net.gW, i, L["in_dim"] * L["out_dim"]).reshape(L["in_dim"], L["out_dim"])
+            elif k == "prefinal-layer":
+                big, small, din = L["big_dim"], L["small_dim"], L["in_dim"]
+                out[n + ".BigW"] = get(self.net.gW, i, din * big).reshape(din, big)
+                out[n + ".BigBias"] = get(self.net.gb, i, big).reshape(1, -1)
+                out[n + ".SmallW"] = get(self.net.gW2, i, big * small).reshape(big, small)
+            elif k == "output-layer":
+                out[n + ".W"] = get(self.net.gW, i, L["in_dim"] * L["out_dim"]).reshape(L["in_dim"], L["out_dim"])
+                out[n + ".Bias"] = get(self.net.gb, i, L["out_dim"]).reshape(1, -1)
+        return out
+
+    def close(self):
+        if self.net is not None:
+            lib().orc_net_free(C.byref(self.net))
+            self.net = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,129 @@
+"""HIP path vs the CPU oracle, through the C-ABI (SURVEY §8d tolerances).
+
+Activations: rel-Frobenius <= 2e-3 and max-abs <= 1e-2 * max|ref| against the
+oracle's fused-rounding mode (F); rel-Frobenius <= 1e-2 against the reference's
+round-after-every-op mode (R). Weight gradients: rel-Frobenius <= 5e-3.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import max_abs_rel, rel_fro
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_product(kfp16, xcfg, T, seed=42, out_grad=None):
+    from kfp16 import synth
+    net = kfp16.Network(xcfg, max_frames=T)
+    params, bns = synth.init_network(net, seed=seed)
+    feats = synth.make_features(T, 40)
+    fbuf = kfp16.upload_fp16(feats)
+    net.forward(fbuf.ptr, T)
+    return net, params, bns, feats, fbuf
+
+
+def _oracle(xcfg, params, bns, feats, mode=oracle.ROUND_FUSED):
+    from kfp16 import synth
+    tp = {k: synth.trunc_fp16(v) for k, v in params.items()}   # weights enter by truncation
+    on = oracle.OracleNet(xcfg, tp, bns, round_mode=mode, threads=16)
+    on.forward(feats.astype(np.float32))
+    return on
+
+
+def test_ops_gemm_matches_fp32(gpu):
+    kfp16 = gpu
+    rng = np.random.default_rng(3)
+    h = kfp16.core.ops_cublas_create()
+    for (M, N, K, alpha, beta) in [(256, 128, 64, 1.0, 0.0), (300, 3080, 256, 1.0, 0.0),
+                                   (1, 64, 96000, 1.0, 0.0), (130, 160, 3072, 0.5, 1.0),
+                                   (37, 24, 9, 1.0, 0.0), (64, 40, 40, 2.0, -1.0)]:
+        A = rng.standard_normal((M, K)).astype(np.float16)
+        B = (rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float16)
+        C0 = rng.standard_normal((M, N)).astype(np.float16)
+        dA, dB, dC = kfp16.upload_fp16(A), kfp16.upload_fp16(B), kfp16.upload_fp16(C0)
+        kfp16.check(kfp16.core.ops_gemm(h, M, N, K, alpha, dA.ptr, K, dB.ptr, N, beta, dC.ptr, N), "gemm")
+        got = kfp16.read_fp16(dC.ptr, (M, N)).astype(np.float64)
+        ref = alpha * (A.astype(np.float64) @ B.astype(np.float64)) + beta * C0.astype(np.float64)
+        tol = 2 * np.abs(ref) * 2 ** -11 + 1e-6 * K * np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64) + 1e-3
+        assert np.all(np.abs(got - ref) <= tol), (M, N, K, float(np.max(np.abs(got - ref) - tol)))
+    kfp16.core.ops_cublas_destroy(h)
+
+
+@pytest.mark.parametrize("T", [150, 517])
+def test_tiny_network_forward_backward(gpu, T):
+    kfp16 = gpu
+    from kfp16 import synth
+    xcfg = synth.load_xconfig("tiny.xconfig")
+    net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
+    on = _oracle(xcfg, params, bns, feats)
+    onr = _oracle(xcfg, params, bns, feats, oracle.ROUND_REF)
+    for name, ty, din, dout in net.layers:
+        got = net.read_activation(name).astype(np.float32)
+        ref = on.act(name)
+        assert rel_fro(got, ref) <= 2e-3, (name, rel_fro(got, ref))
+        assert max_abs_rel(got, ref) <= 1e-2, (name, max_abs_rel(got, ref))
+        assert rel_fro(got, onr.act(name)) <= 1e-2, (name, "vs R mode")
+    # backward from a fixed fp16 output gradient
+    P = net.layers[-1][3]
+    og = (np.random.default_rng(7).standard_normal((T, P)) * 0.05).astype(np.float16)
+    gbuf = kfp16.upload_fp16(og)
+    net.backward(gbuf.ptr)
+    got = net.read_grads()
+    on.backward(og.astype(np.float32))
+    ref = on.grads()
+    for k in ref:
+        assert rel_fro(got[k], ref[k]) <= 5e-3, (k, rel_fro(got[k], ref[k]))
+
+
+def test_sgd_step_matches_oracle(gpu):
+    kfp16 = gpu
+    from kfp16 import synth
+    xcfg = synth.load_xconfig("tiny.xconfig")
+    T = 96
+    net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
+    og = (np.random.default_rng(9).standard_normal((T, 200)) * 0.05).astype(np.float16)
+    gbuf = kfp16.upload_fp16(og)
+    w0 = net.get_params()
+    lr, mom = 1e-3, 0.9
+    net.backward(gbuf.ptr)
+    g1 = net.read_grads()
+    net.sgd(lr, mom)
+    net.forward(fbuf.ptr, T)
+    net.backward(gbuf.ptr)
+    g2 = net.read_grads()
+    net.sgd(lr, mom)
+    w2 = net.get_params()
+    import ctypes
+    L = oracle.lib()
+    for k in w0:
+        w = w0[k].astype(np.float32).ravel().copy()
+        v = np.zeros_like(w)
+        for g in (g1[k], g2[k]):
+            gg = np.ascontiguousarray(g.ravel(), np.float32)
+            L.orc_sgd(w.ctypes.data, gg.ctypes.data, v.ctypes.data, lr, mom, w.size)
+        np.testing.assert_allclose(w2[k].ravel(), w, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.slow
+def test_full_model_one_eg(gpu):
+    """The benchmark model (cnn_tdnn_17f) on one 1500-frame eg."""
+    kfp16 = gpu
+    from kfp16 import synth
+    xcfg = synth.load_xconfig("cnn_tdnn_17f.xconfig")
+    T = 1500
+    net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
+    on = _oracle(xcfg, params, bns, feats)
+    for name in ("cnn1", "cnn3", "cnn6", "tdnnf7", "tdnnf15", "tdnnf23", "prefinal-chain", "output"):
+        got = net.read_activation(name).astype(np.float32)
+        ref = on.act(name)
+        assert rel_fro(got, ref) <= 2e-3, (name, rel_fro(got, ref))
+        assert max_abs_rel(got, ref) <= 1e-2, (name, max_abs_rel(got, ref))
+    og = (np.random.default_rng(7).standard_normal((T, 3080)) * 0.02).astype(np.float16)
+    gbuf = kfp16.upload_fp16(og)
+    net.backward(gbuf.ptr)
+    got = net.read_grads()
+    on.backward(og.astype(np.float32))
+    ref = on.grads()
+    for k in ref:
+        assert rel_fro(got[k], ref[k]) <= 5e-3, (k, rel_fro(got[k], ref[k]))
