@@ -771,7 +771,30 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
 
 }  // namespace
 
+static int backward_impl(KfNet *net, const void *out_grad, int max_layers);
 extern "C" int nnet_backward(KfNet *net, const void *out_grad) {
+    return backward_impl(net, out_grad, 1 << 30);
+}
+// debugging / tests: back-propagate through the top `n` layers only
+extern "C" int nnet_backward_n(KfNet *net, const void *out_grad, int n) {
+    return backward_impl(net, out_grad, n);
+}
+// debugging / tests: device pointers of internal tensors
+extern "C" const void *nnet_debug_tensor(KfNet *net, const char *what, int layer) {
+    std::string w = what;
+    if (w == "dz0") return net->dz[0];
+    if (w == "dz1") return net->dz[1];
+    if (w == "g0") return net->g[0];
+    if (w == "g1") return net->g[1];
+    if (w == "dbott") return net->dbott;
+    if (layer < 0 || layer >= (int)net->layers.size()) return nullptr;
+    if (w == "aux") return net->layers[layer].aux;
+    if (w == "mask") return net->layers[layer].mask;
+    if (w == "bn_scale") return net->layers[layer].bn_scale;
+    if (w == "bn2_scale") return net->layers[layer].bn2_scale;
+    return nullptr;
+}
+static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     const int T = net->T;
     if (T <= 0) {
         set_err("backward before forward");
@@ -781,8 +804,8 @@ extern "C" int nnet_backward(KfNet *net, const void *out_grad) {
     // the top layer must be the chain output
     const void *dz = out_grad;  // gradient w.r.t. pre-activation of the current layer
     const void *gcur = out_grad;  // stored gradient w.r.t. the current layer's output
-    int flip = 0;
-    for (int li = n - 1; li >= 0; li = net->layers[li].input) {
+    int flip = 0, done = 0;
+    for (int li = n - 1; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
         NetLayer &nl = net->layers[li];
         const Layer &L = nl.L;
         const int din = L.in_dim, dout = L.out_dim;

@@ -87,6 +87,8 @@ _sig(nnet, "nnet_master_buffer", _vp, _vp)
 _sig(nnet, "nnet_weight_buffer", _vp, _vp)
 _sig(nnet, "nnet_sgd", _i, _vp, _f, _f)
 _sig(nnet, "nnet_bind_grad_buffer", _i, _vp, _vp)
+_sig(nnet, "nnet_backward_n", _i, _vp, _vp, _i)
+_sig(nnet, "nnet_debug_tensor", _vp, _vp, C.c_char_p, _i)
 _sig(core, "kf_prof_enable", None, _i)
 _sig(core, "kf_prof_collect", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double))
 _sig(core, "kf_prof_reset", None)
@@ -267,6 +269,21 @@ class Network:
     def master_ptr(self):
         return nnet.nnet_master_buffer(self.h)
 
+    def relu_masks(self) -> dict:
+        """Every layer's ReLU decisions (bit-packed on device) as uint8 per element."""
+        out = {}
+        for i, (name, ty, din, dout) in enumerate(self.layers):
+            width = {6: dout, 7: dout, 9: None}.get(ty, 0)
+            if width is None:
+                width = self.params[name + ".BigW"][1]
+            if not width:
+                continue
+            p = nnet.nnet_debug_tensor(self.h, b"mask", i)
+            n = self.T * width
+            raw = read_fp16(p, ((n + 15) // 16,)).view(np.uint8)
+            out[name] = np.unpackbits(raw, bitorder="little")[:n]
+        return out
+
     def read_grads(self) -> dict:
         return self.unflatten(read_f32(self.grad_ptr, (self.num_params,)))
 
@@ -297,3 +314,44 @@ def read_header_symbols(header: str):
     text = re.sub(r"//[^\n]*", "", text)
     names = re.findall(r"\b([a-z][a-z0-9_]*)\s*\([^;{]*\)\s*;", text)
     return sorted(set(n for n in names if not n.startswith(("sizeof", "typedef"))))
+
+
+# ---------------------------------------------------------------- kf_ops structs
+MAXP = 9
+
+
+class KfOperand(C.Structure):
+    _fields_ = [("base", _vp), ("ld", _ll), ("nrows", _i), ("ncols", _i), ("kcontig", _i),
+                ("nparts", _i), ("part_width", _i), ("T", _i), ("hout", _i), ("hsrc", _i),
+                ("hmul", _i), ("hdiv", _i), ("tpolicy", _i), ("dt", _i * MAXP), ("dh", _i * MAXP),
+                ("edge_t", _i * MAXP), ("edge_ptr", _vp * MAXP)]
+
+
+class KfEpilogue(C.Structure):
+    _fields_ = [("out", _vp), ("ldo", _ll), ("alpha", _f), ("beta", _f), ("bias", _vp), ("relu", _i),
+                ("mask_out", _vp), ("scale", _vp), ("shift", _vp), ("resid", _vp), ("ldr", _ll),
+                ("resid_alpha", _f), ("out2", _vp), ("ldo2", _ll), ("scale2", _vp), ("mask_in", _vp)]
+
+
+def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, hout=1, hsrc=1,
+            hmul=0, hdiv=1, tpolicy=0, dt=(), dh=(), edges=()):
+    o = KfOperand()
+    o.base, o.ld, o.nrows, o.ncols, o.kcontig = base, ld, rows, cols, kcontig
+    o.nparts, o.part_width = nparts, part_width if part_width is not None else cols
+    o.T = T if T is not None else rows
+    o.hout, o.hsrc, o.hmul, o.hdiv, o.tpolicy = hout, hsrc, hmul, hdiv, tpolicy
+    for i in range(MAXP):
+        o.edge_t[i] = -1
+    for i, v in enumerate(dt):
+        o.dt[i] = v
+    for i, v in enumerate(dh):
+        o.dh[i] = v
+    for p, t, ptr in edges:
+        o.edge_t[p] = t
+        o.edge_ptr[p] = ptr
+    return o
+
+
+_sig(core, "kf_gemm_fused", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), C.POINTER(KfEpilogue))
+_sig(core, "kf_gemm_wgrad", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i)
+_sig(core, "kf_rows_sum", _i, _vp, _vp, _ll, _i, _i, _i)

@@ -284,7 +284,7 @@ static void col2im_add(const OrcLayer *L, const float *dp, int T, float *dx) {
 
 /* relu + BN (+ bias) epilogue; R mode rounds after every reference op */
 static void bias_relu_bn(float *z, int rows, int D, const float *bias, const OrcBN *bn,
-                         uint8_t *mask, int mode, int relu) {
+                         uint8_t *mask, int mode, int relu, const uint8_t *force) {
     for (long long i = 0; i < (long long)rows * D; ++i) {
         int d = (int)(i % D);
         float v = z[i];
@@ -294,8 +294,9 @@ static void bias_relu_bn(float *z, int rows, int D, const float *bias, const Orc
             if (mode == ORC_ROUND_REF) v = rh(v);
         }
         if (relu) {
-            if (mask) mask[i] = v > 0.f;
-            if (!(v > 0.f)) v = 0.f;
+            const int on = force ? force[i] != 0 : v > 0.f;
+            if (mask) mask[i] = (uint8_t)on;
+            if (!on) v = 0.f;
         }
         if (bn && bn->mean) {
             v = bn_apply(bn, d, v);
@@ -330,6 +331,7 @@ static void alloc_net(OrcNet *net) {
     net->gact = (float **)xalloc(sizeof(float *) * n);
 }
 
+#define FM(li) (net->force_mask ? net->force_mask[li] : NULL)
 int orc_net_forward(OrcNet *net, const float *features) {
     const int T = net->T, mode = net->round_mode;
     if (!net->act) alloc_net(net);
@@ -352,7 +354,7 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 orc_matmul(T * L->hout, L->fout, L->noff * L->fin, p, L->W, y);
                 free(p);
                 net->mask[li] = (uint8_t *)xalloc((size_t)T * dout);
-                bias_relu_bn(y, T * L->hout, L->fout, L->b, &L->bn, net->mask[li], mode, 1);
+                bias_relu_bn(y, T * L->hout, L->fout, L->b, &L->bn, net->mask[li], mode, 1, FM(li));
                 if (mode) orc_round_f16(y, (long long)T * dout);
                 break;
             }
@@ -371,7 +373,7 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 orc_matmul(T, dout, s > 0 ? 2 * bn : bn, aff_in, L->W2, y);
                 free(tmp);
                 net->mask[li] = (uint8_t *)xalloc((size_t)T * dout);
-                bias_relu_bn(y, T, dout, L->b2, &L->bn, net->mask[li], mode, 1);
+                bias_relu_bn(y, T, dout, L->b2, &L->bn, net->mask[li], mode, 1, FM(li));
                 if (L->bypass > 0.f && din == dout) {
                     for (long long i = 0; i < (long long)T * dout; ++i) {
                         float v = y[i] + L->bypass * x[i];
@@ -391,17 +393,17 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 float *bg = (float *)xalloc(sizeof(float) * (size_t)T * big);
                 orc_matmul(T, big, din, x, L->W, bg);
                 net->mask[li] = (uint8_t *)xalloc((size_t)T * big);
-                bias_relu_bn(bg, T, big, L->b, &L->bn, net->mask[li], mode, 1);
+                bias_relu_bn(bg, T, big, L->b, &L->bn, net->mask[li], mode, 1, FM(li));
                 if (mode) orc_round_f16(bg, (long long)T * big);
                 orc_matmul(T, small, big, bg, L->W2, y);
-                bias_relu_bn(y, T, small, NULL, &L->bn2, NULL, mode, 0);
+                bias_relu_bn(y, T, small, NULL, &L->bn2, NULL, mode, 0, NULL);
                 if (mode) orc_round_f16(y, (long long)T * small);
                 net->aux[li] = bg;
                 break;
             }
             case ORC_OUTPUT:
                 orc_matmul(T, dout, din, x, L->W, y);
-                bias_relu_bn(y, T, dout, L->b, NULL, NULL, mode, 0);
+                bias_relu_bn(y, T, dout, L->b, NULL, NULL, mode, 0, NULL);
                 if (mode) orc_round_f16(y, (long long)T * dout);
                 break;
             default:

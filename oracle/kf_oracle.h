@@ -83,6 +83,11 @@ typedef struct {
     float **aux;      /* [nlayers] tdnnf bottleneck / prefinal big */
     float **gW, **gb, **gW2, **gb2; /* [nlayers] parameter gradients (fp32) */
     float **gact;     /* [nlayers] gradient w.r.t. each layer's output */
+    /* optional: per-layer ReLU decisions to replay instead of recomputing
+     * (1 byte per element, NULL = compute). Parity tests use it to compare
+     * gradients without the sqrt(flip-fraction) noise of near-zero
+     * pre-activations that two fp16 paths legitimately decide differently. */
+    const uint8_t **force_mask;
 } OrcNet;
 
 int orc_net_forward(OrcNet *net, const float *features);

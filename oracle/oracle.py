@@ -78,7 +78,8 @@ class OrcNet(C.Structure):
                 ("feat_dim", C.c_int), ("round_mode", C.c_int),
                 ("act", C.POINTER(_fp)), ("mask", C.POINTER(C.POINTER(C.c_uint8))),
                 ("aux", C.POINTER(_fp)), ("gW", C.POINTER(_fp)), ("gb", C.POINTER(_fp)),
-                ("gW2", C.POINTER(_fp)), ("gb2", C.POINTER(_fp)), ("gact", C.POINTER(_fp))]
+                ("gW2", C.POINTER(_fp)), ("gb2", C.POINTER(_fp)), ("gact", C.POINTER(_fp)),
+                ("force_mask", C.POINTER(C.POINTER(C.c_uint8)))]
 
 
 def parse_xconfig(text: str):
@@ -213,8 +214,17 @@ class OracleNet:
         m, v, g, b = spec
         return OrcBN(self._p(m), self._p(v), self._p(g), self._p(b), 1e-3, target_rms)
 
-    def forward(self, features: np.ndarray):
+    def forward(self, features: np.ndarray, force_masks: dict = None):
+        """force_masks: layer name -> uint8 ReLU decisions to replay (see kf_oracle.h)."""
         x = np.ascontiguousarray(features, dtype=np.float32)
+        fm = None
+        if force_masks:
+            fm = (C.POINTER(C.c_uint8) * len(self.L))()
+            for name, m in force_masks.items():
+                m = np.ascontiguousarray(m, dtype=np.uint8)
+                self.keep.append(m)
+                fm[self.index[name]] = m.ctypes.data_as(C.POINTER(C.c_uint8))
+            self.keep.append(fm)
         self.x = x
         if self.net is not None:
             lib().orc_net_free(C.byref(self.net))
@@ -224,6 +234,8 @@ class OracleNet:
         self.net.T = x.shape[0]
         self.net.feat_dim = x.shape[1]
         self.net.round_mode = self.round_mode
+        if fm is not None:
+            self.net.force_mask = fm
         rc = lib().orc_net_forward(C.byref(self.net), x.ctypes.data)
         assert rc == 0
 
@@ -231,6 +243,13 @@ class OracleNet:
         i = self.index[name]
         T, d = self.net.T, self.L[i]["out_dim"]
         return np.ctypeslib.as_array(self.net.act[i], shape=(T * d,)).reshape(T, d).copy()
+
+    def mask(self, name):
+        i = self.index[name]
+        L = self.L[i]
+        width = L["big_dim"] if L["kind"] == "prefinal-layer" else L["out_dim"]
+        p = self.net.mask[i]
+        return None if not p else np.ctypeslib.as_array(p, shape=(self.net.T * width,)).copy()
 
     def backward(self, out_grad: np.ndarray):
         g = np.ascontiguousarray(out_grad, dtype=np.float32)

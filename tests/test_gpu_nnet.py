@@ -50,6 +50,23 @@ def test_ops_gemm_matches_fp32(gpu):
     kfp16.core.ops_cublas_destroy(h)
 
 
+def _forward_parity(net, on, onr):
+    """Activations within SURVEY §8d tolerances; ReLU decisions agree except for
+    a small fraction of near-zero pre-activations."""
+    masks = net.relu_masks()
+    for name, ty, din, dout in net.layers:
+        got = net.read_activation(name).astype(np.float32)
+        ref = on.act(name)
+        assert rel_fro(got, ref) <= 2e-3, (name, rel_fro(got, ref))
+        assert max_abs_rel(got, ref) <= 1e-2, (name, max_abs_rel(got, ref))
+        if onr is not None:
+            assert rel_fro(got, onr.act(name)) <= 1e-2, (name, "vs R mode")
+        if name in masks:
+            agree = float(np.mean(masks[name] == on.mask(name)))
+            assert agree >= 0.999, (name, agree)
+    return masks
+
+
 @pytest.mark.parametrize("T", [150, 517])
 def test_tiny_network_forward_backward(gpu, T):
     kfp16 = gpu
@@ -58,13 +75,12 @@ def test_tiny_network_forward_backward(gpu, T):
     net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
     on = _oracle(xcfg, params, bns, feats)
     onr = _oracle(xcfg, params, bns, feats, oracle.ROUND_REF)
-    for name, ty, din, dout in net.layers:
-        got = net.read_activation(name).astype(np.float32)
-        ref = on.act(name)
-        assert rel_fro(got, ref) <= 2e-3, (name, rel_fro(got, ref))
-        assert max_abs_rel(got, ref) <= 1e-2, (name, max_abs_rel(got, ref))
-        assert rel_fro(got, onr.act(name)) <= 1e-2, (name, "vs R mode")
-    # backward from a fixed fp16 output gradient
+    masks = _forward_parity(net, on, onr)
+    # backward from a fixed fp16 output gradient; the oracle replays the
+    # product's ReLU decisions so gradients compare without flip noise
+    on.close()
+    on = _oracle(xcfg, params, bns, feats)
+    on.forward(feats.astype(np.float32), force_masks=masks)
     P = net.layers[-1][3]
     og = (np.random.default_rng(7).standard_normal((T, P)) * 0.05).astype(np.float16)
     gbuf = kfp16.upload_fp16(og)
@@ -72,8 +88,9 @@ def test_tiny_network_forward_backward(gpu, T):
     got = net.read_grads()
     on.backward(og.astype(np.float32))
     ref = on.grads()
-    for k in ref:
-        assert rel_fro(got[k], ref[k]) <= 5e-3, (k, rel_fro(got[k], ref[k]))
+    errs = {k: rel_fro(got[k], ref[k]) for k in ref}
+    bad = {k: v for k, v in errs.items() if v > 5e-3}
+    assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
 
 
 def test_sgd_step_matches_oracle(gpu):
@@ -114,16 +131,15 @@ def test_full_model_one_eg(gpu):
     T = 1500
     net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
     on = _oracle(xcfg, params, bns, feats)
-    for name in ("cnn1", "cnn3", "cnn6", "tdnnf7", "tdnnf15", "tdnnf23", "prefinal-chain", "output"):
-        got = net.read_activation(name).astype(np.float32)
-        ref = on.act(name)
-        assert rel_fro(got, ref) <= 2e-3, (name, rel_fro(got, ref))
-        assert max_abs_rel(got, ref) <= 1e-2, (name, max_abs_rel(got, ref))
+    masks = _forward_parity(net, on, None)
+    on.close()
+    on = _oracle(xcfg, params, bns, feats)
+    on.forward(feats.astype(np.float32), force_masks=masks)
     og = (np.random.default_rng(7).standard_normal((T, 3080)) * 0.02).astype(np.float16)
     gbuf = kfp16.upload_fp16(og)
     net.backward(gbuf.ptr)
     got = net.read_grads()
     on.backward(og.astype(np.float32))
     ref = on.grads()
-    for k in ref:
-        assert rel_fro(got[k], ref[k]) <= 5e-3, (k, rel_fro(got[k], ref[k]))
+    errs = {k: rel_fro(got[k], ref[k]) for k in ref}
+    assert all(v <= 5e-3 for v in errs.values()), errs
