@@ -13,8 +13,9 @@
  * from memory by this rule (all counts in elements):
  *   part p = c / part_width, kk = c % part_width      (nparts parts)
  *   t = r / hout, h = r % hout                         (hout = 1 for TDNN rows)
- *   if edge_t[p] >= 0 and t == edge_t[p]: read edge_ptr[p][kk]
- *   st = t + dt[p]; outside [0, T): clamp (tpolicy=KF_CLAMP) or zero (KF_ZERO)
+ *   if edge_t[p] >= 0 and t == edge_t[p]: st = edge_row[p] (a spare row of the
+ *      same buffer, e.g. row T, holding a precomputed sum; no range checks)
+ *   else st = t + dt[p]; outside [0, T): clamp (tpolicy=KF_CLAMP) or zero (KF_ZERO)
  *   shn = h*hmul + dh[p]; zero unless shn % hdiv == 0; sh = shn / hdiv,
  *   zero unless 0 <= sh < hsrc
  *   value = base[st*ld + sh*part_width + kk]
@@ -52,7 +53,7 @@ typedef struct {
     int dt[KF_MAX_PARTS];
     int dh[KF_MAX_PARTS];
     int edge_t[KF_MAX_PARTS];
-    const void *edge_ptr[KF_MAX_PARTS];
+    int edge_row[KF_MAX_PARTS];
 } KfOperand;
 
 /*
@@ -102,7 +103,8 @@ int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
 int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW,
                   long long ldw, float *bias_grad, int accumulate);
 
-/* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols */
+/* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols
+ * (edge may be a spare row of src's own allocation) */
 int kf_rows_sum(void *edge, const void *src, long long ld, int r0, int r1, int cols);
 
 /* ---- non-MFMA layer pieces (csrc/layers.hip) ---- */

@@ -32,10 +32,34 @@ extern "C" const char *kf_last_error(void) { return kf_err_.get(); }
 extern "C" void kf_clear_error(void) { kf_err_.clear(); }
 
 // ---------------------------------------------------------------------------
-// operand addressing
+// operand addressing (device form of KfOperand, see kf_ops.h)
 // ---------------------------------------------------------------------------
+struct OpD {
+    const h16 *base;
+    long long ld;
+    int nrows, ncols;
+    int nparts, pw;
+    int T, hout, hsrc, hmul, hshift;
+    int tclamp, simple, p64;
+    unsigned inv_hout;  // ceil(2^16 / hout): exact t = h/hout for h*hout < 2^16
+    int dt[KF_MAX_PARTS], dh[KF_MAX_PARTS], et[KF_MAX_PARTS], er[KF_MAX_PARTS];
+};
+
+// compile-time loop: body(I) with I a std::integral_constant (forces full unrolling,
+// so register arrays are never indexed dynamically and never fall to scratch)
+#include <utility>
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 template <typename T>
-__device__ __forceinline__ T sel9(const T (&a)[KF_MAX_PARTS], int p) {
+__device__ __forceinline__ T sel9(const T (&a)[KF_MAX_PARTS], int p, int nparts) {
+    if (nparts <= 2) return p ? a[1] : a[0];
     T v = a[0];
 #pragma unroll
     for (int i = 1; i < KF_MAX_PARTS; ++i)
@@ -43,51 +67,35 @@ __device__ __forceinline__ T sel9(const T (&a)[KF_MAX_PARTS], int p) {
     return v;
 }
 
-__device__ __forceinline__ bool op_plain(const KfOperand &d) {
-    return d.nparts == 1 && d.hout == 1 && d.dt[0] == 0 && d.edge_t[0] < 0;
-}
-
-// pointer to the 8-element chunk Op[r][c..c+7], or nullptr when it reads as zero
-__device__ __forceinline__ const h16 *op_chunk(const KfOperand &d, bool plain, int r, int c) {
-    if (r >= d.nrows || c >= d.ncols) return nullptr;
-    const h16 *base = (const h16 *)d.base;
-    if (plain) return base + (long long)r * d.ld + c;
-    int p = 0, kk = c;
-    if (d.nparts > 1) {
-        p = c / d.part_width;
-        kk = c - p * d.part_width;
+// element offset of Op row (t, h), part p, in-part column kk; -1 = reads as zero
+__device__ __forceinline__ long long op_off(const OpD &d, int t, int h, int kk, int dtp, int dhp,
+                                            int etp, int erp) {
+    int st;
+    if (t == etp) {
+        st = erp;
+    } else {
+        st = t + dtp;
+        if (d.tclamp) st = min(max(st, 0), d.T - 1);
+        else if ((unsigned)st >= (unsigned)d.T) return -1;
     }
-    int t = r, h = 0;
-    if (d.hout > 1) {
-        t = r / d.hout;
-        h = r - t * d.hout;
+    int sh = h * d.hmul + dhp;
+    if (d.hshift) {
+        if (sh & ((1 << d.hshift) - 1)) return -1;
+        sh >>= d.hshift;
     }
-    const int et = sel9(d.edge_t, p);
-    if (et >= 0 && t == et) return (const h16 *)sel9(d.edge_ptr, p) + kk;
-    int st = t + sel9(d.dt, p);
-    if (st < 0 || st >= d.T) {
-        if (d.tpolicy != KF_CLAMP) return nullptr;
-        st = st < 0 ? 0 : d.T - 1;
-    }
-    int sh = h * d.hmul + sel9(d.dh, p);
-    if (d.hdiv > 1) {
-        if (sh < 0 || (sh % d.hdiv) != 0) return nullptr;
-        sh /= d.hdiv;
-    }
-    if (sh < 0 || sh >= d.hsrc) return nullptr;
-    return base + (long long)st * d.ld + (long long)sh * d.part_width + kk;
+    if ((unsigned)sh >= (unsigned)d.hsrc) return -1;
+    return (long long)st * d.ld + (long long)sh * d.pw + kk;
 }
 
 // ---------------------------------------------------------------------------
-// LDS images
+// LDS images (both bank-conflict free for the 16x16x32 fragment maps; the
+// swizzles were checked offline against the ds_read lane groups of
+// MI355X_MICROARCH §LDS). BK is fixed at 64 halves.
 // ---------------------------------------------------------------------------
-// k-contiguous [rows][BK] halves, 16-byte chunk c of row r stored at c ^ ((r>>1)&(CPR-1))
-template <int BK>
-__device__ __forceinline__ int kc_off(int r, int c) {
-    constexpr int CPR = BK / 8;
-    return r * (BK * 2) + 16 * (c ^ ((r >> 1) & (CPR - 1)));
-}
-// reduction-major [BK][W] halves, 8-byte unit u of row r stored at u ^ swz(r)
+constexpr int BK = 64;
+// k-contiguous [rows][64] halves: 16-byte chunk c of row r at slot c ^ ((r>>1)&7)
+__device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
+// reduction-major [64][W] halves: 8-byte unit u of row r at u ^ swz(r)
 template <int W>
 __device__ __forceinline__ int mn_swz(int r) {
     if constexpr (W == 64) return ((r & 2) << 1) ^ (((r >> 3) & 1) << 3);
@@ -102,13 +110,13 @@ __device__ __forceinline__ int mn_off(int r, int u) {
 
 typedef __attribute__((address_space(3))) short4v lds_s4;
 
-// fragment for v_mfma_f32_16x16x32_f16: lane l holds Op[idx0 + (l&15)][k = 32s + 8(l>>4) + j]
-template <bool KC, int W, int BK>
+// v_mfma_f32_16x16x32_f16 fragment: lane l holds Op[idx0 + (l&15)][k = 32s + 8(l>>4) + j]
+template <bool KC, int W>
 __device__ __forceinline__ half8 load_frag(const char *tile, int idx0, int s, int lane) {
     if constexpr (KC) {
         const int r = idx0 + (lane & 15);
         const int c = s * 4 + (lane >> 4);
-        return *reinterpret_cast<const half8 *>(tile + kc_off<BK>(r, c));
+        return *reinterpret_cast<const half8 *>(tile + kc_off(r, c));
     } else {
         const int q = (lane & 15) >> 2, p = lane & 3, g = lane >> 4;
         const int r0 = s * 32 + 8 * g + q;
@@ -123,20 +131,191 @@ __device__ __forceinline__ half8 load_frag(const char *tile, int idx0, int s, in
 }
 
 // ---------------------------------------------------------------------------
-// epilogue on 8 consecutive columns of one row
+// per-thread LDS-DMA staging of one operand tile
+//   KC: tile [TR][64], rows fixed per chunk, columns advance with k
+//   MN: tile [64][TR], columns fixed per chunk, rows advance with k
+// Each wave owns NC consecutive 1 KiB pieces; lane l fills bytes 16l..16l+15
+// of a piece, so the swizzle is applied to the SOURCE address (rule 21).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void epilogue8(const KfEpilogue &E, int m, int n, float v[8]) {
+// operand kinds, chosen on the host: the stager keeps only the state its kind needs
+enum { OP_SIMPLE = 0, OP_P2 = 1, OP_GEN = 2 };
+constexpr unsigned BAD = 0xFFFFFFFFu;  // byte offset that reads as zero (buffer range check)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)0xFFFFFFFF,
+                                             0x00020000);
+}
+
+// byte offset of (row t,h ; part p ; in-part column kk) or BAD
+__device__ __forceinline__ unsigned op_boff(const OpD &d, int t, int h, int kk, int dtp, int dhp,
+                                            int etp, int erp) {
+    const long long off = op_off(d, t, h, kk, dtp, dhp, etp, erp);
+    return off < 0 ? BAD : (unsigned)(off * 2);
+}
+
+template <bool KC, int TR, int MODE>
+struct Stager {
+    static constexpr int NC = TR / 32;  // 1 KiB pieces (= chunks) per thread, 4 waves
+    unsigned o0[NC];                    // KC: part-0 row byte offset; MN: fixed byte offset base
+    unsigned o1[MODE == OP_P2 && KC ? NC : 1];  // KC/P2: part-1 row byte offset
+    int th[MODE == OP_GEN ? NC : 1];    // GEN: KC packed (t<<8)|h ; MN packed part info
+    int dt1[!KC && MODE != OP_SIMPLE ? NC : 1];  // MN: dt of the chunk's part
+    int curp;
+
+    __device__ __forceinline__ static int kc_row(int q, int lane) { return q * 8 + (lane >> 3); }
+    __device__ __forceinline__ static int kc_col(int q, int lane) {
+        return 8 * ((lane & 7) ^ ((kc_row(q, lane) >> 1) & 7));
+    }
+    __device__ __forceinline__ static int mn_row(int q, int lane) {
+        return (q * 1024 + 16 * lane) / (2 * TR);
+    }
+    __device__ __forceinline__ static int mn_col(int q, int lane) {  // column in tile
+        const int P = q * 1024 + 16 * lane, row = P / (2 * TR), within = P - row * (2 * TR);
+        return 4 * ((within >> 3) ^ mn_swz<TR>(row));
+    }
+
+    __device__ __forceinline__ void init(const OpD &d, int tile0, int wave, int lane) {
+        curp = -1;
+        static_for<NC>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const int q = wave * NC + j;
+            if constexpr (KC) {
+                const int r = tile0 + kc_row(q, lane);
+                const bool ok = r < d.nrows;
+                if constexpr (MODE == OP_SIMPLE) {
+                    o0[j] = ok ? (unsigned)((long long)r * d.ld * 2) : BAD;
+                } else if constexpr (MODE == OP_P2) {
+                    o0[j] = ok ? op_boff(d, r, 0, 0, d.dt[0], d.dh[0], d.et[0], d.er[0]) : BAD;
+                    o1[j] = ok && d.nparts > 1 ? op_boff(d, r, 0, 0, d.dt[1], d.dh[1], d.et[1], d.er[1])
+                                               : BAD;
+                } else {
+                    const int t = d.hout > 1 ? r / d.hout : r;
+                    th[j] = ok ? (t << 8) | (r - t * d.hout) : -1;
+                    o0[j] = BAD;
+                }
+            } else {
+                const int col = tile0 + mn_col(q, lane);
+                const int rrel = mn_row(q, lane);
+                const bool ok = col < d.ncols;
+                if constexpr (MODE == OP_SIMPLE) {
+                    o0[j] = ok ? (unsigned)(((long long)rrel * d.ld + col) * 2) : BAD;
+                } else {
+                    const int p = d.nparts > 1 ? col / d.pw : 0;
+                    const int kk = col - p * d.pw;
+                    o0[j] = ok ? (unsigned)(kk * 2) : BAD;
+                    dt1[j] = sel9(d.dt, p, d.nparts);
+                    if constexpr (MODE == OP_GEN)
+                        th[j] = ((sel9(d.dh, p, d.nparts) + 128) & 0xFF) | (p << 8);
+                }
+            }
+        });
+    }
+
+    // issue the NC LDS-DMA loads of the tile at reduction offset k0 into `dst`
+    __device__ __forceinline__ void issue(const OpD &d, __amdgpu_buffer_rsrc_t rs, int k0, int kend,
+                                          char *dst, int wave, int lane) {
+        const int klim = min(kend, KC ? d.ncols : d.nrows);
+        if constexpr (KC && MODE == OP_GEN) {
+            // part of this K step is uniform when part_width % 64 == 0
+            if (d.p64) {
+                const int pu = k0 / d.pw;
+                if (pu != curp) {
+                    curp = pu;
+                    const int dtp = sel9(d.dt, pu, d.nparts), dhp = sel9(d.dh, pu, d.nparts);
+                    const int etp = sel9(d.et, pu, d.nparts), erp = sel9(d.er, pu, d.nparts);
+                    static_for<NC>([&](auto J) {
+                        constexpr int j = decltype(J)::value;
+                        o0[j] = th[j] < 0 ? BAD
+                                          : op_boff(d, th[j] >> 8, th[j] & 0xFF, 0, dtp, dhp, etp, erp);
+                    });
+                }
+            }
+        }
+        int t0 = 0, h0 = 0;
+        if constexpr (!KC && MODE == OP_GEN) {
+            t0 = k0 / d.hout;
+            h0 = k0 - t0 * d.hout;
+        }
+        static_for<NC>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const int q = wave * NC + j;
+            unsigned voff = BAD;
+            if constexpr (KC) {
+                const int col = k0 + kc_col(q, lane);
+                if (col < klim) {
+                    if constexpr (MODE == OP_SIMPLE) {
+                        if (o0[j] != BAD) voff = o0[j] + col * 2;
+                    } else if constexpr (MODE == OP_P2) {
+                        const bool p1 = col >= d.pw;
+                        const unsigned b = p1 ? o1[j] : o0[j];
+                        if (b != BAD) voff = b + (col - (p1 ? d.pw : 0)) * 2;
+                    } else {
+                        if (d.p64) {
+                            if (o0[j] != BAD) voff = o0[j] + (col - curp * d.pw) * 2;
+                        } else if (th[j] >= 0) {  // general (tests): part per chunk
+                            const int p = col / d.pw;
+                            voff = op_boff(d, th[j] >> 8, th[j] & 0xFF, col - p * d.pw,
+                                           sel9(d.dt, p, d.nparts), sel9(d.dh, p, d.nparts),
+                                           sel9(d.et, p, d.nparts), sel9(d.er, p, d.nparts));
+                        }
+                    }
+                }
+            } else {
+                const int r = k0 + mn_row(q, lane);
+                if (r < klim && o0[j] != BAD) {
+                    if constexpr (MODE == OP_SIMPLE) {
+                        voff = o0[j] + (unsigned)((long long)k0 * d.ld * 2);
+                    } else if constexpr (MODE == OP_P2) {
+                        int st = r + dt1[j];
+                        bool ok = true;
+                        if (d.tclamp) st = min(max(st, 0), d.T - 1);
+                        else ok = (unsigned)st < (unsigned)d.T;
+                        if (ok) voff = (unsigned)((long long)st * d.ld * 2) + o0[j];
+                    } else {
+                        const int hx = h0 + mn_row(q, lane);
+                        const int qd = (int)(((unsigned)hx * d.inv_hout) >> 16);
+                        const int tt = t0 + qd, hh = hx - qd * d.hout;
+                        const int p = th[j] >> 8;
+                        const unsigned b = op_boff(d, tt, hh, 0, dt1[j], (th[j] & 0xFF) - 128,
+                                                   sel9(d.et, p, d.nparts), sel9(d.er, p, d.nparts));
+                        if (b != BAD) voff = b + o0[j];
+                    }
+                }
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, (__attribute__((address_space(3))) void *)(dst + q * 1024), 16, voff, 0, 0, 0);
+        });
+    }
+};
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0], vmcnt[5:4] at 15:14)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+// ---------------------------------------------------------------------------
+// epilogue on 8 consecutive columns of one row. Per-column parameters come from
+// LDS (staged once per workgroup); the row operands (residual, input mask, old C)
+// were prefetched by the caller, so no global load sits between two stores.
+// ---------------------------------------------------------------------------
+struct EpiCols {
+    const float *bias, *scale, *shift, *scale2;  // LDS, indexed by local column
+};
+
+__device__ __forceinline__ void epilogue8(const KfEpilogue &E, const EpiCols &P, int m, int n,
+                                          int nl, float v[8], half8 cold, half8 rres,
+                                          unsigned mbits) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= E.alpha;
     if (E.beta != 0.f) {
-        half8 o = load_h8((const h16 *)E.out + (long long)m * E.ldo + n);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += E.beta * (float)o[e];
+        for (int e = 0; e < 8; ++e) v[e] += E.beta * (float)cold[e];
     }
     if (E.bias) {
-        half8 b = load_h8((const h16 *)E.bias + n);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += (float)b[e];
+        for (int e = 0; e < 8; ++e) v[e] += P.bias[nl + e];
     }
     if (E.relu) {
         unsigned bits = 0;
@@ -148,20 +327,12 @@ __device__ __forceinline__ void epilogue8(const KfEpilogue &E, int m, int n, flo
         if (E.mask_out) E.mask_out[((long long)m * E.ldo + n) >> 3] = (uint8_t)bits;
     }
     if (E.scale) {
-        float4v s0 = *reinterpret_cast<const float4v *>(E.scale + n);
-        float4v s1 = *reinterpret_cast<const float4v *>(E.scale + n + 4);
-        float4v b0 = *reinterpret_cast<const float4v *>(E.shift + n);
-        float4v b1 = *reinterpret_cast<const float4v *>(E.shift + n + 4);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            v[e] = fmaf(v[e], s0[e], b0[e]);
-            v[e + 4] = fmaf(v[e + 4], s1[e], b1[e]);
-        }
+        for (int e = 0; e < 8; ++e) v[e] = fmaf(v[e], P.scale[nl + e], P.shift[nl + e]);
     }
     if (E.resid) {
-        half8 r = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaf(E.resid_alpha, (float)r[e], v[e]);
+        for (int e = 0; e < 8; ++e) v[e] = fmaf(E.resid_alpha, (float)rres[e], v[e]);
     }
     if (E.out) {
         half8 o;
@@ -170,27 +341,14 @@ __device__ __forceinline__ void epilogue8(const KfEpilogue &E, int m, int n, flo
         store_h8((h16 *)E.out + (long long)m * E.ldo + n, o);
     }
     if (E.out2) {
-        float w[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) w[e] = v[e];
-        if (E.scale2) {
-            float4v s0 = *reinterpret_cast<const float4v *>(E.scale2 + n);
-            float4v s1 = *reinterpret_cast<const float4v *>(E.scale2 + n + 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                w[e] *= s0[e];
-                w[e + 4] *= s1[e];
-            }
-        }
-        if (E.mask_in) {
-            unsigned bits = E.mask_in[((long long)m * E.ldo2 + n) >> 3];
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                if (!((bits >> e) & 1u)) w[e] = 0.f;
-        }
         half8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2h(w[e]);
+        for (int e = 0; e < 8; ++e) {
+            float w = v[e];
+            if (E.scale2) w *= P.scale2[nl + e];
+            if (E.mask_in && !((mbits >> e) & 1u)) w = 0.f;
+            o[e] = f2h(w);
+        }
         store_h8((h16 *)E.out2 + (long long)m * E.ldo2 + n, o);
     }
 }
@@ -204,33 +362,44 @@ struct WgradArgs {
     int k_per_split;    // multiple of BK
 };
 
-template <int BM, int BN, int BK>
+template <int BM, int BN, int ST>
 struct SmemSize {
-    static constexpr int pipe = 2 * (BM + BN) * BK * 2;
-    static constexpr int epi = BM * (BN + 4) * 4;
-    static constexpr int bytes = pipe > epi ? pipe : epi;
+    static constexpr int stage = (BM + BN) * BK * 2;
+    static constexpr int pipe = ST * stage;
+    static constexpr int bytes = pipe;
 };
 
-template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, bool WGRAD>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(int M, int N, int K, KfOperand A,
-                                                      KfOperand B, KfEpilogue E, WgradArgs G,
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE>
+__global__ __launch_bounds__(256, 1) void gemm_kernel(int M, int N, int K, OpD A, OpD B,
+                                                      KfEpilogue E, WgradArgs G, int n_mtiles,
                                                       int n_ntiles) {
     static_assert(WM * WN == 4, "4 waves");
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     static_assert(TM * 16 == WTM && TN * 16 == WTN, "wave tile multiple of 16");
-    constexpr int KS = BK / 32;
-    constexpr int CA = BM * BK / 8 / 256, CB = BN * BK / 8 / 256;
-    static_assert(CA * 256 * 8 == BM * BK && CB * 256 * 8 == BN * BK, "chunk split");
     constexpr int A_STAGE = BM * BK * 2, B_STAGE = BN * BK * 2;
+    constexpr int STAGE = A_STAGE + B_STAGE;
+    using SA = Stager<AKC, BM, AM>;
+    using SB = Stager<BKC, BN, BMODE>;
+    constexpr int LPT = SA::NC + SB::NC;  // LDS-DMA instructions per thread per stage
+    static_assert(ST == 2 || ST == 3, "stages");
+    static_assert(4 * BN * 4 + (32 * (WTN + 4) * 4) * 4 <= SmemSize<BM, BN, ST>::bytes,
+                  "epilogue staging");
 
-    __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, BK>::bytes];
-    auto sA = [&](int buf) { return smem + buf * A_STAGE; };
-    auto sB = [&](int buf) { return smem + 2 * A_STAGE + buf * B_STAGE; };
+    __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, ST>::bytes];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
-    const int tile = blockIdx.x;
+
+    // XCD-aware tile order: consecutive tile ids (the N tiles of one M tile, which
+    // share the A rows) land on one XCD, whose L2 then serves the A re-reads.
+    const int ntiles = n_mtiles * n_ntiles;
+    int tile = blockIdx.x;
+    if (ntiles >= 8) {
+        const int q = ntiles / 8, rmd = ntiles % 8, xcd = tile % 8, loc = tile / 8;
+        tile = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + loc;
+    }
     const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
     const int m0 = mt * BM, n0 = nt * BN;
     int kbeg = 0, kend = K;
@@ -238,154 +407,145 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(int M, int N, int K, KfOpe
         kbeg = blockIdx.y * G.k_per_split;
         kend = min(K, kbeg + G.k_per_split);
     }
-    const int nk = (kend - kbeg + BK - 1) / BK;
-    const bool aplain = op_plain(A), bplain = op_plain(B);
+    const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-    uint4 ra[CA], rb[CB];
-    auto ldg = [&](int k0) {
-#pragma unroll
-        for (int i = 0; i < CA; ++i) {
-            const int id = tid + 256 * i;
-            int r, c;
-            if constexpr (AKC) {
-                r = m0 + id / (BK / 8);
-                c = k0 + 8 * (id % (BK / 8));
-            } else {
-                r = k0 + id / (BM / 8);
-                c = m0 + 8 * (id % (BM / 8));
-            }
-            const bool inb = AKC ? (c < kend) : (r < kend);
-            const h16 *p = inb ? op_chunk(A, aplain, r, c) : nullptr;
-            ra[i] = p ? *reinterpret_cast<const uint4 *>(p) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < CB; ++i) {
-            const int id = tid + 256 * i;
-            int r, c;
-            if constexpr (BKC) {
-                r = n0 + id / (BK / 8);
-                c = k0 + 8 * (id % (BK / 8));
-            } else {
-                r = k0 + id / (BN / 8);
-                c = n0 + 8 * (id % (BN / 8));
-            }
-            const bool inb = BKC ? (c < kend) : (r < kend);
-            const h16 *p = inb ? op_chunk(B, bplain, r, c) : nullptr;
-            rb[i] = p ? *reinterpret_cast<const uint4 *>(p) : make_uint4(0, 0, 0, 0);
-        }
-    };
-    auto sts = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < CA; ++i) {
-            const int id = tid + 256 * i;
-            int off;
-            if constexpr (AKC) off = kc_off<BK>(id / (BK / 8), id % (BK / 8));
-            else off = mn_off<BM>(id / (BM / 8), 2 * (id % (BM / 8)));
-            *reinterpret_cast<uint4 *>(sA(buf) + off) = ra[i];
-        }
-#pragma unroll
-        for (int i = 0; i < CB; ++i) {
-            const int id = tid + 256 * i;
-            int off;
-            if constexpr (BKC) off = kc_off<BK>(id / (BK / 8), id % (BK / 8));
-            else off = mn_off<BN>(id / (BN / 8), 2 * (id % (BN / 8)));
-            *reinterpret_cast<uint4 *>(sB(buf) + off) = rb[i];
-        }
+    SA sa;
+    SB sb;
+    sa.init(A, m0, wave, lane);
+    sb.init(B, n0, wave, lane);
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(A.base), rb = make_rsrc(B.base);
+    auto issue = [&](int stage, int k0) {
+        char *base = smem + stage * STAGE;
+        sa.issue(A, ra, k0, kend, base, wave, lane);
+        sb.issue(B, rb, k0, kend, base + A_STAGE, wave, lane);
     };
 
     float4v acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = float4v{0.f, 0.f, 0.f, 0.f};
+    static_for<TM>([&](auto I) {
+        static_for<TN>([&](auto J) { acc[I][J] = float4v{0.f, 0.f, 0.f, 0.f}; });
+    });
 
-    // column sums of B (bias gradient) by the blocks of the first M tile
     const bool do_bsum = WGRAD && G.bias_slab != nullptr && mt == 0 && !BKC;
     float bsum = 0.f;
 
-    if (nk > 0) {
-        ldg(kbeg);
-        sts(0);
-        __syncthreads();
-    }
+    if (nk > 0) issue(0, kbeg);
+    if (ST == 3 && nk > 1) issue(1, kbeg + BK);
     for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) ldg(kbeg + (kt + 1) * BK);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
+        if (ST == 3 && kt + 1 < nk) wait_vmcnt<LPT>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + ST - 1 < nk) issue((kt + ST - 1) % ST, kbeg + (kt + ST - 1) * BK);
+        const char *ta = smem + (kt % ST) * STAGE;
+        const char *tb = ta + A_STAGE;
+        static_for<BK / 32>([&](auto S) {
+            constexpr int s = decltype(S)::value;
             half8 fa[TM], fb[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-                fa[i] = load_frag<AKC, BM, BK>(sA(cur), wm * WTM + i * 16, s, lane);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                fb[j] = load_frag<BKC, BN, BK>(sB(cur), wn * WTN + j * 16, s, lane);
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j],
-                                                                       0, 0, 0);
-        }
+            static_for<TM>([&](auto I) { fa[I] = load_frag<AKC, BM>(ta, wm * WTM + I * 16, s, lane); });
+            static_for<TN>([&](auto J) { fb[J] = load_frag<BKC, BN>(tb, wn * WTN + J * 16, s, lane); });
+            static_for<TM>([&](auto I) {
+                static_for<TN>([&](auto J) {
+                    acc[I][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[I], fb[J], acc[I][J], 0, 0, 0);
+                });
+            });
+        });
         if constexpr (WGRAD && !BKC) {
             if (do_bsum && tid < BN) {
                 for (int r = 0; r < BK; ++r) {
-                    const int u = tid >> 2;
-                    const char *p = sB(cur) + mn_off<BN>(r, u) + 2 * (tid & 3);
+                    const char *p = tb + mn_off<BN>(r, tid >> 2) + 2 * (tid & 3);
                     bsum += (float)*reinterpret_cast<const h16 *>(p);
                 }
             }
         }
-        if (kt + 1 < nk) sts(cur ^ 1);
-        __syncthreads();
+        __builtin_amdgcn_sched_barrier(0);
     }
 
     if constexpr (WGRAD) {
         float *slab = G.slab + (long long)blockIdx.y * M * N;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int n = n0 + wn * WTN + j * 16 + (lane & 15);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int m = m0 + wm * WTM + i * 16 + 4 * (lane >> 4) + e;
-                    if (m < M && n < N) slab[(long long)m * N + n] = acc[i][j][e];
-                }
-            }
+        static_for<TM>([&](auto I) {
+            static_for<TN>([&](auto J) {
+                const int n = n0 + wn * WTN + J * 16 + (lane & 15);
+                static_for<4>([&](auto EI) {
+                    const int m = m0 + wm * WTM + I * 16 + 4 * (lane >> 4) + EI;
+                    if (m < M && n < N) slab[(long long)m * N + n] = acc[I][J][decltype(EI)::value];
+                });
+            });
+        });
         if (do_bsum && tid < BN && n0 + tid < N)
             G.bias_slab[(long long)blockIdx.y * N + n0 + tid] = bsum;
     } else {
-        // stage fp32 accumulators through LDS: [BM][BN+4]
-        float *st = reinterpret_cast<float *>(smem);
-        constexpr int LDT = BN + 4;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int c = wn * WTN + j * 16 + (lane & 15);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int r = wm * WTM + i * 16 + 4 * (lane >> 4) + e;
-                    st[r * LDT + c] = acc[i][j][e];
-                }
-            }
+        // Per-column parameters go to LDS once per workgroup; then every wave
+        // stages its accumulators through its own LDS region 32 rows at a time and
+        // each lane owns 8 consecutive columns of a row (16-byte global I/O).
+        wait_vmcnt<0>();
         __syncthreads();
-        constexpr int GROUPS = BM * BN / 8;
-        for (int it = tid; it < GROUPS; it += 256) {
-            const int r = it / (BN / 8), cg = it - r * (BN / 8);
-            const int m = m0 + r, n = n0 + 8 * cg;
-            if (m >= M || n >= N) continue;
-            float v[8];
-            float4v x0 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg);
-            float4v x1 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg + 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                v[e] = x0[e];
-                v[e + 4] = x1[e];
-            }
-            epilogue8(E, m, n, v);
+        float *prm = reinterpret_cast<float *>(smem);
+        for (int c = tid; c < BN; c += 256) {
+            const int n = n0 + c;
+            const bool in = n < N;
+            prm[c] = (E.bias && in) ? (float)((const h16 *)E.bias)[n] : 0.f;
+            prm[BN + c] = (E.scale && in) ? E.scale[n] : 0.f;
+            prm[2 * BN + c] = (E.scale && in) ? E.shift[n] : 0.f;
+            prm[3 * BN + c] = (E.scale2 && in) ? E.scale2[n] : 1.f;
         }
+        __syncthreads();
+        const EpiCols P{prm, prm + BN, prm + 2 * BN, prm + 3 * BN};
+        constexpr int LDT = WTN + 4;
+        float *st = prm + 4 * BN + wave * 32 * LDT;
+        constexpr int CG = WTN / 8;
+        constexpr int ITEMS = 32 * CG / 64;
+        static_assert(ITEMS * 64 == 32 * CG, "items per lane");
+        static_assert(TM % 2 == 0, "epilogue stages 32 rows");
+        static_for<TM / 2>([&](auto IC) {
+            constexpr int ic = decltype(IC)::value;
+            static_for<2>([&](auto I2) {
+                static_for<TN>([&](auto J) {
+                    const int c = J * 16 + (lane & 15);
+                    static_for<4>([&](auto EI) {
+                        const int r = I2 * 16 + 4 * (lane >> 4) + EI;
+                        st[r * LDT + c] = acc[2 * ic + I2][J][decltype(EI)::value];
+                    });
+                });
+            });
+            // prefetch the row operands of every item before any store
+            half8 rres[ITEMS], cold[ITEMS];
+            unsigned mb[ITEMS];
+            static_for<ITEMS>([&](auto K) {
+                constexpr int k = decltype(K)::value;
+                const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+                const int m = m0 + wm * WTM + ic * 32 + r, n = n0 + wn * WTN + 8 * cg;
+                const bool ok = m < M && n < N;
+                rres[k] = half8{};
+                cold[k] = half8{};
+                mb[k] = 0xFFu;
+                if (ok && E.resid) rres[k] = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
+                if (ok && E.beta != 0.f) cold[k] = load_h8((const h16 *)E.out + (long long)m * E.ldo + n);
+                if (ok && E.mask_in) mb[k] = E.mask_in[((long long)m * E.ldo2 + n) >> 3];
+            });
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            static_for<ITEMS>([&](auto K) {
+                constexpr int k = decltype(K)::value;
+                const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+                const int nl = wn * WTN + 8 * cg;
+                const int m = m0 + wm * WTM + ic * 32 + r, n = n0 + nl;
+                if (m < M && n < N) {
+                    float v[8];
+                    float4v x0 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg);
+                    float4v x1 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg + 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[e] = x0[e];
+                        v[e + 4] = x1[e];
+                    }
+                    epilogue8(E, P, m, n, nl, v, cold[k], rres[k], mb[k]);
+                }
+            });
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        });
     }
 }
 
@@ -467,11 +627,75 @@ extern "C" void kf_prof_reset(void) {
 }
 
 // ---------------------------------------------------------------------------
-// host side: tile selection and launch
+// host side: operand conversion, tile selection and launch
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int BK, int WM, int WN, bool AKC, bool BKC, bool WGRAD>
-static int launch(int M, int N, int K, const KfOperand &A, const KfOperand &B,
-                  const KfEpilogue &E, const WgradArgs &G, int splits) {
+static bool to_dev(const KfOperand &d, OpD &o, const char *name) {
+    if (!d.base) {
+        kf_set_error("operand %s: null base", name);
+        return false;
+    }
+    if (d.nparts < 1 || d.nparts > KF_MAX_PARTS || d.part_width <= 0 || d.hout < 1 || d.hdiv < 1 ||
+        (d.hdiv & (d.hdiv - 1)) || d.hdiv > 8) {
+        kf_set_error("operand %s: bad addressing (nparts=%d width=%d hout=%d hdiv=%d)", name,
+                     d.nparts, d.part_width, d.hout, d.hdiv);
+        return false;
+    }
+    if (d.part_width % 8 != 0 || d.ncols % 8 != 0 || d.ld % 8 != 0 || ((uintptr_t)d.base & 15)) {
+        kf_set_error("operand %s: columns / ld / base must be 16-byte granular", name);
+        return false;
+    }
+    if (d.hout > 1 && (long long)(d.hout + BK) * d.hout >= 65536) {
+        kf_set_error("operand %s: hout %d too large", name, d.hout);
+        return false;
+    }
+    memset(&o, 0, sizeof o);
+    o.base = (const h16 *)d.base;
+    o.ld = d.ld;
+    o.nrows = d.nrows;
+    o.ncols = d.ncols;
+    o.nparts = d.nparts;
+    o.pw = d.part_width;
+    o.T = d.T;
+    o.hout = d.hout;
+    o.hsrc = d.hsrc;
+    o.hmul = d.hmul;
+    o.hshift = d.hdiv == 1 ? 0 : d.hdiv == 2 ? 1 : d.hdiv == 4 ? 2 : 3;
+    o.tclamp = d.tpolicy == KF_CLAMP;
+    o.p64 = d.part_width % BK == 0;
+    o.inv_hout = (65536u + d.hout - 1) / d.hout;
+    bool edges = false;
+    for (int i = 0; i < KF_MAX_PARTS; ++i) {
+        o.dt[i] = d.dt[i];
+        o.dh[i] = d.dh[i];
+        o.et[i] = i < d.nparts ? d.edge_t[i] : -1;
+        o.er[i] = d.edge_row[i];
+        if (i < d.nparts && d.edge_t[i] >= 0) edges = true;
+    }
+    o.simple = d.nparts == 1 && d.hout == 1 && d.dt[0] == 0 && !edges;
+    // 32-bit byte offsets (buffer addressing): the largest source row must fit
+    long long rows = d.nrows;
+    if (!o.simple) {
+        rows = d.T + 2;
+        for (int i = 0; i < d.nparts; ++i)
+            if (d.edge_t[i] >= 0 && d.edge_row[i] + 1 > rows) rows = d.edge_row[i] + 1;
+    }
+    if (rows * d.ld * 2 >= (1LL << 32) - 64) {
+        kf_set_error("operand %s: %lld x %lld elements exceed 32-bit buffer addressing", name, rows,
+                     d.ld);
+        return false;
+    }
+    return true;
+}
+
+static int op_mode(const OpD &o) {
+    if (o.simple) return OP_SIMPLE;
+    if (o.nparts <= 2 && o.hout == 1 && o.hmul == 0 && o.hshift == 0) return OP_P2;
+    return OP_GEN;
+}
+
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE>
+static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilogue &E,
+                  const WgradArgs &G, int splits) {
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     dim3 grid(mt * nt, WGRAD ? splits : 1);
     ProfRec rec{};
@@ -482,8 +706,8 @@ static int launch(int M, int N, int K, const KfOperand &A, const KfOperand &B,
         rec.flops = 2.0 * M * N * (double)K;
         hipEventRecord(rec.a, kf_stream());
     }
-    gemm_kernel<BM, BN, BK, WM, WN, AKC, BKC, WGRAD>
-        <<<grid, 256, 0, kf_stream()>>>(M, N, K, A, B, E, G, nt);
+    gemm_kernel<BM, BN, WM, WN, AKC, BKC, WGRAD, ST, AM, BMODE>
+        <<<grid, 256, 0, kf_stream()>>>(M, N, K, A, B, E, G, mt, nt);
     if (g_prof) {
         hipEventRecord(rec.b, kf_stream());
         g_prof_recs.push_back(rec);
@@ -496,34 +720,11 @@ static int launch(int M, int N, int K, const KfOperand &A, const KfOperand &B,
     return 0;
 }
 
-static bool check_operand(const KfOperand &d, const char *name) {
-    if (!d.base) {
-        kf_set_error("operand %s: null base", name);
-        return false;
-    }
-    if (d.nparts < 1 || d.nparts > KF_MAX_PARTS || d.part_width <= 0 || d.hout < 1 ||
-        d.hdiv < 1) {
-        kf_set_error("operand %s: bad addressing (nparts=%d width=%d hout=%d hdiv=%d)", name,
-                     d.nparts, d.part_width, d.hout, d.hdiv);
-        return false;
-    }
-    if (d.part_width % 8 != 0 || d.ncols % 8 != 0 || d.ld % 8 != 0 ||
-        ((uintptr_t)d.base & 15) != 0) {
-        kf_set_error("operand %s: columns / ld / base must be 16-byte granular", name);
-        return false;
-    }
-    for (int p = 0; p < d.nparts; ++p)
-        if (d.edge_t[p] >= 0 && (((uintptr_t)d.edge_ptr[p]) & 15)) {
-            kf_set_error("operand %s: edge row %d misaligned", name, p);
-            return false;
-        }
-    return true;
-}
-
 extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              const KfEpilogue *epi) {
     if (M <= 0 || N <= 0) return 0;
-    if (!check_operand(*A, "A") || !check_operand(*B, "B")) return -1;
+    OpD a, b;
+    if (!to_dev(*A, a, "A") || !to_dev(*B, b, "B")) return -1;
     if (N % 8 != 0) {
         kf_set_error("kf_gemm_fused: N=%d must be a multiple of 8", N);
         return -1;
@@ -539,34 +740,40 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         return -1;
     }
     WgradArgs G{nullptr, nullptr, 0};
-    // tile choice by output width
-    if (B->kcontig) {
-        if (N % 160 == 0 && N <= 320)
-            return launch<128, 160, 64, 2, 2, true, true, false>(M, N, K, *A, *B, E, G, 1);
-        if (N <= 64) return launch<256, 64, 32, 4, 1, true, true, false>(M, N, K, *A, *B, E, G, 1);
-        return launch<128, 128, 64, 2, 2, true, true, false>(M, N, K, *A, *B, E, G, 1);
-    } else {
-        if (N % 160 == 0 && N <= 320)
-            return launch<128, 160, 64, 2, 2, true, false, false>(M, N, K, *A, *B, E, G, 1);
-        if (N <= 64)
-            return launch<256, 64, 32, 4, 1, true, false, false>(M, N, K, *A, *B, E, G, 1);
-        return launch<128, 128, 64, 2, 2, true, false, false>(M, N, K, *A, *B, E, G, 1);
+    const int am = op_mode(a), bm = op_mode(b);
+    const int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : 0);
+#define KF_FUSED(BKC_, AM_, BM_)                                                                 \
+    do {                                                                                         \
+        if (tile == 1) return launch<128, 160, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
+        if (tile == 2) return launch<256, 64, 4, 1, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);  \
+        return launch<128, 128, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);               \
+    } while (0)
+    if (!B->kcontig) {
+        if (bm == OP_SIMPLE) {
+            if (am == OP_SIMPLE) KF_FUSED(false, OP_SIMPLE, OP_SIMPLE);
+            if (am == OP_P2) KF_FUSED(false, OP_P2, OP_SIMPLE);
+            KF_FUSED(false, OP_GEN, OP_SIMPLE);
+        }
+        KF_FUSED(false, OP_GEN, OP_GEN);
     }
+    if (am == OP_SIMPLE && bm == OP_SIMPLE) KF_FUSED(true, OP_SIMPLE, OP_SIMPLE);
+    if (am == OP_P2 && bm == OP_P2) KF_FUSED(true, OP_P2, OP_P2);
+    KF_FUSED(true, OP_GEN, OP_GEN);
+#undef KF_FUSED
 }
 
 extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              float *dW, long long ldw, float *bias_grad, int accumulate) {
     if (M <= 0 || N <= 0) return 0;
-    if (!check_operand(*A, "A") || !check_operand(*B, "B")) return -1;
+    OpD a, b;
+    if (!to_dev(*A, a, "A") || !to_dev(*B, b, "B")) return -1;
     if (A->kcontig || B->kcontig) {
         kf_set_error("kf_gemm_wgrad: A and B must be reduction-major");
         return -1;
     }
-    // tile + split choice: aim for >= ~2 workgroups per CU
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
     if (BNc == 64) BMc = 256;
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
-    const int BK = (BNc == 64) ? 32 : 64;
     int splits = (512 + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
     if (splits > maxsplit) splits = maxsplit;
@@ -582,14 +789,17 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
                      slab_bytes + bias_bytes);
         return -1;
     }
-    WgradArgs G{(float *)ws, bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255))
-                                       : nullptr,
-                kps};
+    WgradArgs G{(float *)ws,
+                bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255)) : nullptr, kps};
     KfEpilogue E{};
+    const int am = op_mode(a), bm = op_mode(b);
     int rc;
-    if (BNc == 160) rc = launch<128, 160, 64, 2, 2, false, false, true>(M, N, K, *A, *B, E, G, splits);
-    else if (BNc == 64) rc = launch<256, 64, 32, 4, 1, false, false, true>(M, N, K, *A, *B, E, G, splits);
-    else rc = launch<128, 128, 64, 2, 2, false, false, true>(M, N, K, *A, *B, E, G, splits);
+#define KF_WG(AM_, BM_)                                                                                do {                                                                                                   if (BNc == 160) rc = launch<128, 160, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits);         else if (BNc == 64) rc = launch<256, 64, 4, 1, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits);         else rc = launch<128, 128, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits);     } while (0)
+    if (bm == OP_SIMPLE && am == OP_SIMPLE) KF_WG(OP_SIMPLE, OP_SIMPLE);
+    else if (bm == OP_SIMPLE && am == OP_P2) KF_WG(OP_P2, OP_SIMPLE);
+    else if (bm == OP_SIMPLE) KF_WG(OP_GEN, OP_SIMPLE);
+    else KF_WG(OP_GEN, OP_GEN);
+#undef KF_WG
     if (rc) return rc;
     k_slab_reduce<<<kf_blocks((long long)M * N, 256, 4096), 256, 0, kf_stream()>>>(
         G.slab, splits, M, N, dW, ldw, accumulate);
@@ -636,6 +846,7 @@ static KfOperand plain_operand(const void *p, long long ld, int rows, int cols, 
     for (int i = 0; i < KF_MAX_PARTS; ++i) d.edge_t[i] = -1;
     return d;
 }
+
 
 // ---------------------------------------------------------------------------
 // reference ABI GEMM (ops.h) on the same kernels

@@ -465,11 +465,12 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
                         nl.bn2_scale, nl.bn2_shift)))
             return nullptr;
     }
+    // gradient buffers carry two spare rows for the splice-transpose edge sums
     for (int i = 0; i < 2; ++i) {
-        net->dz[i] = net->dalloc(T * maxw * 2);
-        net->g[i] = net->dalloc(T * maxw * 2);
+        net->dz[i] = net->dalloc((T + 2) * maxw * 2);
+        net->g[i] = net->dalloc((T + 2) * maxw * 2);
     }
-    net->dbott = net->dalloc(T * maxw * 2);
+    net->dbott = net->dalloc((T + 2) * maxw * 2);
     net->edge_half = align_up(maxw * 2, 256);
     net->edge = net->dalloc(net->edge_half * 2);
     if (!net->dz[0] || !net->dz[1] || !net->g[0] || !net->g[1] || !net->dbott || !net->edge) {
@@ -879,12 +880,13 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 E1.out = dbott;
                 E1.ldo = bn;
                 if (s > 0) {
-                    void *edge = net->edge;
+                    // spare row T of dz holds sum_{t >= T-1-s} dz[t] (clamped-splice transpose)
+                    void *edge = (char *)dz + (size_t)T * dout * 2;
                     if (!ck(kf_rows_sum(edge, dz, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout), "edge"))
                         return -1;
                     KfOperand A1 = op_splice(dz, T, dout, 0, -s, KF_ZERO, 1);
                     A1.edge_t[1] = T - 1;
-                    A1.edge_ptr[1] = edge;
+                    A1.edge_row[1] = T;
                     KfOperand B1 = op_wrows(wptr(net, nl.pW2), 2, bn, dout);
                     if (!ck(kf_gemm_fused(T, bn, 2 * dout, &A1, &B1, &E1), "tdnnf affine dgrad"))
                         return -1;
@@ -903,12 +905,13 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 if (want_dx) {
                     // input gradient: transpose of the [-s, 0] clamped splice
                     if (s > 0) {
-                        void *edge = (char *)net->edge + net->edge_half;
+                        // spare row T of dbott holds sum_{t <= s} dbott[t]
+                        void *edge = (char *)dbott + (size_t)T * bn * 2;
                         if (!ck(kf_rows_sum(edge, dbott, bn, 0, s + 1 < T ? s + 1 : T, bn), "edge"))
                             return -1;
                         KfOperand A3 = op_splice(dbott, T, bn, s, 0, KF_ZERO, 1);
                         A3.edge_t[0] = 0;
-                        A3.edge_ptr[0] = edge;
+                        A3.edge_row[0] = T;
                         KfOperand B3 = op_wrows(wptr(net, nl.pW), 2, din, bn);
                         if (!ck(kf_gemm_fused(T, din, 2 * bn, &A3, &B3, &E), "tdnnf linear dgrad"))
                             return -1;

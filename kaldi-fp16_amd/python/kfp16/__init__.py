@@ -324,7 +324,7 @@ class KfOperand(C.Structure):
     _fields_ = [("base", _vp), ("ld", _ll), ("nrows", _i), ("ncols", _i), ("kcontig", _i),
                 ("nparts", _i), ("part_width", _i), ("T", _i), ("hout", _i), ("hsrc", _i),
                 ("hmul", _i), ("hdiv", _i), ("tpolicy", _i), ("dt", _i * MAXP), ("dh", _i * MAXP),
-                ("edge_t", _i * MAXP), ("edge_ptr", _vp * MAXP)]
+                ("edge_t", _i * MAXP), ("edge_row", _i * MAXP)]
 
 
 class KfEpilogue(C.Structure):
@@ -346,9 +346,9 @@ def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, ho
         o.dt[i] = v
     for i, v in enumerate(dh):
         o.dh[i] = v
-    for p, t, ptr in edges:
+    for p, t, row in edges:
         o.edge_t[p] = t
-        o.edge_ptr[p] = ptr
+        o.edge_row[p] = row
     return o
 
 
