@@ -42,6 +42,8 @@ struct OpD {
     int T, hout, hsrc, hmul, hshift;
     int tclamp, simple, p64;
     unsigned inv_hout;  // ceil(2^16 / hout): exact t = h/hout for h*hout < 2^16
+    unsigned ldb, pwb;  // ld and part_width in bytes (32-bit addressing is checked on the host)
+    int edges;          // any edge rows
     int dt[KF_MAX_PARTS], dh[KF_MAX_PARTS], et[KF_MAX_PARTS], er[KF_MAX_PARTS];
 };
 
@@ -264,21 +266,26 @@ struct Stager {
                 const int r = k0 + mn_row(q, lane);
                 if (r < klim && o0[j] != BAD) {
                     if constexpr (MODE == OP_SIMPLE) {
-                        voff = o0[j] + (unsigned)((long long)k0 * d.ld * 2);
+                        voff = o0[j] + (unsigned)k0 * d.ldb;
                     } else if constexpr (MODE == OP_P2) {
                         int st = r + dt1[j];
                         bool ok = true;
                         if (d.tclamp) st = min(max(st, 0), d.T - 1);
                         else ok = (unsigned)st < (unsigned)d.T;
-                        if (ok) voff = (unsigned)((long long)st * d.ld * 2) + o0[j];
+                        if (ok) voff = (unsigned)st * d.ldb + o0[j];
                     } else {
+                        // conv im2col rows (t, h): no edge rows on this path (host-checked)
                         const int hx = h0 + mn_row(q, lane);
                         const int qd = (int)(((unsigned)hx * d.inv_hout) >> 16);
-                        const int tt = t0 + qd, hh = hx - qd * d.hout;
-                        const int p = th[j] >> 8;
-                        const unsigned b = op_boff(d, tt, hh, 0, dt1[j], (th[j] & 0xFF) - 128,
-                                                   sel9(d.et, p, d.nparts), sel9(d.er, p, d.nparts));
-                        if (b != BAD) voff = b + o0[j];
+                        const int st = t0 + qd + dt1[j];
+                        int sh = (hx - qd * d.hout) * d.hmul + ((th[j] & 0xFF) - 128);
+                        bool ok = (unsigned)st < (unsigned)d.T;
+                        if (d.hshift) {
+                            ok = ok && !(sh & ((1 << d.hshift) - 1));
+                            sh >>= d.hshift;
+                        }
+                        ok = ok && (unsigned)sh < (unsigned)d.hsrc;
+                        if (ok) voff = (unsigned)st * d.ldb + (unsigned)sh * d.pwb + o0[j];
                     }
                 }
             }
@@ -672,6 +679,9 @@ static bool to_dev(const KfOperand &d, OpD &o, const char *name) {
         if (i < d.nparts && d.edge_t[i] >= 0) edges = true;
     }
     o.simple = d.nparts == 1 && d.hout == 1 && d.dt[0] == 0 && !edges;
+    o.edges = edges;
+    o.ldb = (unsigned)(d.ld * 2);
+    o.pwb = (unsigned)(d.part_width * 2);
     // 32-bit byte offsets (buffer addressing): the largest source row must fit
     long long rows = d.nrows;
     if (!o.simple) {
@@ -691,6 +701,14 @@ static int op_mode(const OpD &o) {
     if (o.simple) return OP_SIMPLE;
     if (o.nparts <= 2 && o.hout == 1 && o.hmul == 0 && o.hshift == 0) return OP_P2;
     return OP_GEN;
+}
+// the reduction-major general stager has no edge-row path
+static bool mn_gen_ok(const OpD &o, const char *name) {
+    if (op_mode(o) == OP_GEN && o.edges) {
+        kf_set_error("operand %s: edge rows need a time-only (<= 2 part) reduction-major operand", name);
+        return false;
+    }
+    return true;
 }
 
 template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE>
@@ -733,6 +751,7 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         kf_set_error("kf_gemm_fused: A must be k-contiguous");
         return -1;
     }
+    if (!B->kcontig && !mn_gen_ok(b, "B")) return -1;
     const KfEpilogue &E = *epi;
     if ((E.out && E.ldo % 8) || (E.out2 && E.ldo2 % 8) || (E.resid && E.ldr % 8) ||
         (E.mask_out && E.ldo % 8)) {
@@ -771,6 +790,7 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         kf_set_error("kf_gemm_wgrad: A and B must be reduction-major");
         return -1;
     }
+    if (!mn_gen_ok(a, "A") || !mn_gen_ok(b, "B")) return -1;
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
     if (BNc == 64) BMc = 256;
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);

@@ -93,40 +93,70 @@ __global__ void k_conv_c1_fwd(ConvC1 c, const h16 *x, const h16 *W, const h16 *b
     }
 }
 
-// partial dW / db of the 1-filter conv: each block reduces a contiguous range of
-// rows into slab[block][noff+1][fout] (row noff = bias), fixed order (deterministic)
-__global__ void k_conv_c1_wgrad(ConvC1 c, const h16 *x, const h16 *dz, float *slab,
-                                int rows_per_block) {
-    const int f = threadIdx.x % c.fout;
-    const int rg = threadIdx.x / c.fout, nrg = blockDim.x / c.fout;
+// partial dW / db of the 1-filter conv. Thread = (row group, 8 consecutive
+// filters): 16-byte dz loads, the <= 9 input taps per row read through L1.
+// Each block reduces a contiguous range of rows in a fixed order into
+// slab[block][noff+1][fout] (row noff = bias): deterministic, HBM-rate.
+constexpr int C1_UNROLL = 4;
+__global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, const h16 *x, const h16 *dz,
+                                                       float *slab, int rows_per_block) {
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [256][10*8]
+    const int fg = c.fout / 8;                 // threads per row
+    const int lane_f = threadIdx.x % fg, rg = threadIdx.x / fg, nrg = blockDim.x / fg;
     const long long rows = (long long)c.T * c.hout;
     const long long r0 = (long long)blockIdx.x * rows_per_block;
     const long long r1 = min(rows, r0 + rows_per_block);
-    float acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (long long r = r0 + rg; r < r1; r += nrg) {
-        const float g = h2f(dz[r * c.fout + f]);
-        const int t = (int)(r / c.hout), h = (int)(r - (long long)t * c.hout);
+    float acc[10][8];
 #pragma unroll
-        for (int o = 0; o < 9; ++o) {
-            if (o >= c.noff) break;
-            const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
-            if (ts < 0 || ts >= c.T || hs < 0 || hs >= c.hin) continue;
-            acc[o] += g * h2f(x[(long long)ts * c.hin + hs]);
+    for (int o = 0; o < 10; ++o)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[o][e] = 0.f;
+    for (long long rb = r0 + rg; rb < r1; rb += (long long)nrg * C1_UNROLL) {
+        half8 g[C1_UNROLL];
+        float xv[C1_UNROLL][9];
+#pragma unroll
+        for (int u = 0; u < C1_UNROLL; ++u) {
+            const long long r = rb + (long long)u * nrg;
+            g[u] = half8{};
+#pragma unroll
+            for (int o = 0; o < 9; ++o) xv[u][o] = 0.f;
+            if (r < r1) {
+                g[u] = load_h8(dz + r * c.fout + 8 * lane_f);
+                const int t = (int)(r / c.hout), h = (int)(r - (long long)t * c.hout);
+#pragma unroll
+                for (int o = 0; o < 9; ++o) {
+                    if (o >= c.noff) break;
+                    const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
+                    if (ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin)
+                        xv[u][o] = h2f(x[(long long)ts * c.hin + hs]);
+                }
+            }
         }
-        acc[9] += g;
+#pragma unroll
+        for (int u = 0; u < C1_UNROLL; ++u)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float gv = (float)g[u][e];
+#pragma unroll
+                for (int o = 0; o < 9; ++o) acc[o][e] = fmaf(gv, xv[u][o], acc[o][e]);
+                acc[9][e] += gv;
+            }
     }
-    __shared__ float red[256 * 10];
+    float *mine = red + threadIdx.x * 80;
 #pragma unroll
-    for (int o = 0; o < 10; ++o) red[o * 256 + threadIdx.x] = acc[o];
+    for (int o = 0; o < 10; ++o)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mine[o * 8 + e] = acc[o][e];
     __syncthreads();
-    if (rg == 0) {
-        float *out = slab + (long long)blockIdx.x * (c.noff + 1) * c.fout;
-        for (int o = 0; o <= c.noff; ++o) {
-            const int src = o == c.noff ? 9 : o;
-            float s = 0.f;
-            for (int k = 0; k < nrg; ++k) s += red[src * 256 + k * c.fout + f];
-            out[o * c.fout + f] = s;
-        }
+    // output (o, f): sum over row groups in fixed order
+    float *out = slab + (long long)blockIdx.x * (c.noff + 1) * c.fout;
+    for (int i = threadIdx.x; i < (c.noff + 1) * c.fout; i += blockDim.x) {
+        const int o = i / c.fout, f = i - o * c.fout;
+        const int src = o == c.noff ? 9 : o;
+        const int tf = f / 8, e = f - tf * 8;
+        float s = 0.f;
+        for (int k = 0; k < nrg; ++k) s += red[(k * fg + tf) * 80 + src * 8 + e];
+        out[i] = s;
     }
 }
 
@@ -228,7 +258,7 @@ int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, co
 
 int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
                      const int *dh, const void *x, const void *dz, float *dW, float *db) {
-    if (noff > 9 || fout > 256 || 256 % fout) {
+    if (noff > 9 || fout % 8 || fout > 256 || 256 % (fout / 8)) {
         lay_set_error("conv_c1_wgrad: noff=%d fout=%d unsupported", noff, fout);
         return -1;
     }
@@ -238,9 +268,9 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
         c.dh[i] = dh[i];
     }
     const long long rows = (long long)T * hout;
-    int nblk = 1024;
+    int nblk = 2048;
     int rpb = (int)((rows + nblk - 1) / nblk);
-    if (rpb < 64) rpb = 64;
+    if (rpb < 256) rpb = 256;
     nblk = (int)((rows + rpb - 1) / rpb);
     const int n = (noff + 1) * fout;
     float *slab = (float *)kf_workspace((size_t)nblk * n * 4, 2);
@@ -248,7 +278,8 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
         lay_set_error("conv_c1_wgrad: workspace");
         return -1;
     }
-    k_conv_c1_wgrad<<<nblk, 256, 0, kf_stream()>>>(c, (const h16 *)x, (const h16 *)dz, slab, rpb);
+    k_conv_c1_wgrad<<<nblk, 256, 256 * 80 * 4, kf_stream()>>>(c, (const h16 *)x, (const h16 *)dz,
+                                                              slab, rpb);
     k_conv_c1_reduce<<<(n + 255) / 256, 256, 0, kf_stream()>>>(slab, nblk, n, dW, db, noff * fout);
     return lay_check("conv_c1_wgrad");
 }
