@@ -2,10 +2,12 @@
 """bench.py — frames/sec of the CNN-TDNN fwd+bwd training step on MI355X.
 
 Metric (BASELINE.json): frames/sec CNN-TDNN fwd+bwd, 40-dim x 1500-frame egs,
-1/2/4/8 MI355X. One step = forward + backward + gradient all-reduce (N > 1) +
-SGD over one minibatch of 64 synthetic egs (96,000 frames) per GPU, on the
-pinned synthetic 17-TDNN-F model (configs/cnn_tdnn_17f.xconfig).
-Inputs are resident in HBM before the timed region.
+1/2/4/8 MI355X. One step = TrainStep (train_step.go:142-283): forward, chain
+LF-MMI objective + derivative (numerator and leaky-HMM denominator per eg,
+backward.go:224-371), backward, gradient all-reduce (N > 1) and SGD, over one
+minibatch of 64 synthetic egs (96,000 frames) per GPU, on the pinned synthetic
+17-TDNN-F model (configs/cnn_tdnn_17f.xconfig) with the synthetic den graph and
+numerator FSTs of SURVEY §8d. Inputs are resident in HBM before the timed region.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one process per GPU, RCCL all-reduce of the flat fp32
@@ -38,7 +40,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--egs", type=int, default=64, help="egs per GPU")
     p.add_argument("--xconfig", default="cnn_tdnn_17f.xconfig")
-    p.add_argument("--lr", type=float, default=1e-4)
+    # the reference's plain SGD has no max-change; with the chain gradient summed over
+    # 31,360 supervised frames per GPU, 1e-8 keeps the random-init model from diverging
+    p.add_argument("--lr", type=float, default=1e-8)
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-frames", type=int, default=1500)
@@ -47,8 +51,9 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(xcfg, params, bns, frames, threads):
-    """The C oracle (a port of the reference's CNN-TDNN math) timed on host cores."""
+def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
+    """The C oracle (a port of the reference's CNN-TDNN math and chain objective)
+    timed on host cores: forward, objective on the subsampled frames, backward."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from kfp16 import synth
@@ -60,15 +65,21 @@ def cpu_baseline(xcfg, params, bns, frames, threads):
     tp = {k: synth.trunc_fp16(v) for k, v in params.items()}
     on = oracle.OracleNet(xcfg, tp, bns, round_mode=oracle.ROUND_FUSED, threads=threads)
     feats = synth.make_features(frames, 40).astype(np.float32)
-    og = (np.random.default_rng(5).standard_normal((frames, 3080)) * 0.02).astype(np.float16).astype(np.float32)
+    g, init = den
+    row0, nfr, stride = synth.chain_layout(1, frames)
+    rows = row0[0] + np.arange(nfr[0]) * stride
     t0 = time.perf_counter()
     on.forward(feats)
+    out = on.act("output")
+    deriv, _ = oracle.chain_objf(g, init, num_fst, out[rows])
+    og = np.zeros_like(out)
+    og[rows] = (-deriv).astype(np.float16).astype(np.float32)
     on.backward(og)
     dt = time.perf_counter() - t0
     on.close()
     return {"value": round(frames / dt, 2), "unit": "frames/sec", "cores": threads, "kind": "port",
-            "sample": f"C oracle fwd+bwd of cnn_tdnn_17f on {frames} frames (1 eg), fp32 math, "
-                      f"{threads} threads, {dt:.1f} s"}
+            "sample": f"C oracle train step (fwd, chain objective, bwd) of cnn_tdnn_17f on {frames} "
+                      f"frames (1 eg), fp32 math, {threads} threads for the GEMMs, {dt:.1f} s"}
 
 
 def main():
@@ -97,16 +108,23 @@ def main():
     feats = synth.make_features(T, 40, seed=1234 + rank)   # this rank's shard of egs
     fbuf = torch.from_numpy(feats.view(np.int16)).to("cuda")
     P = net.layers[-1][3]
-    # output gradient of the chain objective's shape: non-zero only on the
-    # subsampled frames (leftCtx 30, stride 3), as TrainStep scatters it
-    og = np.zeros((T, P), np.float16)
-    rows = np.concatenate([np.arange(30, FRAMES_PER_EG, 3) + e * FRAMES_PER_EG for e in range(a.egs)])
-    og[rows] = (np.random.default_rng(99 + rank).standard_normal((len(rows), P)) * 0.02).astype(np.float16)
-    gbuf = torch.from_numpy(og.view(np.int16)).to("cuda")
+    # chain supervision: shared den graph, one numerator FST per eg
+    # (seed 7 + global eg index); the objective writes the output gradient on the
+    # subsampled rows (leftCtx 30, stride 3) — every other row stays zero
+    from kfp16 import chain
+    den_g = synth.make_den_graph(num_pdfs=P)
+    dgraph = chain.DenGraph(den_g)
+    fsts = [synth.make_num_fst(rank * a.egs + e, num_pdfs=P) for e in range(a.egs)]
+    nbatch = chain.NumBatch(fsts)
+    row0, nfr, stride = synth.chain_layout(a.egs, FRAMES_PER_EG)
+    objective = chain.Chain(dgraph, max_seqs=a.egs, max_frames=int(nfr.max()))
+    out_ptr = net.activation("output")[0]
+    gbuf = torch.zeros((T, P), dtype=torch.float16, device="cuda")
     torch.cuda.synchronize()
 
     def step():
         net.forward(fbuf.data_ptr(), T)
+        objective.compute(nbatch, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
         net.backward(gbuf.data_ptr())
         if world > 1:
             dist.all_reduce(grad)
@@ -115,6 +133,9 @@ def main():
 
     for _ in range(a.warmup):
         step()
+        if os.environ.get("KF_BENCH_CHECK"):
+            r = objective.result()
+            print("warmup objf/frame", r.objf / max(r.frames, 1), "ok", r.num_ok, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -135,12 +156,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    prof = {}
+    prof, chain_prof = {}, {}
     if not a.no_prof:
         for cls, name in ((0, "gemm_fused"), (1, "gemm_wgrad")):
             n, ms, fl = kfp16.prof_collect(cls)
             prof[name] = (n, ms, fl)
+        for cls, name in ((2, "chain_num"), (3, "chain_den")):
+            chain_prof[name] = kfp16.prof_collect(cls)
         kfp16.core.kf_prof_reset()
+    res = objective.result()
+    stats = torch.tensor([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
+                         dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(stats)
 
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
@@ -154,8 +182,16 @@ def main():
             "config": {"workload": "cnn_tdnn_17f train step (fwd+bwd+SGD), 64 egs x 1500 frames per GPU",
                        "xconfig": a.xconfig, "egs_per_gpu": a.egs, "frames_per_eg": FRAMES_PER_EG,
                        "global_batch_egs": a.egs * world, "parallelism": f"dp{world}",
-                       "output_grad": "synthetic fp16 on subsampled frames (chain objective not in step)"},
+                       "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)"},
+            "objf_per_frame": round(float(stats[0]) / max(float(stats[3]), 1.0), 5),
+            "objective_finite_seqs": f"{int(stats[4])}/{a.egs * world}",
         }
+        if chain_prof:
+            (nn, nms, _), (dn, dms, dbytes) = chain_prof["chain_num"], chain_prof["chain_den"]
+            out["chain"] = {"num_ms_per_step": round(nms / a.steps, 3),
+                            "den_ms_per_step": round(dms / a.steps, 3),
+                            "den_algorithmic_GBps": round(dbytes / (dms * 1e-3) / 1e9, 1) if dms else None,
+                            "ok_seqs": int(stats[4])}
         if prof:
             dom = max(prof, key=lambda k: prof[k][1])
             n, ms, fl = prof[dom]
@@ -166,8 +202,13 @@ def main():
                                "all_gemm_tflops": round(sum(v[2] for v in prof.values()) /
                                                         (sum(v[1] for v in prof.values()) * 1e-3) / 1e12, 2)}
         if world == 1 and not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, a.cpu_threads)
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+            den = (den_g, oracle.den_initial_probs(den_g))
+            out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, a.cpu_threads,
+                                               den, synth.make_num_fst(0, num_pdfs=P))
         print(json.dumps(out), flush=True)
+    objective.close()
     net.close()
     if world > 1:
         dist.destroy_process_group()

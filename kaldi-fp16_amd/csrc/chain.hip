@@ -1,0 +1,2251 @@
+// chain.hip — chain LF-MMI objective on MI355X (gfx950).
+//
+// Two workgroup-resident kernels replace the reference's per-frame launch
+// storms (chain.cu launches T kernels per pass with CAS atomics;
+// chain_den.cu ~10 launches + 3 blocking D2H copies per frame):
+//
+//   k_logfb   log-domain forward-backward of one FST per workgroup, all frames
+//             in one launch, fixed arc order (the deterministic algorithm of
+//             chain_det.cu:55-237; posteriors summed per pdf in arc order, i.e.
+//             exactly the order of chain_det.cu:147-190's single thread).
+//   k_den_fb  probability-space denominator of chain_den.cu:496-706 with the
+//             leaky HMM, one sequence per workgroup: alpha'/beta state vectors
+//             and the frame's exp(x) row live in LDS; arcs are streamed from a
+//             sliced, degree-sorted table (SELL-64: lane = state, one coalesced
+//             8-byte record per arc and step); den posteriors accumulate in LDS
+//             as 2^-44 fixed point (ds_add_u64 — order-independent, hence
+//             deterministic); the product mode fuses the whole objective
+//             assembly of backward.go:224-371 (penalty, +w*num, -w*den, L2, NaN
+//             rule) into the per-frame epilogue and writes the fp16 gradient
+//             row straight into the network's output-gradient matrix.
+//
+// The C-ABI of chain.h / chain_den.h / chain_backward_api.h is served by the same
+// kernels; kf_chain.h is the batched, device-resident product interface.
+#include "kf_common.h"
+#include "../../include/chain.h"
+#include "../../include/chain_backward_api.h"
+#include "../../include/chain_den.h"
+#include "../../include/kf_chain.h"
+#include "../../include/kf_ops.h"
+
+#include <cmath>
+#include <map>
+#include <mutex>
+#include <vector>
+
+KF_DECLARE_ERR(chain)
+KF_DECLARE_ERR(den)
+KF_DECLARE_ERR(kfc)
+
+extern "C" const char *chain_last_error(void) { return chain_err_.get(); }
+extern "C" void chain_clear_error(void) { chain_err_.clear(); }
+extern "C" const char *den_last_error(void) { return den_err_.get(); }
+extern "C" void den_clear_error(void) { den_err_.clear(); }
+extern "C" const char *kf_chain_last_error(void) { return kfc_err_.get(); }
+extern "C" void kf_chain_clear_error(void) { kfc_err_.clear(); }
+
+static const float kLogZero = -1.0e+30f;
+static const float kFix = 17592186044416.0f;          // 2^44
+static const double kInvFix = 1.0 / 17592186044416.0;  // 2^-44
+
+// ===========================================================================
+// Device helpers
+// ===========================================================================
+__device__ __forceinline__ float logadd_dev(float a, float b) {  // chain_det.cu:26-35
+    if (a <= kLogZero) return b;
+    if (b <= kLogZero) return a;
+    float mx = fmaxf(a, b), mn = fminf(a, b);
+    return mx + log1pf(expf(mn - mx));
+}
+
+template <typename XT>
+__device__ __forceinline__ float ld_x(const XT *p) { return (float)*p; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+// Deterministic block sum: wave butterflies, then the per-wave sums in wave order.
+// Every thread returns the same value. Contains one barrier; `red` must not be
+// reused before the next barrier.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float *red) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w];
+    return s;
+}
+template <int NW>
+__device__ __forceinline__ double block_sum_d(double v, double *red) {
+    v = wave_sum_d(v);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w];
+    return s;
+}
+
+// ===========================================================================
+// Log-domain forward-backward (numerator; chain.h ABI)
+// ===========================================================================
+struct LogFstDev {
+    const int *row_ptr, *in_ptr, *in_arc, *arc_src, *arc_dst, *arc_pdf;
+    const float *arc_w;
+    const int *grp_ptr, *grp_pdf, *grp_arc;
+    // pre-gathered copies for the LDS-resident kernel (k_num_fb)
+    const int *in_src, *in_g, *arc_g, *gsrc, *gdst;
+    const float *in_w, *gw;
+    const int *fin_state;
+    const float *fin_w;
+    int S, A, G, nfinal, start, T;
+    int mode;        // bit0: forward+backward, bit1: posteriors
+    int stride;
+    long long row0;  // frame t -> nnet row row0 + t*stride
+    float *alpha, *beta;  // [(T+1) x S]
+    float *post_sparse;   // [T x G] or null
+    float *post_dense;    // [T x P] or null
+    float *total;         // [1] (in: when mode has no forward)
+};
+
+enum { LF_FB = 1, LF_POST = 2 };
+
+__global__ __launch_bounds__(256) void k_logfb(const LogFstDev *fsts, const h16 *nnet, long long ld,
+                                               int P) {
+    const LogFstDev f = fsts[blockIdx.x];
+    const int S = f.S, T = f.T, tid = threadIdx.x;
+    if (S <= 0 || T < 0) return;
+    float total;
+    if (f.mode & LF_FB) {
+        for (int s = tid; s < S; s += 256) f.alpha[s] = (s == f.start) ? 0.0f : kLogZero;
+        __syncthreads();
+        for (int t = 0; t < T; ++t) {
+            const h16 *xr = nnet + (f.row0 + (long long)t * f.stride) * ld;
+            const float *ac = f.alpha + (size_t)t * S;
+            float *an = f.alpha + (size_t)(t + 1) * S;
+            for (int d = tid; d < S; d += 256) {
+                float v = kLogZero;
+                for (int k = f.in_ptr[d]; k < f.in_ptr[d + 1]; ++k) {
+                    int a = f.in_arc[k];
+                    int p = f.arc_pdf[a];
+                    if (p <= 0 || p > P) continue;
+                    float sa = ac[f.arc_src[a]];
+                    if (sa <= kLogZero) continue;
+                    v = logadd_dev(v, sa + (float)xr[p - 1] + f.arc_w[a]);
+                }
+                an[d] = v;
+            }
+            __syncthreads();
+        }
+        total = kLogZero;
+        for (int i = 0; i < f.nfinal; ++i)
+            total = logadd_dev(total, f.alpha[(size_t)T * S + f.fin_state[i]] + f.fin_w[i]);
+        if (tid == 0) *f.total = total;
+        float *bT = f.beta + (size_t)T * S;
+        for (int s = tid; s < S; s += 256) bT[s] = kLogZero;
+        __syncthreads();
+        if (tid == 0)
+            for (int i = 0; i < f.nfinal; ++i) bT[f.fin_state[i]] = f.fin_w[i];
+        __syncthreads();
+    } else {
+        total = *f.total;
+    }
+    for (int t = T - 1; t >= 0; --t) {
+        const h16 *xr = nnet + (f.row0 + (long long)t * f.stride) * ld;
+        const float *bn = f.beta + (size_t)(t + 1) * S;
+        if (f.mode & LF_FB) {
+            float *bc = f.beta + (size_t)t * S;
+            for (int s = tid; s < S; s += 256) {
+                float v = kLogZero;
+                for (int a = f.row_ptr[s]; a < f.row_ptr[s + 1]; ++a) {
+                    int p = f.arc_pdf[a];
+                    if (p <= 0 || p > P) continue;
+                    float b = bn[f.arc_dst[a]];
+                    if (b <= kLogZero) continue;
+                    v = logadd_dev(v, b + (float)xr[p - 1] + f.arc_w[a]);
+                }
+                bc[s] = v;
+            }
+        }
+        if (f.mode & LF_POST) {
+            float *pd = f.post_dense ? f.post_dense + (size_t)t * P : nullptr;
+            if (pd) {
+                for (int p = tid; p < P; p += 256) pd[p] = 0.0f;
+                __syncthreads();
+            }
+            const float *ac = f.alpha + (size_t)t * S;
+            for (int g = tid; g < f.G; g += 256) {
+                int p = f.grp_pdf[g];
+                float acc = 0.0f;
+                if (p > 0 && p <= P) {
+                    float xv = (float)xr[p - 1];
+                    for (int k = f.grp_ptr[g]; k < f.grp_ptr[g + 1]; ++k) {
+                        int a = f.grp_arc[k];
+                        float av = ac[f.arc_src[a]];
+                        if (av <= kLogZero) continue;
+                        float b = bn[f.arc_dst[a]];
+                        if (b <= kLogZero) continue;
+                        float lp = av + xv + f.arc_w[a] + b - total;
+                        if (lp > 0.0f) lp = 0.0f;  // chain.cu:309-311
+                        acc += expf(lp);
+                    }
+                    if (pd) pd[p - 1] = acc;
+                }
+                if (f.post_sparse) f.post_sparse[(size_t)t * f.G + g] = acc;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Product numerator: the whole FST (arcs pre-gathered per incoming / outgoing /
+// pdf-group order) lives in LDS; per frame only the G distinct pdf values of the
+// output row are fetched, one frame ahead. Same arithmetic and order as k_logfb.
+// ---------------------------------------------------------------------------
+#define NUM_THREADS 256
+#define NUM_PRE 16  // S, G <= 4096
+
+struct NumLds {  // word offsets into dynamic LDS
+    int a0, a1, ar0, ar1, xg0, xg1, in_ptr, in_src, in_g, in_w, row_ptr, arc_dst, arc_g, arc_w,
+        grp_ptr, gsrc, gdst, gw, gpdf, misc, words;
+};
+__host__ __device__ inline NumLds num_lds_layout(int S, int A, int G, int Ag) {
+    NumLds L;
+    int o = 0;
+    L.a0 = o; o += S;
+    L.a1 = o; o += S;
+    L.ar0 = o; o += S;
+    L.ar1 = o; o += S;
+    L.xg0 = o; o += G;
+    L.xg1 = o; o += G;
+    L.in_ptr = o; o += S + 1;
+    L.in_src = o; o += A;
+    L.in_g = o; o += A;
+    L.in_w = o; o += A;
+    L.row_ptr = o; o += S + 1;
+    L.arc_dst = o; o += A;
+    L.arc_g = o; o += A;
+    L.arc_w = o; o += A;
+    L.grp_ptr = o; o += G + 1;
+    L.gsrc = o; o += Ag;
+    L.gdst = o; o += Ag;
+    L.gw = o; o += Ag;
+    L.gpdf = o; o += G;
+    L.misc = o; o += 4;
+    L.words = o;
+    return L;
+}
+
+__global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, const h16 *nnet,
+                                                        long long ld, int P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const LogFstDev f = fsts[blockIdx.x];
+    const int S = f.S, A = f.A, G = f.G, T = f.T, tid = threadIdx.x;
+    const int Ag = f.G > 0 ? f.grp_ptr[f.G] : 0;
+    const NumLds L = num_lds_layout(S, A, G, Ag);
+    float *W = reinterpret_cast<float *>(smem);
+    int *I = reinterpret_cast<int *>(smem);
+    // stage the FST; arcs whose pdf is outside [1, P] get group -1 (skipped)
+    for (int i = tid; i <= S; i += NUM_THREADS) {
+        I[L.in_ptr + i] = f.in_ptr[i];
+        I[L.row_ptr + i] = f.row_ptr[i];
+    }
+    for (int q = tid; q < G; q += NUM_THREADS) I[L.gpdf + q] = f.grp_pdf[q];
+    for (int q = tid; q <= G; q += NUM_THREADS) I[L.grp_ptr + q] = f.grp_ptr[q];
+    for (int k = tid; k < A; k += NUM_THREADS) {
+        int g0 = f.in_g[k], g1 = f.arc_g[k];
+        int p0 = g0 >= 0 ? f.grp_pdf[g0] : 0, p1 = g1 >= 0 ? f.grp_pdf[g1] : 0;
+        I[L.in_src + k] = f.in_src[k];
+        I[L.in_g + k] = (p0 > 0 && p0 <= P) ? g0 : -1;
+        W[L.in_w + k] = f.in_w[k];
+        I[L.arc_dst + k] = f.arc_dst[k];
+        I[L.arc_g + k] = (p1 > 0 && p1 <= P) ? g1 : -1;
+        W[L.arc_w + k] = f.arc_w[k];
+    }
+    for (int k = tid; k < Ag; k += NUM_THREADS) {
+        I[L.gsrc + k] = f.gsrc[k];
+        I[L.gdst + k] = f.gdst[k];
+        W[L.gw + k] = f.gw[k];
+    }
+    float *cur = W + L.a0, *nxt = W + L.a1;
+    for (int s = tid; s < S; s += NUM_THREADS) {
+        float v = (s == f.start) ? 0.0f : kLogZero;
+        cur[s] = v;
+        f.alpha[s] = v;
+    }
+    __syncthreads();
+    auto row_of = [&](int t) { return nnet + (f.row0 + (long long)t * f.stride) * ld; };
+    float pre[NUM_PRE];
+    auto fetch_x = [&](int t) {
+        const h16 *xr = row_of(t);
+#pragma unroll
+        for (int i = 0; i < NUM_PRE; ++i) {
+            int q = tid + i * NUM_THREADS;
+            int p = q < G ? I[L.gpdf + q] : 0;
+            pre[i] = (p > 0 && p <= P) ? (float)xr[p - 1] : 0.0f;
+        }
+    };
+    auto store_x = [&](float *xg) {
+#pragma unroll
+        for (int i = 0; i < NUM_PRE; ++i) {
+            int q = tid + i * NUM_THREADS;
+            if (q < G) xg[q] = pre[i];
+        }
+    };
+    // ---- forward
+    if (T > 0) {
+        fetch_x(0);
+        store_x(W + L.xg0);
+        if (T > 1) fetch_x(1);
+    }
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+        const float *xg = W + ((t & 1) ? L.xg1 : L.xg0);
+        float *an = f.alpha + (size_t)(t + 1) * S;
+        for (int d = tid; d < S; d += NUM_THREADS) {
+            float v = kLogZero;
+            for (int k = I[L.in_ptr + d]; k < I[L.in_ptr + d + 1]; ++k) {
+                int g = I[L.in_g + k];
+                if (g < 0) continue;
+                float sa = cur[I[L.in_src + k]];
+                if (sa <= kLogZero) continue;
+                v = logadd_dev(v, sa + xg[g] + W[L.in_w + k]);
+            }
+            nxt[d] = v;
+            an[d] = v;
+        }
+        if (t + 1 < T) {
+            store_x(W + ((t & 1) ? L.xg0 : L.xg1));
+            if (t + 2 < T) fetch_x(t + 2);
+        }
+        __syncthreads();
+        float *tmp = cur;
+        cur = nxt;
+        nxt = tmp;
+    }
+    // total over the finals, in order (chain.cu:213-240)
+    if (tid == 0) {
+        float tot = kLogZero;
+        for (int i = 0; i < f.nfinal; ++i) tot = logadd_dev(tot, cur[f.fin_state[i]] + f.fin_w[i]);
+        W[L.misc] = tot;
+        *f.total = tot;
+    }
+    // ---- backward + posteriors
+    float *bn = W + L.a0, *bc = W + L.a1;  // beta[t+1], beta[t]
+    __syncthreads();
+    const float total = W[L.misc];
+    for (int s = tid; s < S; s += NUM_THREADS) bn[s] = kLogZero;
+    float apre[NUM_PRE];
+    auto fetch_alpha = [&](int t) {
+        const float *ar = f.alpha + (size_t)t * S;
+#pragma unroll
+        for (int i = 0; i < NUM_PRE; ++i) {
+            int s = tid + i * NUM_THREADS;
+            apre[i] = s < S ? ar[s] : 0.0f;
+        }
+    };
+    auto store_alpha = [&](float *dst) {
+#pragma unroll
+        for (int i = 0; i < NUM_PRE; ++i) {
+            int s = tid + i * NUM_THREADS;
+            if (s < S) dst[s] = apre[i];
+        }
+    };
+    if (T > 0) {
+        fetch_x(T - 1);
+        store_x(W + L.xg0);
+        fetch_alpha(T - 1);
+        store_alpha(W + L.ar0);
+        if (T > 1) {
+            fetch_x(T - 2);
+            fetch_alpha(T - 2);
+        }
+    }
+    __syncthreads();
+    if (tid == 0)
+        for (int i = 0; i < f.nfinal; ++i) bn[f.fin_state[i]] = f.fin_w[i];
+    __syncthreads();
+    for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
+        const float *xg = W + ((it & 1) ? L.xg1 : L.xg0);
+        const float *ar = W + ((it & 1) ? L.ar1 : L.ar0);
+        for (int s = tid; s < S; s += NUM_THREADS) {
+            float v = kLogZero;
+            for (int k = I[L.row_ptr + s]; k < I[L.row_ptr + s + 1]; ++k) {
+                int g = I[L.arc_g + k];
+                if (g < 0) continue;
+                float b = bn[I[L.arc_dst + k]];
+                if (b <= kLogZero) continue;
+                v = logadd_dev(v, b + xg[g] + W[L.arc_w + k]);
+            }
+            bc[s] = v;
+        }
+        float *ps = f.post_sparse + (size_t)t * G;
+        for (int q = tid; q < G; q += NUM_THREADS) {
+            int p = I[L.gpdf + q];
+            float acc = 0.0f;
+            if (p > 0 && p <= P) {
+                const float xv = xg[q];
+                for (int k = I[L.grp_ptr + q]; k < I[L.grp_ptr + q + 1]; ++k) {
+                    float av = ar[I[L.gsrc + k]];
+                    if (av <= kLogZero) continue;
+                    float b = bn[I[L.gdst + k]];
+                    if (b <= kLogZero) continue;
+                    float lp = av + xv + W[L.gw + k] + b - total;
+                    if (lp > 0.0f) lp = 0.0f;  // chain.cu:309-311
+                    acc += expf(lp);
+                }
+            }
+            ps[q] = acc;
+        }
+        if (t > 0) {
+            store_x(W + ((it & 1) ? L.xg0 : L.xg1));
+            store_alpha(W + ((it & 1) ? L.ar0 : L.ar1));
+            if (t > 1) {
+                fetch_x(t - 2);
+                fetch_alpha(t - 2);
+            }
+        }
+        __syncthreads();
+        float *tmp = bn;
+        bn = bc;
+        bc = tmp;
+    }
+}
+
+// ===========================================================================
+// Denominator (prob space, leaky HMM) — SELL-64 arc tables
+// ===========================================================================
+struct SellDev {  // sliced ELL, 64 rows per slice, rows sorted by degree
+    int nsl;
+    const int *perm, *len, *off;
+    const uint2 *arc;  // {f1 | f2 << 16, tp}
+};
+struct DenDev {
+    int S, P;
+    SellDev f;  // rows = destination states: {src, pdf0}
+    SellDev b;  // rows = source states:      {dst, pdf0}
+    SellDev q;  // rows = pdfs:               {src, dst}
+    const float *init;
+};
+
+struct DenRun {
+    const void *nnet;
+    long long ld;
+    const long long *row0;  // [nseq]
+    const int *frames;      // [nseq]
+    int stride, max_frames;
+    float leaky;
+    int backward;           // 0: forward only
+    float *den_out;         // [nseq][2] {total_prob, log-prob} from k_den_fwd
+    unsigned long long *trace;  // optional phase timestamps (kf_chain_trace), null = off
+    float *alpha_store;     // [nseq][(max_frames+1) x S]
+    float *asum_store;      // [nseq][max_frames+1]
+    float *stats;           // [nseq][8]
+    // ABI mode
+    float *post_dense;      // [T x P] (single sequence)
+    // product mode
+    const LogFstDev *nums;  // [nseq] numerator descriptors (total, G, grp_pdf, post_sparse)
+    h16 *out_grad;
+    long long ldg;
+    KfChainOpts opts;
+};
+
+enum { DEN_ABI = 0, DEN_PRODUCT = 1 };
+#define DEN_THREADS 1024
+#define DEN_WAVES 16
+#define DEN_MAXPT 4  // P <= 4096
+#define DEN_MAXS 8  // S <= 8192
+
+// Loads are unconditional (index clamped, value selected afterwards): a
+// "load or constant" select makes hipcc branch and wait vmcnt(0) per element.
+template <typename XT>
+__device__ __forceinline__ void den_fetch_row(float (&r)[DEN_MAXPT], const XT *row, int P) {
+#pragma unroll
+    for (int i = 0; i < DEN_MAXPT; ++i) {
+        int p = threadIdx.x + i * DEN_THREADS;
+        float v = (float)row[min(p, P - 1)];
+        r[i] = (p < P) ? v : 0.0f;
+    }
+}
+// Row prefetch held in registers between frames: fp16 rows stay packed (2 per VGPR).
+template <typename XT> struct RowPre {
+    float v[DEN_MAXPT];
+    __device__ __forceinline__ void fetch(const XT *row, int P) { den_fetch_row(v, row, P); }
+    __device__ __forceinline__ float get(int i) const { return v[i]; }
+};
+template <> struct RowPre<h16> {
+    uint32_t v[DEN_MAXPT / 2];
+    __device__ __forceinline__ void fetch(const h16 *row, int P) {
+        const unsigned short *u = reinterpret_cast<const unsigned short *>(row);
+#pragma unroll
+        for (int i = 0; i < DEN_MAXPT / 2; ++i) {
+            int p0 = threadIdx.x + (2 * i) * DEN_THREADS, p1 = p0 + DEN_THREADS;
+            uint32_t lo = __builtin_nontemporal_load(u + min(p0, P - 1));
+            uint32_t hi = __builtin_nontemporal_load(u + min(p1, P - 1));
+            v[i] = (p0 < P ? lo : 0u) | ((p1 < P ? hi : 0u) << 16);
+        }
+    }
+    __device__ __forceinline__ float get(int i) const {
+        unsigned short b = (unsigned short)((i & 1) ? (v[i >> 1] >> 16) : (v[i >> 1] & 0xFFFF));
+        return (float)__builtin_bit_cast(h16, b);
+    }
+};
+struct StatePre {  // alpha' row prefetch (S <= DEN_MAXS * DEN_THREADS)
+    float v[DEN_MAXS];
+    __device__ __forceinline__ void fetch(const float *row, int S) {
+#pragma unroll
+        for (int i = 0; i < DEN_MAXS; ++i) {
+            int s = threadIdx.x + i * DEN_THREADS;
+            float x = __builtin_nontemporal_load(row + min(s, S - 1));
+            v[i] = s < S ? x : 0.0f;
+        }
+    }
+};
+
+static size_t den_fwd_lds_bytes(int S, int P, int nsl) {
+    return (size_t)4 * (64 + 2 * (size_t)S + P + (size_t)nsl * 66);
+}
+static size_t den_lds_bytes(int S, int P, int nsl, int nslq) {
+    return (size_t)4 * (64 + 2 * (size_t)S + 3 * (size_t)P + (size_t)(nsl + nslq) * 66);
+}
+
+// ---------------------------------------------------------------------------
+// Cross-workgroup exchange (G workgroups per sequence). Hand-off recipe of
+// cdna_hip_programming.md §6 Guideline 16 (R1, counter form, all-sc1): every
+// payload word is stored write-through (sc1) by its wave, every storing wave
+// drains vmcnt, the workgroup barriers, one lane adds to the sequence's counter
+// (agent scope); consumers poll that counter relaxed (bounded, s_sleep), barrier,
+// and read every payload word with sc1 loads. Counters and the timeout word are
+// zeroed by hipMemsetAsync before every launch.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned int gu32_t;
+#define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
+
+__device__ __forceinline__ void st_sc1(float *p, float v) {
+    __hip_atomic_store((gu32_t *)p, __float_as_uint(v), RLX_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __uint_as_float(__hip_atomic_load((gu32_t *)p, RLX_AGENT));
+}
+
+struct DenX {
+    float *buf;     // [nseq][2][G][blk]; blk = spg*64 + 64 (tail: lane 0 = partial sum)
+    unsigned *cnt;  // [nseq] arrivals, then [1] timeout word (zeroed before each launch)
+    int G, lgG, spg, blk, nseq;
+};
+
+// seq / slice-owner of this block; the G blocks of a sequence share an XCD when
+// the grid allows it (blocks b and b+8 share one, MI355X_MICROARCH.md) — speed only
+__device__ __forceinline__ void den_map(const DenX &X, int &seq, int &gi) {
+    const int nb = X.nseq * X.G, b = blockIdx.x;
+    int w = b;
+    if (nb % 8 == 0 && (nb / 8) % X.G == 0) w = (b % 8) * (nb / 8) + b / 8;
+    seq = w >> X.lgG;
+    gi = w & (X.G - 1);
+}
+
+// publish: the payload's sc1 stores are drained by every wave; wave 0 stores the
+// tail {psum} and one lane adds the arrival
+__device__ __forceinline__ void den_publish(const DenX &X, float *tail, const float *red, int seq) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < 64) {
+        float ps = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < DEN_WAVES; ++w2) ps += red[w2];
+        st_sc1(tail + lane, lane == 0 ? ps : 0.0f);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[seq], 1u, RLX_AGENT);
+    }
+}
+// wait for `target` arrivals (one lane polls); false on timeout, uniform
+__device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target, int *lds_flag) {
+    if (threadIdx.x == 0) {
+        unsigned *tmo = X.cnt + X.nseq;
+        int ok = 1;
+        for (unsigned it = 0;; ++it) {
+            if (__hip_atomic_load((gu32_t *)&X.cnt[seq], RLX_AGENT) >= target) break;
+            if ((it & 255) == 255 && __hip_atomic_load((gu32_t *)tmo, RLX_AGENT)) {
+                ok = 0;
+                break;
+            }
+            if (it > (1u << 21)) {  // ~seconds: a partner block is not resident
+                __hip_atomic_store((gu32_t *)tmo, 1u, RLX_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *lds_flag = ok;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return *lds_flag != 0;
+}
+// the G partial sums of buffer `buf` in block order (every lane: same value)
+__device__ __forceinline__ float den_gather_psum(const DenX &X, int seq, int buf) {
+    const int lane = threadIdx.x & 63;
+    float v = 0.0f;
+    if (lane < X.G) v = ld_sc1(X.buf + (((size_t)seq * 2 + buf) * X.G + lane) * X.blk + X.spg * 64);
+    float s = 0.0f;
+    for (int g2 = 0; g2 < X.G; ++g2) s += __shfl(v, g2, 64);
+    return s;
+}
+// all exchanged slices of buffer `buf`, scattered to their states: f(state, value)
+template <class F>
+__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, int nsl, const int *perml,
+                                            F f) {
+    const int tid = threadIdx.x;
+    const float *xb = X.buf + ((size_t)seq * 2 + buf) * X.G * X.blk;
+    float v[DEN_MAXS];
+#pragma unroll
+    for (int m = 0; m < DEN_MAXS; ++m) {  // all loads in flight at once, unconditionally
+        const int c = min(tid + m * DEN_THREADS, nsl * 64 - 1), j = c >> 6;
+        v[m] = ld_sc1(xb + (size_t)(j & (X.G - 1)) * X.blk + (j >> X.lgG) * 64 + (c & 63));
+    }
+#pragma unroll
+    for (int m = 0; m < DEN_MAXS; ++m) {
+        const int c = tid + m * DEN_THREADS;
+        if (c < nsl * 64) {
+            const int st = perml[c];
+            if (st >= 0) f(st, v[m], (c >> 6) & (X.G - 1));
+        }
+    }
+}
+
+// gather-sum over one slice of a SELL table (fixed arc order)
+template <class Term>
+__device__ __forceinline__ float sell_slice(const uint2 *arcs, int len, int off, int lane, Term term) {
+    const uint2 *e = arcs + (size_t)off * 64 + lane;
+    float acc = 0.f;
+    int k = 0;
+    for (; k < len; k += 8) {  // 8 records in flight per lane (len is a multiple of 8)
+        uint2 rr[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            acc += term(rr[i].x & 0xFFFF, rr[i].x >> 16, __uint_as_float(rr[i].y));
+    }
+    return acc;
+}
+
+// SELL meta (perm, len, off) staged in LDS: perm [nsl*64] then len [nsl], off [nsl]
+__device__ __forceinline__ void stage_sell(const SellDev &T, int *dst) {
+    for (int i = threadIdx.x; i < T.nsl * 64; i += DEN_THREADS) dst[i] = T.perm[i];
+    for (int i = threadIdx.x; i < T.nsl; i += DEN_THREADS) {
+        dst[T.nsl * 64 + i] = T.len[i];
+        dst[T.nsl * 65 + i] = T.off[i];
+    }
+}
+
+// Forward pass (chain_den.cu:583-620), G blocks per sequence: block gi computes
+// alpha[t+1] for the destination rows of slices gi, gi+G, ... and all blocks
+// rebuild the full alpha'[t+1] in LDS from the exchanged slices. alpha' of every
+// frame goes to HBM for the backward kernel.
+template <typename XT>
+__global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const DenRun r, const DenX X) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int seq, gi;
+    den_map(X, seq, gi);
+    const int G = X.G, nsl = g.f.nsl;
+    float *red = reinterpret_cast<float *>(smem);          // [32]
+    int *flag = reinterpret_cast<int *>(smem) + 32;        // [32]
+    float *va = reinterpret_cast<float *>(smem) + 64;      // [S] alpha'[t]
+    float *initl = va + S;                                 // [S]
+    float *xe = initl + S;                                 // [P] exp(clamp(x))
+    int *meta = reinterpret_cast<int *>(xe + P);           // perm, len, off of g.f
+    const int *perml = meta, *lenl = meta + nsl * 64, *offl = meta + nsl * 65;
+
+    const int T = r.frames[seq];
+    const long long row0 = r.row0[seq];
+    const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
+    float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * S;
+    float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
+    const float leaky = r.leaky;
+
+    stage_sell(g.f, meta);
+    float part = 0.f;
+    for (int s = tid; s < S; s += DEN_THREADS) {
+        float v = g.init[s];
+        initl[s] = v;
+        part += v;
+    }
+    float as = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
+    for (int s = tid; s < S; s += DEN_THREADS) {
+        float v = initl[s] + as * leaky * initl[s];
+        va[s] = v;
+        if (gi == 0) astore[s] = v;
+    }
+    if (gi == 0 && tid == 0) {
+        asum[0] = as;
+        r.stats[(size_t)seq * 8 + 3] = 0.0f;  // accumulated by k_den_bwd
+        r.stats[(size_t)seq * 8 + 6] = 0.0f;
+    }
+    RowPre<XT> pre;
+    if (T > 0) {
+        pre.fetch(nnet + row0 * r.ld, P);
+#pragma unroll
+        for (int i = 0; i < DEN_MAXPT; ++i) {
+            int p = tid + i * DEN_THREADS;
+            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));  // kernel_apply_exp
+        }
+    }
+    __syncthreads();
+    const int nk = (nsl - gi + G - 1) / G;  // slices owned by this block
+    const bool tr = r.trace && seq == 0 && gi == 0 && tid == 0;
+#define DEN_TP(i) \
+    if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
+    for (int t = 0; t < T; ++t) {
+        DEN_TP(0);
+        const int buf = (t + 1) & 1;
+        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        const bool scale = as > 0.0f;
+        const float inv = scale ? 1.0f / as : 1.0f;
+        part = 0.f;
+        for (int k = wave; k < nk; k += DEN_WAVES) {
+            const int j = gi + G * k;
+            const int st = perml[j * 64 + lane];
+            float acc = sell_slice(g.f.arc, lenl[j], offl[j], lane, [&](int src, int pdf, float tp) {
+                return va[src] * tp * xe[pdf];
+            });
+            float v = (st >= 0) ? (scale ? acc * inv : acc) : 0.0f;
+            st_sc1(blk + k * 64 + lane, v);
+            part += v;
+        }
+        DEN_TP(1);
+        part = wave_sum(part);
+        if (lane == 0) red[wave] = part;
+        den_publish(X, blk + X.spg * 64, red, seq);
+        DEN_TP(2);
+        if (t + 1 < T) pre.fetch(nnet + (row0 + (long long)(t + 1) * r.stride) * r.ld, P);
+        DEN_TP(3);
+        if (!den_wait(X, seq, (unsigned)(G * (t + 1)), flag)) return;
+        DEN_TP(4);
+        const float as1 = den_gather_psum(X, seq, buf);
+        DEN_TP(5);
+        float *an = astore + (size_t)(t + 1) * S;
+        den_consume(X, seq, buf, nsl, perml, [&](int st, float v, int owner) {
+            float a = v + as1 * leaky * initl[st];
+            va[st] = a;
+            if (owner == gi) __builtin_nontemporal_store(a, an + st);  // keep L2 for the arcs
+        });
+        DEN_TP(6);
+        if (t + 1 < T) {
+#pragma unroll
+            for (int i = 0; i < DEN_MAXPT; ++i) {
+                int p = tid + i * DEN_THREADS;
+                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+            }
+        }
+        if (gi == 0 && tid == 0) asum[t + 1] = as1;
+        as = as1;
+        __syncthreads();
+        DEN_TP(7);
+    }
+#undef DEN_TP
+    if (gi != 0) return;
+    // total_prob = sum(alpha'[T]); log_correction = sum_{t<T} log(alpha_sum[t])
+    part = 0.f;
+    for (int s = tid; s < S; s += DEN_THREADS) part += va[s];
+    const float total = block_sum<DEN_WAVES>(part, red);
+    double lc = 0.0;
+    for (int t = tid; t < T; t += DEN_THREADS) {
+        float a = asum[t];
+        if (a > 0.0f) lc += log((double)a);
+    }
+    double *redd = reinterpret_cast<double *>(smem) + 8;  // red[16..31]
+    __syncthreads();
+    lc = block_sum_d<DEN_WAVES>(lc, redd);
+    if (tid == 0) {
+        r.den_out[seq * 2 + 0] = total;
+        r.den_out[seq * 2 + 1] = (float)(log((double)total) + lc);
+        r.stats[(size_t)seq * 8 + 1] = r.den_out[seq * 2 + 1];
+    }
+}
+
+// Backward pass + posteriors (chain_den.cu:632-684), G blocks per sequence. Per
+// frame: beta'[t] over the source rows of this block's slices (exchanged), gamma[t]
+// over this block's pdf rows (summed per pdf in arc order, no atomics), and in the
+// product mode the objective assembly of backward.go:224-371 for those pdfs into
+// the fp16 gradient row. The whole pass always runs; a non-finite objective only
+// zeroes what is written.
+template <typename XT, int MODE>
+__global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const DenRun r, const DenX X) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int seq, gi;
+    den_map(X, seq, gi);
+    const int G = X.G, nsl = g.b.nsl, nslq = g.q.nsl;
+    float *red = reinterpret_cast<float *>(smem);      // [32]
+    int *flag = reinterpret_cast<int *>(smem) + 32;    // [32]
+    float *va = reinterpret_cast<float *>(smem) + 64;  // [S] alpha'[t]
+    float *vb = va + S;                                // [S] beta[t+1]
+    float *xe = vb + S;                                // [P] exp(clamp(x))
+    float *xr = xe + P;                                // [P] raw x
+    float *numrow = xr + P;                            // [P]
+    int *metab = reinterpret_cast<int *>(numrow + P);  // perm, len, off of g.b
+    int *metaq = metab + nsl * 66;                     // ... of g.q
+    const int *permb = metab, *lenb = metab + nsl * 64, *offb = metab + nsl * 65;
+    const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
+
+    const int T = r.frames[seq];
+    const long long row0 = r.row0[seq];
+    const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
+    const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * S;
+    const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
+    const float leaky = r.leaky;
+    const float total = r.den_out[seq * 2 + 0];
+    const float den_lp = r.den_out[seq * 2 + 1];
+
+    float *st8 = r.stats + (size_t)seq * 8;
+    int ok = 1;
+    float w = 1.0f;
+    const LogFstDev *nf = nullptr;
+    int NG = 0;
+    if (MODE == DEN_PRODUCT) {
+        nf = &r.nums[seq];
+        NG = nf->G;
+        w = r.opts.supervision_weight;
+        const float num_lp = *nf->total;
+        double objf = (double)w * ((double)num_lp - (double)den_lp);
+        ok = !(isnan(objf) || isinf(objf));
+        if (gi == 0 && tid == 0) {
+            st8[0] = num_lp;
+            st8[1] = den_lp;
+            st8[2] = ok ? (float)objf : (float)(-10.0 * w * T);  // backward.go:356-363
+            st8[4] = w * (float)T;
+            st8[5] = (float)T;
+            st8[7] = ok ? 1.0f : 0.0f;
+        }
+    }
+    stage_sell(g.b, metab);
+    stage_sell(g.q, metaq);
+    const float inv_tot = total > 0.0f ? 1.0f / total : 0.0f;
+    float part = 0.f;
+    for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s] * inv_tot;
+    float tb = leaky * block_sum<DEN_WAVES>(part, red);
+    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = inv_tot + tb;
+    for (int p = tid; p < P; p += DEN_THREADS) numrow[p] = 0.0f;
+
+    const float l2s = r.opts.supervision_weight * r.opts.l2_regularize;
+    const float oscale = 2.0f * r.opts.out_of_range_regularize;
+    const bool do_oor = MODE == DEN_PRODUCT && r.opts.out_of_range_regularize > 0.0f;
+    const bool do_l2 = MODE == DEN_PRODUCT && r.opts.l2_regularize > 0.0f;
+    float oor = 0.f, sq = 0.f;
+    RowPre<XT> pre;
+    StatePre apre;
+    auto fetch = [&](int t) {
+        pre.fetch(nnet + (row0 + (long long)t * r.stride) * r.ld, P);
+        apre.fetch(astore + (size_t)t * S, S);
+    };
+    auto put = [&](int t) {  // same thread <-> element map as the reads in the gradient loop
+#pragma unroll
+        for (int i = 0; i < DEN_MAXPT; ++i) {
+            int p = tid + i * DEN_THREADS;
+            if (p < P) {
+                const float x = pre.get(i);
+                xr[p] = x;
+                xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, x)));
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < DEN_MAXS; ++i) {
+            int s = tid + i * DEN_THREADS;
+            if (s < S) va[s] = apre.v[i];
+        }
+        if (MODE == DEN_PRODUCT) {  // the numerator's pdf set is the same every frame
+            const float *nps = nf->post_sparse + (size_t)t * NG;
+            for (int q = tid; q < NG; q += DEN_THREADS) {
+                int p = nf->grp_pdf[q];
+                if (p > 0 && p <= P) numrow[p - 1] = nps[q];
+            }
+        }
+    };
+    __syncthreads();  // numrow zeroed before the first scatter
+    if (T > 0) {
+        fetch(T - 1);
+        put(T - 1);
+    }
+    __syncthreads();
+    const int nk = (nsl - gi + G - 1) / G, nkq = (nslq - gi + G - 1) / G;
+    for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
+        const int buf = t & 1;
+        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        const float at = asum[t];
+        const bool scale = at > 0.0f;
+        const float inv = scale ? 1.0f / at : 1.0f;
+        part = 0.f;
+        // beta'[t] by source state (kernel_den_backward_transitions)
+        for (int k = wave; k < nk; k += DEN_WAVES) {
+            const int j = gi + G * k;
+            const int st = permb[j * 64 + lane];
+            float acc = sell_slice(g.b.arc, lenb[j], offb[j], lane, [&](int dst, int pdf, float tp) {
+                return vb[dst] * tp * xe[pdf];
+            });
+            float bd = (st >= 0) ? (scale ? acc * inv : acc) : 0.0f;
+            st_sc1(blk + k * 64 + lane, bd);
+            if (st >= 0) part += g.init[st] * bd;
+        }
+        // gamma[t] by pdf (kernel_den_posteriors) and the gradient of those pdfs
+        h16 *orow = (MODE == DEN_PRODUCT) ? r.out_grad + (row0 + (long long)t * r.stride) * r.ldg : nullptr;
+        const bool even = (t & 1) == 0;
+        for (int k = wave; k < nkq; k += DEN_WAVES) {
+            const int j = gi + G * k;
+            const int pdf = permq[j * 64 + lane];
+            float acc = sell_slice(g.q.arc, lenq[j], offq[j], lane, [&](int src, int dst, float tp) {
+                return va[src] * tp * vb[dst];
+            });
+            if (pdf < 0) continue;
+            float gv = acc * xe[pdf];
+            const float den = scale ? gv * inv : gv;
+            if (MODE == DEN_ABI) {
+                r.post_dense[(size_t)t * P + pdf] = den;
+            } else {
+                const float x = xr[pdf];
+                float d = 0.0f;
+                if (do_oor && even) {  // chain_backward.cu:27-67
+                    if (x < -30.0f) {
+                        d += (-30.0f - x) * oscale;
+                        oor += 1.0f;
+                    } else if (x > 30.0f) {
+                        d += (30.0f - x) * oscale;
+                        oor += 1.0f;
+                    }
+                }
+                d += w * numrow[pdf];
+                d -= w * den;
+                if (do_l2) {
+                    d -= l2s * x;
+                    sq += x * x;
+                }
+                orow[pdf] = ok ? (h16)(-d) : (h16)0.0f;  // loss gradient = -deriv
+            }
+        }
+        part = wave_sum(part);
+        if (lane == 0) red[wave] = part;
+        den_publish(X, blk + X.spg * 64, red, seq);
+        if (t > 0) fetch(t - 1);
+        if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
+        tb = leaky * den_gather_psum(X, seq, buf);
+        den_consume(X, seq, buf, nsl, permb, [&](int st, float v, int) { vb[st] = v + tb; });
+        if (t > 0) put(t - 1);
+        __syncthreads();
+    }
+    if (MODE == DEN_PRODUCT) {
+        float o = block_sum<DEN_WAVES>(oor, red);
+        __syncthreads();
+        float q = block_sum<DEN_WAVES>(sq, red);
+        if (tid == 0) {
+            if (o > 0.0f) atomicAdd(&st8[6], o);
+            if (do_l2 && ok) atomicAdd(&st8[3], -0.5f * l2s * q);
+        }
+    }
+}
+
+// ===========================================================================
+// Host: SELL-64 tables and graph objects
+// ===========================================================================
+namespace {
+
+struct Sell {
+    std::vector<int> perm, len, off;
+    std::vector<uint2> arcs;
+};
+
+// rows = key states; each row lists (other | pdf<<16, tp) in arc order
+// rows = values of key[] in [0, nrows); each row lists {f1 | f2<<16, tp} in arc order
+Sell build_sell(int nrows, int A, const int32_t *key, const int32_t *f1, const int32_t *f2,
+                const float *tp) {
+    Sell s;
+    std::vector<int> deg(nrows, 0);
+    for (int a = 0; a < A; ++a) deg[key[a]]++;
+    std::vector<int> order(nrows);
+    for (int i = 0; i < nrows; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return deg[a] > deg[b]; });
+    const int nsl = (nrows + 63) / 64;
+    s.perm.assign((size_t)nsl * 64, -1);
+    s.len.resize(nsl);
+    s.off.resize(nsl);
+    std::vector<int> rowpos(nrows);
+    int tot = 0;
+    for (int j = 0; j < nsl; ++j) {
+        int mx = 0;
+        for (int l = 0; l < 64; ++l) {
+            int r = j * 64 + l;
+            if (r < nrows) {
+                s.perm[r] = order[r];
+                rowpos[order[r]] = r;
+                mx = std::max(mx, deg[order[r]]);
+            }
+        }
+        mx = (mx + 7) & ~7;  // whole 8-record steps; the padding records have tp = 0
+        s.len[j] = mx;
+        s.off[j] = tot;
+        tot += mx;
+    }
+    s.arcs.assign((size_t)tot * 64, make_uint2(0u, 0u));  // tp = 0 padding
+    std::vector<int> fill(nrows, 0);
+    for (int a = 0; a < A; ++a) {
+        int r = rowpos[key[a]];
+        int j = r / 64, l = r % 64;
+        int k = fill[key[a]]++;
+        uint32_t tpu;
+        memcpy(&tpu, &tp[a], 4);
+        s.arcs[((size_t)s.off[j] + k) * 64 + l] =
+            make_uint2((uint32_t)f1[a] | ((uint32_t)f2[a] << 16), tpu);
+    }
+    return s;
+}
+
+template <typename T>
+T *dev_upload(const std::vector<T> &v, std::vector<void *> &owned) {
+    void *p = nullptr;
+    size_t bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    owned.push_back(p);
+    if (!v.empty()) hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    return (T *)p;
+}
+
+struct DenTables {
+    DenDev dev{};
+    std::vector<void *> owned;
+    ~DenTables() {
+        for (void *p : owned) hipFree(p);
+    }
+};
+
+DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_t *dst,
+                           const int32_t *pdf0, const float *tp, const char **why) {
+    if (S <= 0 || P <= 0 || A <= 0) {
+        *why = "empty denominator graph";
+        return nullptr;
+    }
+    if (S > 65535 || P > 65535) {
+        *why = "den graph needs num_states, num_pdfs <= 65535 (16-bit arc fields)";
+        return nullptr;
+    }
+    if (P > DEN_MAXPT * DEN_THREADS) {
+        *why = "num_pdfs > 4096 not supported";
+        return nullptr;
+    }
+    if (den_lds_bytes(S, P, (S + 63) / 64, (P + 63) / 64) > 160 * 1024 ||
+        den_fwd_lds_bytes(S, P, (S + 63) / 64) > 160 * 1024 || S > DEN_MAXS * DEN_THREADS) {
+        *why = "den graph too large for the LDS-resident kernels (S <= 8192, ~12*S + 14*P B)";
+        return nullptr;
+    }
+    for (int a = 0; a < A; ++a)
+        if (src[a] < 0 || src[a] >= S || dst[a] < 0 || dst[a] >= S || pdf0[a] < 0 ||
+            pdf0[a] >= P || !(tp[a] >= 0.0f)) {
+            *why = "den transition out of range (state, pdf or negative probability)";
+            return nullptr;
+        }
+    Sell sf = build_sell(S, A, dst, src, pdf0, tp);
+    Sell sb = build_sell(S, A, src, dst, pdf0, tp);
+    Sell sq = build_sell(P, A, pdf0, src, dst, tp);
+    auto *t = new DenTables();
+    DenDev &d = t->dev;
+    d.S = S;
+    d.P = P;
+    bool ok = true;
+    auto put = [&](SellDev &o, const Sell &h) {
+        o.nsl = (int)h.len.size();
+        o.perm = dev_upload(h.perm, t->owned);
+        o.len = dev_upload(h.len, t->owned);
+        o.off = dev_upload(h.off, t->owned);
+        o.arc = dev_upload(h.arcs, t->owned);
+        ok = ok && o.perm && o.len && o.off && o.arc;
+    };
+    put(d.f, sf);
+    put(d.b, sb);
+    put(d.q, sq);
+    if (!ok) {
+        delete t;
+        *why = "hipMalloc failed for den tables";
+        return nullptr;
+    }
+    return t;
+}
+
+// denominator.go:131-171
+void compute_initial_probs(int S, int A, const int32_t *src, const int32_t *dst, const float *tp,
+                   int start, float *out) {
+    std::vector<double> cur(S, 0.0), next(S, 0.0), avg(S, 0.0);
+    cur[start] = 1.0;
+    for (int it = 0; it < 100; ++it) {
+        for (int s = 0; s < S; ++s) avg[s] += cur[s] / 100.0;
+        std::fill(next.begin(), next.end(), 0.0);
+        for (int a = 0; a < A; ++a) next[dst[a]] += cur[src[a]] * (double)tp[a];
+        double tot = 0.0;
+        for (int s = 0; s < S; ++s) tot += next[s];
+        if (tot > 0) {
+            double inv = 1.0 / tot;
+            for (int s = 0; s < S; ++s) next[s] *= inv;
+        }
+        cur.swap(next);
+    }
+    for (int s = 0; s < S; ++s) out[s] = (float)avg[s];
+}
+
+// G blocks per sequence: as many as the CUs allow (every block must be resident:
+// the exchange polls are bounded, so a shortfall ends in the timeout word, not a hang)
+int den_pick_G(int nseq) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 1;
+    }
+    if (const char *e = getenv("KF_DEN_G")) {
+        int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4 || v == 8) return (nseq * v <= cus) ? v : 1;
+    }
+    for (int G = 4; G > 1; G /= 2)
+        if (nseq * G <= cus) return G;
+    return 1;
+}
+
+// exchange buffers + counters for up to nseq sequences at G blocks each
+struct DenXBuf {
+    float *buf = nullptr;
+    unsigned *cnt = nullptr;
+    size_t buf_cap = 0, cnt_cap = 0;
+    ~DenXBuf() {
+        if (buf) hipFree(buf);
+        if (cnt) hipFree(cnt);
+    }
+    bool make(const DenDev &g, int nseq, int G, DenX &X) {
+        X.G = G;
+        X.nseq = nseq;
+        X.lgG = G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
+        X.spg = (g.f.nsl + G - 1) / G;
+        X.blk = X.spg * 64 + 64;
+        size_t nb = (size_t)nseq * 2 * G * X.blk * 4;
+        size_t nc = (((size_t)nseq + 1) * 4 + 15) / 16 * 16;
+        if (nb > buf_cap) {
+            if (buf) hipFree(buf);
+            buf = nullptr;
+            buf_cap = 0;
+            if (hipMalloc(&buf, nb) != hipSuccess) return false;
+            buf_cap = nb;
+        }
+        if (nc > cnt_cap) {
+            if (cnt) hipFree(cnt);
+            cnt = nullptr;
+            cnt_cap = 0;
+            if (hipMalloc(&cnt, nc) != hipSuccess) return false;
+            cnt_cap = nc;
+        }
+        X.buf = buf;
+        X.cnt = cnt;
+        return true;
+    }
+    void zero(hipStream_t st) { hipMemsetAsync(cnt, 0, cnt_cap, st); }
+    bool timed_out(hipStream_t st, int nseq) {
+        unsigned v = 0;
+        hipMemcpyAsync(&v, cnt + nseq, 4, hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+        return v != 0;
+    }
+};
+
+void launch_den_fwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb, bool fp32_in) {
+    size_t lds = den_fwd_lds_bytes(g.S, g.P, g.f.nsl);
+    hipStream_t st = kf_stream();
+    xb.zero(st);
+    dim3 grid(X.nseq * X.G);
+    if (fp32_in)
+        hipLaunchKernelGGL((k_den_fwd<float>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+    else
+        hipLaunchKernelGGL((k_den_fwd<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+}
+void launch_den_bwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb, bool fp32_in,
+                    int mode) {
+    size_t lds = den_lds_bytes(g.S, g.P, g.b.nsl, g.q.nsl);
+    hipStream_t st = kf_stream();
+    xb.zero(st);
+    dim3 grid(X.nseq * X.G);
+    if (mode == DEN_PRODUCT)
+        hipLaunchKernelGGL((k_den_bwd<h16, DEN_PRODUCT>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+    else if (fp32_in)
+        hipLaunchKernelGGL((k_den_bwd<float, DEN_ABI>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+    else
+        hipLaunchKernelGGL((k_den_bwd<h16, DEN_ABI>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+}
+
+// ---- numerator FST host preparation (reverse CSR + pdf groups) -------------
+struct NumHost {  // one FST, local indices
+    int S, A, nfinal, start;
+    std::vector<int> row_ptr, in_ptr, in_arc, arc_src, arc_dst, arc_pdf, grp_ptr, grp_pdf, grp_arc,
+        fin_state, in_src, in_g, arc_g, gsrc, gdst;
+    std::vector<float> arc_w, fin_w, in_w, gw;
+};
+
+bool prepare_num(NumHost &h, const char **why) {
+    const int S = h.S, A = h.A;
+    if (S <= 0) {
+        *why = "FST has no states";
+        return false;
+    }
+    if ((int)h.row_ptr.size() != S + 1 || h.row_ptr[0] != 0 || h.row_ptr[S] != A) {
+        *why = "row_ptr does not describe num_arcs arcs";
+        return false;
+    }
+    h.arc_src.assign(A, 0);
+    for (int s = 0; s < S; ++s) {
+        if (h.row_ptr[s + 1] < h.row_ptr[s]) {
+            *why = "row_ptr not monotone";
+            return false;
+        }
+        for (int a = h.row_ptr[s]; a < h.row_ptr[s + 1]; ++a) h.arc_src[a] = s;
+    }
+    for (int a = 0; a < A; ++a)
+        if (h.arc_dst[a] < 0 || h.arc_dst[a] >= S) {
+            *why = "arc destination out of range";
+            return false;
+        }
+    for (int i = 0; i < h.nfinal; ++i)
+        if (h.fin_state[i] < 0 || h.fin_state[i] >= S) {
+            *why = "final state out of range";
+            return false;
+        }
+    if (h.start < 0 || h.start >= S) {
+        *why = "start state out of range";
+        return false;
+    }
+    // reverse CSR, incoming arcs in arc-index order (chain_det.cu:243-290)
+    h.in_ptr.assign(S + 1, 0);
+    for (int a = 0; a < A; ++a) h.in_ptr[h.arc_dst[a] + 1]++;
+    for (int s = 0; s < S; ++s) h.in_ptr[s + 1] += h.in_ptr[s];
+    h.in_arc.assign(A, 0);
+    std::vector<int> pos(h.in_ptr.begin(), h.in_ptr.end() - 1);
+    for (int a = 0; a < A; ++a) h.in_arc[pos[h.arc_dst[a]]++] = a;
+    // pdf groups, arcs in arc-index order inside each group
+    std::vector<int> idx;
+    for (int a = 0; a < A; ++a)
+        if (h.arc_pdf[a] > 0) idx.push_back(a);
+    std::stable_sort(idx.begin(), idx.end(),
+                     [&](int x, int y) { return h.arc_pdf[x] < h.arc_pdf[y]; });
+    h.grp_ptr.assign(1, 0);
+    h.grp_pdf.clear();
+    h.grp_arc = idx;
+    for (size_t i = 0; i < idx.size(); ++i) {
+        if (i == 0 || h.arc_pdf[idx[i]] != h.arc_pdf[idx[i - 1]]) {
+            if (i) h.grp_ptr.push_back((int)i);
+            h.grp_pdf.push_back(h.arc_pdf[idx[i]]);
+        }
+    }
+    if (!idx.empty()) h.grp_ptr.push_back((int)idx.size());
+    // pre-gathered arc fields for k_num_fb
+    h.arc_g.assign(A, -1);
+    for (size_t q = 0; q + 1 < h.grp_ptr.size(); ++q)
+        for (int k = h.grp_ptr[q]; k < h.grp_ptr[q + 1]; ++k) h.arc_g[h.grp_arc[k]] = (int)q;
+    h.in_src.resize(A);
+    h.in_g.resize(A);
+    h.in_w.resize(A);
+    for (int k = 0; k < A; ++k) {
+        int a = h.in_arc[k];
+        h.in_src[k] = h.arc_src[a];
+        h.in_g[k] = h.arc_g[a];
+        h.in_w[k] = h.arc_w[a];
+    }
+    h.gsrc.resize(idx.size());
+    h.gdst.resize(idx.size());
+    h.gw.resize(idx.size());
+    for (size_t k = 0; k < idx.size(); ++k) {
+        h.gsrc[k] = h.arc_src[idx[k]];
+        h.gdst[k] = h.arc_dst[idx[k]];
+        h.gw[k] = h.arc_w[idx[k]];
+    }
+    return true;
+}
+
+// Packs many NumHost into one device blob; fills LogFstDev pointer fields.
+struct NumDevice {
+    std::vector<LogFstDev> desc;  // per FST, pointers set, run fields unset
+    std::vector<int> G, Ag;
+    std::vector<void *> owned;
+    ~NumDevice() {
+        for (void *p : owned) hipFree(p);
+    }
+};
+
+template <typename T>
+void append(std::vector<int32_t> &blob, const std::vector<T> &v, std::vector<size_t> &offs) {
+    offs.push_back(blob.size());
+    size_t n = blob.size();
+    blob.resize(n + v.size());
+    if (!v.empty()) memcpy(blob.data() + n, v.data(), v.size() * 4);
+}
+
+NumDevice *upload_nums(std::vector<NumHost> &hs, const char **why) {
+    std::vector<int32_t> blob;
+    std::vector<std::vector<size_t>> offs(hs.size());
+    for (size_t i = 0; i < hs.size(); ++i) {
+        NumHost &h = hs[i];
+        auto &o = offs[i];
+        append(blob, h.row_ptr, o);
+        append(blob, h.in_ptr, o);
+        append(blob, h.in_arc, o);
+        append(blob, h.arc_src, o);
+        append(blob, h.arc_dst, o);
+        append(blob, h.arc_pdf, o);
+        append(blob, h.arc_w, o);
+        append(blob, h.grp_ptr, o);
+        append(blob, h.grp_pdf, o);
+        append(blob, h.grp_arc, o);
+        append(blob, h.fin_state, o);
+        append(blob, h.fin_w, o);
+        append(blob, h.in_src, o);
+        append(blob, h.in_g, o);
+        append(blob, h.arc_g, o);
+        append(blob, h.gsrc, o);
+        append(blob, h.gdst, o);
+        append(blob, h.in_w, o);
+        append(blob, h.gw, o);
+    }
+    auto *nd = new NumDevice();
+    int32_t *d = dev_upload(blob, nd->owned);
+    if (!d) {
+        delete nd;
+        *why = "hipMalloc failed for numerator FSTs";
+        return nullptr;
+    }
+    for (size_t i = 0; i < hs.size(); ++i) {
+        const auto &o = offs[i];
+        LogFstDev f{};
+        f.row_ptr = d + o[0];
+        f.in_ptr = d + o[1];
+        f.in_arc = d + o[2];
+        f.arc_src = d + o[3];
+        f.arc_dst = d + o[4];
+        f.arc_pdf = d + o[5];
+        f.arc_w = reinterpret_cast<const float *>(d + o[6]);
+        f.grp_ptr = d + o[7];
+        f.grp_pdf = d + o[8];
+        f.grp_arc = d + o[9];
+        f.fin_state = d + o[10];
+        f.fin_w = reinterpret_cast<const float *>(d + o[11]);
+        f.in_src = d + o[12];
+        f.in_g = d + o[13];
+        f.arc_g = d + o[14];
+        f.gsrc = d + o[15];
+        f.gdst = d + o[16];
+        f.in_w = reinterpret_cast<const float *>(d + o[17]);
+        f.gw = reinterpret_cast<const float *>(d + o[18]);
+        f.S = hs[i].S;
+        f.A = hs[i].A;
+        f.G = (int)hs[i].grp_pdf.size();
+        f.nfinal = hs[i].nfinal;
+        f.start = hs[i].start;
+        nd->desc.push_back(f);
+        nd->G.push_back(f.G);
+        nd->Ag.push_back((int)hs[i].grp_arc.size());
+    }
+    return nd;
+}
+
+// ABI helper: device ChainFstGPU -> host NumHost
+bool fetch_fst(const ChainFstGPU *fst, NumHost &h, const char **why) {
+    if (!fst || fst->num_states <= 0 || fst->num_arcs < 0 || fst->num_final < 0) {
+        *why = "invalid ChainFstGPU";
+        return false;
+    }
+    h.S = fst->num_states;
+    h.A = fst->num_arcs;
+    h.nfinal = fst->num_final;
+    h.start = fst->start_state;
+    h.row_ptr.resize(h.S + 1);
+    h.arc_dst.resize(h.A);
+    h.arc_pdf.resize(h.A);
+    h.arc_w.resize(h.A);
+    h.fin_state.resize(h.nfinal);
+    h.fin_w.resize(h.nfinal);
+    hipStreamSynchronize(kf_stream());
+    bool ok = hipMemcpy(h.row_ptr.data(), fst->row_ptr, (h.S + 1) * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    if (h.A) {
+        ok = ok && hipMemcpy(h.arc_dst.data(), fst->col_idx, h.A * 4, hipMemcpyDeviceToHost) == hipSuccess;
+        ok = ok && hipMemcpy(h.arc_pdf.data(), fst->labels, h.A * 4, hipMemcpyDeviceToHost) == hipSuccess;
+        ok = ok && hipMemcpy(h.arc_w.data(), fst->weights, h.A * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    if (h.nfinal) {
+        ok = ok && hipMemcpy(h.fin_state.data(), fst->final_states, h.nfinal * 4, hipMemcpyDeviceToHost) == hipSuccess;
+        ok = ok && hipMemcpy(h.fin_w.data(), fst->final_weights, h.nfinal * 4, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    if (!ok) {
+        *why = "device->host copy of the FST failed";
+        return false;
+    }
+    return prepare_num(h, why);
+}
+
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() {
+        if (p) hipFree(p);
+    }
+    bool alloc(size_t n) {
+        return hipMalloc(&p, std::max<size_t>(n, 16)) == hipSuccess;
+    }
+};
+
+// Runs k_logfb over `fsts` (already filled) and returns the totals.
+bool run_logfb(std::vector<LogFstDev> &fsts, const void *nnet16, long long ld, int P,
+               std::vector<float> &totals, const char **why) {
+    DevBuf d, tot;
+    size_t n = fsts.size();
+    if (!tot.alloc(n * sizeof(float)) || !d.alloc(n * sizeof(LogFstDev))) {
+        *why = "hipMalloc failed";
+        return false;
+    }
+    hipStream_t st = kf_stream();
+    for (size_t i = 0; i < n; ++i)
+        if (!(fsts[i].mode & LF_FB)) {
+            hipMemcpyAsync((float *)tot.p + i, &totals[i], 4, hipMemcpyHostToDevice, st);
+        }
+    for (size_t i = 0; i < n; ++i) fsts[i].total = (float *)tot.p + i;
+    hipMemcpyAsync(d.p, fsts.data(), n * sizeof(LogFstDev), hipMemcpyHostToDevice, st);
+    hipLaunchKernelGGL(k_logfb, dim3(n), dim3(256), 0, st, (const LogFstDev *)d.p,
+                       (const h16 *)nnet16, ld, P);
+    totals.resize(n);
+    hipMemcpyAsync(totals.data(), tot.p, n * 4, hipMemcpyDeviceToHost, st);
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess || hipGetLastError() != hipSuccess) {
+        *why = hipGetErrorString(e);
+        return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+// ===========================================================================
+// chain.h ABI
+// ===========================================================================
+extern "C" size_t chain_workspace_bytes(int T, int num_states) {
+    return 2 * (size_t)(T + 1) * num_states * sizeof(float);
+}
+
+static int fb_common(const void *nnet, const ChainFstGPU *fst, int T, int P, float *alpha,
+                     float *beta, float *total, int mode, const float *post_in_total,
+                     float *post) {
+    const char *why = nullptr;
+    if (!nnet || !alpha || !beta || T < 0 || P <= 0) {
+        chain_set_error("chain_forward_backward: invalid arguments");
+        return -1;
+    }
+    NumHost h;
+    if (!fetch_fst(fst, h, &why)) {
+        chain_set_error("chain_forward_backward: %s", why);
+        return -1;
+    }
+    std::vector<NumHost> hs{h};
+    NumDevice *nd = upload_nums(hs, &why);
+    if (!nd) {
+        chain_set_error("chain_forward_backward: %s", why);
+        return -1;
+    }
+    std::vector<LogFstDev> fs{nd->desc[0]};
+    LogFstDev &f = fs[0];
+    // the caller's own arrays are authoritative for arcs and finals
+    f.arc_dst = fst->col_idx;
+    f.arc_pdf = fst->labels;
+    f.arc_w = fst->weights;
+    f.fin_state = fst->final_states;
+    f.fin_w = fst->final_weights;
+    f.T = T;
+    f.mode = mode;
+    f.stride = 1;
+    f.row0 = 0;
+    f.alpha = alpha;
+    f.beta = beta;
+    f.post_dense = post;
+    std::vector<float> tot{post_in_total ? *post_in_total : 0.0f};
+    bool ok = run_logfb(fs, nnet, P, P, tot, &why);
+    delete nd;
+    if (!ok) {
+        chain_set_error("chain_forward_backward: %s", why);
+        return -1;
+    }
+    if (total) *total = tot[0];
+    return 0;
+}
+
+extern "C" int chain_forward_backward(const void *nnet_output, const ChainFstGPU *fst, int T,
+                                      int num_pdfs, float *alpha, float *beta,
+                                      float *total_logprob) {
+    return fb_common(nnet_output, fst, T, num_pdfs, alpha, beta, total_logprob, LF_FB, nullptr,
+                     nullptr);
+}
+extern "C" int chain_forward_backward_det(const void *nnet_output, const ChainFstGPU *fst, int T,
+                                          int num_pdfs, float *alpha, float *beta,
+                                          float *total_logprob) {
+    return chain_forward_backward(nnet_output, fst, T, num_pdfs, alpha, beta, total_logprob);
+}
+extern "C" int chain_compute_posteriors(const void *nnet_output, const ChainFstGPU *fst, int T,
+                                        int num_pdfs, const float *alpha, const float *beta,
+                                        float total_logprob, float *posteriors) {
+    if (!posteriors) {
+        chain_set_error("chain_compute_posteriors: posteriors is NULL");
+        return -1;
+    }
+    return fb_common(nnet_output, fst, T, num_pdfs, const_cast<float *>(alpha),
+                     const_cast<float *>(beta), nullptr, LF_POST, &total_logprob, posteriors);
+}
+extern "C" int chain_compute_posteriors_det(const void *nnet_output, const ChainFstGPU *fst,
+                                            int T, int num_pdfs, const float *alpha,
+                                            const float *beta, float total_logprob,
+                                            float *posteriors) {
+    return chain_compute_posteriors(nnet_output, fst, T, num_pdfs, alpha, beta, total_logprob,
+                                    posteriors);
+}
+
+__global__ void k_chain_gradient(h16 *g, const float *num, const float *den, long long n, float w) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = (den[i] - num[i]) * w;  // chain.cu:330-352
+    g[i] = (h16)fmaxf(-30.0f, fminf(30.0f, v));
+}
+
+extern "C" int chain_compute_loss(const void *nnet_output, const ChainFstGPU *num_fst,
+                                  const ChainFstGPU *den_fst, int T, int num_pdfs,
+                                  void *grad_output, ChainLossResult *result) {
+    const char *why = nullptr;
+    if (!nnet_output || !result || T < 0 || num_pdfs <= 0) {
+        chain_set_error("chain_compute_loss: invalid arguments");
+        return -1;
+    }
+    std::vector<NumHost> hs(2);
+    if (!fetch_fst(num_fst, hs[0], &why) || !fetch_fst(den_fst, hs[1], &why)) {
+        chain_set_error("chain_compute_loss: %s", why);
+        return -1;
+    }
+    NumDevice *nd = upload_nums(hs, &why);
+    if (!nd) {
+        chain_set_error("chain_compute_loss: %s", why);
+        return -1;
+    }
+    const size_t TP = (size_t)T * num_pdfs;
+    DevBuf ws, post;
+    size_t wsn = 2 * (size_t)(T + 1) * (hs[0].S + hs[1].S);
+    if (!ws.alloc(wsn * 4) || !post.alloc(2 * TP * 4)) {
+        delete nd;
+        chain_set_error("chain_compute_loss: hipMalloc failed");
+        return -1;
+    }
+    std::vector<LogFstDev> fs = nd->desc;
+    float *w = (float *)ws.p;
+    for (int i = 0; i < 2; ++i) {
+        fs[i].T = T;
+        fs[i].mode = LF_FB | (grad_output ? LF_POST : 0);
+        fs[i].stride = 1;
+        fs[i].row0 = 0;
+        fs[i].alpha = w;
+        w += (size_t)(T + 1) * hs[i].S;
+        fs[i].beta = w;
+        w += (size_t)(T + 1) * hs[i].S;
+        fs[i].post_dense = grad_output ? (float *)post.p + i * TP : nullptr;
+    }
+    std::vector<float> tot(2, 0.0f);
+    bool ok = run_logfb(fs, nnet_output, num_pdfs, num_pdfs, tot, &why);
+    delete nd;
+    if (!ok) {
+        chain_set_error("chain_compute_loss: %s", why);
+        return -1;
+    }
+    result->num_logprob = tot[0];
+    result->den_logprob = tot[1];
+    result->loss = -(tot[0] - tot[1]);
+    if (grad_output && TP) {
+        hipLaunchKernelGGL(k_chain_gradient, dim3(kf_blocks(TP, 256)), dim3(256), 0, kf_stream(),
+                           (h16 *)grad_output, (const float *)post.p, (const float *)post.p + TP,
+                           (long long)TP, 1.0f);
+        if (hipStreamSynchronize(kf_stream()) != hipSuccess) {
+            chain_set_error("chain_compute_loss: gradient kernel failed");
+            return -1;
+        }
+    }
+    return 0;
+}
+
+__global__ void k_f32_to_f16(const float *in, h16 *out, long long n) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = (h16)in[i];
+}
+
+static float num_fb_fp32(const int *row_ptr, const int *col_idx, const float *weights,
+                         const int *pdf_ids, const int *final_states, const float *final_weights,
+                         int S, int A, int F, const float *nnet, float *num_post, int T, int P,
+                         void *stream) {
+    if (!nnet || !num_post || T < 0 || P <= 0) {
+        chain_set_error("chain_num_forward_backward: invalid arguments");
+        return -1e30f;
+    }
+    hipStream_t saved = kf_stream();
+    if (stream) kf_set_stream(stream);
+    ChainFstGPU fst{(int32_t *)row_ptr, (int32_t *)col_idx, (int32_t *)pdf_ids, (float *)weights,
+                    (int32_t *)final_states, (float *)final_weights, S, A, F, 0};
+    const size_t TP = (size_t)T * P;
+    DevBuf x16, ws;
+    float result = -1e30f;
+    if (x16.alloc(TP * 2) && ws.alloc(chain_workspace_bytes(T, S))) {
+        hipLaunchKernelGGL(k_f32_to_f16, dim3(kf_blocks(TP, 256)), dim3(256), 0, kf_stream(),
+                           nnet, (h16 *)x16.p, (long long)TP);
+        float *a = (float *)ws.p, *b = a + (size_t)(T + 1) * S;
+        float tot = 0.f;
+        if (fb_common(x16.p, &fst, T, P, a, b, &tot, LF_FB | LF_POST, nullptr, num_post) == 0)
+            result = tot;
+    } else {
+        chain_set_error("chain_num_forward_backward: hipMalloc failed");
+    }
+    if (stream) kf_set_stream((void *)saved);
+    return result;
+}
+
+extern "C" float chain_num_forward_backward(const int *fst_row_ptr, const int *fst_col_idx,
+                                            const float *fst_weights, const int *fst_pdf_ids,
+                                            const int *fst_final_states,
+                                            const float *fst_final_weights, int num_states,
+                                            int num_arcs, int num_final, const float *nnet_output,
+                                            float *num_post, int T, int num_pdfs, void *stream) {
+    return num_fb_fp32(fst_row_ptr, fst_col_idx, fst_weights, fst_pdf_ids, fst_final_states,
+                       fst_final_weights, num_states, num_arcs, num_final, nnet_output, num_post,
+                       T, num_pdfs, stream);
+}
+extern "C" float chain_num_forward_backward_det(
+    const int *fst_row_ptr, const int *fst_col_idx, const float *fst_weights,
+    const int *fst_pdf_ids, const int *fst_final_states, const float *fst_final_weights,
+    int num_states, int num_arcs, int num_final, const float *nnet_output, float *num_post, int T,
+    int num_pdfs, void *stream) {
+    return num_fb_fp32(fst_row_ptr, fst_col_idx, fst_weights, fst_pdf_ids, fst_final_states,
+                       fst_final_weights, num_states, num_arcs, num_final, nnet_output, num_post,
+                       T, num_pdfs, stream);
+}
+
+// ===========================================================================
+// chain_backward_api.h ABI (element-wise objective pieces)
+// ===========================================================================
+__global__ void k_combine16(const float *num, const float *den, float w, h16 *g, long long n) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) g[i] = (h16)(w * (num[i] - den[i]));
+}
+__global__ void k_add_post(const float *num, const float *den, float *g, float w, long long n) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) g[i] += w * (num[i] - den[i]);
+}
+__global__ void k_penalize(const float *x, float *g, float limit, float scale, int T, int P,
+                           int *count) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    int c = 0;
+    if (i < (long long)T * P && ((i / P) % 2) == 0) {
+        float v = x[i];
+        if (v < -limit) {
+            g[i] += (-limit - v) * scale;
+            c = 1;
+        } else if (v > limit) {
+            g[i] += (limit - v) * scale;
+            c = 1;
+        }
+    }
+    float cf = wave_sum((float)c);
+    if ((threadIdx.x & 63) == 0 && cf > 0.0f) atomicAdd(count, (int)cf);
+}
+__global__ void k_l2(const float *x, float *g, float s, long long n, double *acc) {
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    double q = 0.0;
+    if (i < n) {
+        float v = x[i];
+        g[i] -= s * v;
+        q = (double)v * v;
+    }
+    q = wave_sum_d(q);
+    if ((threadIdx.x & 63) == 0) atomicAdd(acc, q);
+}
+
+extern "C" int chain_combine_gradient(const float *num_post, const float *den_post, float weight,
+                                      int T, int num_pdfs, void *grad_output) {
+    long long n = (long long)T * num_pdfs;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_combine16, dim3(kf_blocks(n, 256)), dim3(256), 0, kf_stream(), num_post,
+                       den_post, weight, (h16 *)grad_output, n);
+    if (hipGetLastError() != hipSuccess) {
+        chain_set_error("chain_combine_gradient: launch failed");
+        return -1;
+    }
+    return 0;
+}
+extern "C" int chain_add_posterior_gradient(const float *num_post, const float *den_post,
+                                            float *grad, float weight, int total_elements) {
+    if (total_elements <= 0) return 0;
+    hipLaunchKernelGGL(k_add_post, dim3(kf_blocks(total_elements, 256)), dim3(256), 0, kf_stream(),
+                       num_post, den_post, grad, weight, (long long)total_elements);
+    if (hipGetLastError() != hipSuccess) {
+        chain_set_error("chain_add_posterior_gradient: launch failed");
+        return -1;
+    }
+    return 0;
+}
+extern "C" int chain_penalize_out_of_range(const float *nnet_output, float *grad_output,
+                                           float limit, float scale, int T, int num_pdfs) {
+    long long n = (long long)T * num_pdfs;
+    if (n <= 0) return 0;
+    DevBuf cnt;
+    if (!cnt.alloc(4)) return 0;
+    hipStream_t st = kf_stream();
+    hipMemsetAsync(cnt.p, 0, 4, st);
+    hipLaunchKernelGGL(k_penalize, dim3(kf_blocks(n, 256)), dim3(256), 0, st, nnet_output,
+                       grad_output, limit, scale, T, num_pdfs, (int *)cnt.p);
+    int h = 0;
+    hipMemcpyAsync(&h, cnt.p, 4, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    return h;
+}
+extern "C" float chain_l2_regularize(const float *nnet_output, float *grad_output, float l2_scale,
+                                     int total_elements) {
+    if (total_elements <= 0) return 0.0f;
+    DevBuf acc;
+    if (!acc.alloc(8)) return 0.0f;
+    hipStream_t st = kf_stream();
+    hipMemsetAsync(acc.p, 0, 8, st);
+    hipLaunchKernelGGL(k_l2, dim3(kf_blocks(total_elements, 256)), dim3(256), 0, st, nnet_output,
+                       grad_output, l2_scale, (long long)total_elements, (double *)acc.p);
+    double h = 0.0;
+    hipMemcpyAsync(&h, acc.p, 8, hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    return (float)(-0.5 * l2_scale * h);
+}
+extern "C" int chain_grad_fp32_to_fp16(const float *grad_fp32, void *grad_fp16,
+                                       int total_elements) {
+    if (total_elements <= 0) return 0;
+    hipLaunchKernelGGL(k_f32_to_f16, dim3(kf_blocks(total_elements, 256)), dim3(256), 0,
+                       kf_stream(), grad_fp32, (h16 *)grad_fp16, (long long)total_elements);
+    return 0;
+}
+
+// ===========================================================================
+// chain_den.h ABI
+// ===========================================================================
+static std::mutex g_den_mu;
+static std::map<const void *, DenTables *> g_den_tables;  // keyed by DenFstGPU::src_states
+
+extern "C" int den_fst_upload(DenFstGPU *fst, const int32_t *src, const int32_t *dst,
+                              const int32_t *pdf, const float *trans_probs, int num_trans,
+                              int num_states, int num_pdfs) {
+    const char *why = nullptr;
+    if (!fst || !src || !dst || !pdf || !trans_probs) {
+        den_set_error("den_fst_upload: NULL argument");
+        return -1;
+    }
+    DenTables *t = make_den_tables(num_states, num_pdfs, num_trans, src, dst, pdf, trans_probs, &why);
+    if (!t) {
+        den_set_error("den_fst_upload: %s", why);
+        return -1;
+    }
+    std::vector<int32_t> vs(src, src + num_trans), vd(dst, dst + num_trans), vp(pdf, pdf + num_trans);
+    std::vector<float> vt(trans_probs, trans_probs + num_trans);
+    std::vector<void *> owned;
+    fst->src_states = dev_upload(vs, owned);
+    fst->dst_states = dev_upload(vd, owned);
+    fst->pdf_ids = dev_upload(vp, owned);
+    fst->transition_probs = dev_upload(vt, owned);
+    if (!fst->src_states || !fst->dst_states || !fst->pdf_ids || !fst->transition_probs) {
+        for (void *p : owned) hipFree(p);
+        delete t;
+        den_set_error("den_fst_upload: hipMalloc failed");
+        return -1;
+    }
+    fst->num_transitions = num_trans;
+    fst->num_states = num_states;
+    fst->num_pdfs = num_pdfs;
+    std::lock_guard<std::mutex> lk(g_den_mu);
+    g_den_tables[fst->src_states] = t;
+    return 0;
+}
+
+extern "C" void den_fst_free(DenFstGPU *fst) {
+    if (!fst) return;
+    {
+        std::lock_guard<std::mutex> lk(g_den_mu);
+        auto it = g_den_tables.find(fst->src_states);
+        if (it != g_den_tables.end()) {
+            delete it->second;
+            g_den_tables.erase(it);
+        }
+    }
+    hipFree(fst->src_states);
+    hipFree(fst->dst_states);
+    hipFree(fst->pdf_ids);
+    hipFree(fst->transition_probs);
+    fst->src_states = fst->dst_states = fst->pdf_ids = nullptr;
+    fst->transition_probs = nullptr;
+}
+
+static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_init, int T,
+                     float leaky, float *h_post) {
+    DenTables *t = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_den_mu);
+        auto it = fst ? g_den_tables.find(fst->src_states) : g_den_tables.end();
+        if (it != g_den_tables.end()) t = it->second;
+    }
+    if (!t) {
+        den_set_error("den_forward: FST was not uploaded with den_fst_upload");
+        return -1e30f;
+    }
+    if (!h_nnet || !h_init || T < 0) {
+        den_set_error("den_forward: invalid arguments");
+        return -1e30f;
+    }
+    const int S = t->dev.S, P = t->dev.P;
+    const size_t TP = (size_t)T * P;
+    DevBuf x, init, as, ast, stats, post, row0, frames, dout;
+    if (!x.alloc(TP * 4) || !init.alloc(S * 4) || !as.alloc((size_t)(T + 1) * S * 4) ||
+        !ast.alloc((T + 1) * 4) || !stats.alloc(32) || !row0.alloc(8) || !frames.alloc(4) ||
+        !dout.alloc(8) ||
+        (h_post && !post.alloc(TP * 4))) {
+        den_set_error("den_forward: hipMalloc failed");
+        return -1e30f;
+    }
+    hipStream_t st = kf_stream();
+    long long r0 = 0;
+    hipMemcpyAsync(x.p, h_nnet, TP * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(init.p, h_init, S * 4, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(row0.p, &r0, 8, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(frames.p, &T, 4, hipMemcpyHostToDevice, st);
+    DenDev g = t->dev;
+    g.init = (const float *)init.p;
+    DenRun r{};
+    r.nnet = x.p;
+    r.ld = P;
+    r.row0 = (const long long *)row0.p;
+    r.frames = (const int *)frames.p;
+    r.stride = 1;
+    r.max_frames = T;
+    r.leaky = leaky;
+    r.backward = h_post != nullptr;
+    r.alpha_store = (float *)as.p;
+    r.asum_store = (float *)ast.p;
+    r.stats = (float *)stats.p;
+    r.post_dense = (float *)post.p;
+    r.den_out = (float *)dout.p;
+    DenX X{};
+    DenXBuf xbuf;
+    if (!xbuf.make(g, 1, den_pick_G(1), X)) {
+        den_set_error("den_forward: hipMalloc failed");
+        return -1e30f;
+    }
+    launch_den_fwd(g, r, X, xbuf, true);
+    if (h_post) launch_den_bwd(g, r, X, xbuf, true, DEN_ABI);
+    float st8[8] = {0};
+    hipMemcpyAsync(st8, stats.p, 32, hipMemcpyDeviceToHost, st);
+    if (h_post) hipMemcpyAsync(h_post, post.p, TP * 4, hipMemcpyDeviceToHost, st);
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess || hipGetLastError() != hipSuccess) {
+        den_set_error("den_forward_backward: %s", hipGetErrorString(e));
+        return -1e30f;
+    }
+    if (xbuf.timed_out(st, 1)) {
+        den_set_error("den_forward_backward: cross-workgroup exchange timed out");
+        return -1e30f;
+    }
+    return st8[1];
+}
+
+extern "C" float den_forward(const DenFstGPU *fst, const float *nnet_output,
+                             const float *initial_probs, int T, float leaky_hmm_coeff) {
+    return den_abi(fst, nnet_output, initial_probs, T, leaky_hmm_coeff, nullptr);
+}
+extern "C" float den_forward_backward(const DenFstGPU *fst, const float *nnet_output,
+                                      const float *initial_probs, int T, float leaky_hmm_coeff,
+                                      float *grad_output) {
+    if (!grad_output) {
+        den_set_error("den_forward_backward: grad_output is NULL");
+        return -1e30f;
+    }
+    return den_abi(fst, nnet_output, initial_probs, T, leaky_hmm_coeff, grad_output);
+}
+
+// ===========================================================================
+// kf_chain.h — batched product interface
+// ===========================================================================
+struct KfDenGraph {
+    DenTables *t = nullptr;
+    int num_arcs = 0;
+    std::vector<float> init;
+    float *d_init = nullptr;
+    ~KfDenGraph() {
+        delete t;
+        if (d_init) hipFree(d_init);
+    }
+};
+
+struct KfNumBatch {
+    NumDevice *nd = nullptr;
+    std::vector<int> S;
+    ~KfNumBatch() { delete nd; }
+};
+
+struct KfChain {
+    const KfDenGraph *den = nullptr;
+    int max_seqs = 0, max_frames = 0;
+    float *alpha_store = nullptr, *asum_store = nullptr, *stats = nullptr;
+    float *num_ab = nullptr;      // numerator alpha/beta
+    size_t num_ab_cap = 0;
+    float *num_post = nullptr;    // sparse numerator posteriors
+    size_t num_post_cap = 0;
+    LogFstDev *d_desc = nullptr;  // [max_seqs]
+    long long *d_row0 = nullptr;
+    int *d_frames = nullptr;
+    float *d_num_total = nullptr;
+    // cache of the last run's layout (re-uploaded only when it changes)
+    const KfNumBatch *last_num = nullptr;
+    std::vector<int> last_row0, last_frames;
+    int last_stride = -1, last_nseq = 0;
+    const void *last_nnet = nullptr;
+    long long last_ld = -1, last_rows = -1;
+    std::vector<LogFstDev> host_desc;
+    size_t num_lds = 0;           // dynamic LDS of k_num_fb, 0 = use k_logfb
+    float *den_out = nullptr;     // [max_seqs][2]
+    hipStream_t side = nullptr;   // numerator stream (overlaps the den forward)
+    hipEvent_t ev_in = nullptr, ev_num = nullptr;
+    DenXBuf xbuf;
+    unsigned long long *trace = nullptr;  // kf_chain_trace (diagnostics)
+    ~KfChain() {
+        if (side) hipStreamDestroy(side);
+        if (ev_in) hipEventDestroy(ev_in);
+        if (ev_num) hipEventDestroy(ev_num);
+        if (den_out) hipFree(den_out);
+        for (void *p : {(void *)alpha_store, (void *)asum_store, (void *)stats, (void *)num_ab,
+                        (void *)num_post, (void *)d_desc, (void *)d_row0, (void *)d_frames,
+                        (void *)d_num_total})
+            if (p) hipFree(p);
+    }
+};
+
+extern "C" KfDenGraph *kf_den_graph_create(int S, int P, int A, const int32_t *src,
+                                           const int32_t *dst, const int32_t *pdf0,
+                                           const float *tp, int start_state,
+                                           const float *initial_probs) {
+    const char *why = nullptr;
+    if (!src || !dst || !pdf0 || !tp || start_state < 0 || start_state >= S) {
+        kfc_set_error("kf_den_graph_create: invalid arguments");
+        return nullptr;
+    }
+    DenTables *t = make_den_tables(S, P, A, src, dst, pdf0, tp, &why);
+    if (!t) {
+        kfc_set_error("kf_den_graph_create: %s", why);
+        return nullptr;
+    }
+    auto *g = new KfDenGraph();
+    g->t = t;
+    g->num_arcs = A;
+    g->init.resize(S);
+    if (initial_probs)
+        memcpy(g->init.data(), initial_probs, S * 4);
+    else
+        compute_initial_probs(S, A, src, dst, tp, start_state, g->init.data());
+    std::vector<void *> owned;
+    g->d_init = dev_upload(g->init, owned);
+    if (!g->d_init) {
+        delete g;
+        kfc_set_error("kf_den_graph_create: hipMalloc failed");
+        return nullptr;
+    }
+    g->t->dev.init = g->d_init;
+    return g;
+}
+
+extern "C" int kf_den_graph_initial_probs(const KfDenGraph *g, float *out) {
+    if (!g || !out) return -1;
+    memcpy(out, g->init.data(), g->init.size() * 4);
+    return 0;
+}
+extern "C" void kf_den_graph_free(KfDenGraph *g) { delete g; }
+
+extern "C" KfNumBatch *kf_num_batch_create(int nseq, const int32_t *state_off,
+                                           const int32_t *arc_off, const int32_t *row_ptr,
+                                           const int32_t *dst, const int32_t *pdf1,
+                                           const float *logw, const int32_t *final_off,
+                                           const int32_t *final_state, const float *final_logw) {
+    const char *why = nullptr;
+    if (nseq <= 0 || !state_off || !arc_off || !row_ptr || !final_off) {
+        kfc_set_error("kf_num_batch_create: invalid arguments");
+        return nullptr;
+    }
+    std::vector<NumHost> hs(nseq);
+    for (int i = 0; i < nseq; ++i) {
+        NumHost &h = hs[i];
+        h.S = state_off[i + 1] - state_off[i];
+        h.A = arc_off[i + 1] - arc_off[i];
+        h.nfinal = final_off[i + 1] - final_off[i];
+        h.start = 0;
+        if (h.S <= 0 || h.A < 0 || h.nfinal < 0) {
+            kfc_set_error("kf_num_batch_create: sequence %d has an empty FST", i);
+            return nullptr;
+        }
+        const int32_t *rp = row_ptr + state_off[i] + i;
+        h.row_ptr.assign(rp, rp + h.S + 1);
+        h.arc_dst.assign(dst + arc_off[i], dst + arc_off[i + 1]);
+        h.arc_pdf.assign(pdf1 + arc_off[i], pdf1 + arc_off[i + 1]);
+        h.arc_w.assign(logw + arc_off[i], logw + arc_off[i + 1]);
+        h.fin_state.assign(final_state + final_off[i], final_state + final_off[i + 1]);
+        h.fin_w.assign(final_logw + final_off[i], final_logw + final_off[i + 1]);
+        if (!prepare_num(h, &why)) {
+            kfc_set_error("kf_num_batch_create: sequence %d: %s", i, why);
+            return nullptr;
+        }
+    }
+    NumDevice *nd = upload_nums(hs, &why);
+    if (!nd) {
+        kfc_set_error("kf_num_batch_create: %s", why);
+        return nullptr;
+    }
+    auto *b = new KfNumBatch();
+    b->nd = nd;
+    for (auto &h : hs) b->S.push_back(h.S);
+    return b;
+}
+extern "C" void kf_num_batch_free(KfNumBatch *b) { delete b; }
+
+extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max_frames) {
+    if (!den || max_seqs <= 0 || max_frames <= 0) {
+        kfc_set_error("kf_chain_create: invalid arguments");
+        return nullptr;
+    }
+    auto *c = new KfChain();
+    c->den = den;
+    c->max_seqs = max_seqs;
+    c->max_frames = max_frames;
+    const int S = den->t->dev.S;
+    bool ok = hipMalloc(&c->alpha_store, (size_t)max_seqs * (max_frames + 1) * S * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->asum_store, (size_t)max_seqs * (max_frames + 1) * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->stats, (size_t)max_seqs * 8 * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_desc, (size_t)max_seqs * sizeof(LogFstDev)) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_row0, (size_t)max_seqs * 8) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_frames, (size_t)max_seqs * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->d_num_total, (size_t)max_seqs * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->den_out, (size_t)max_seqs * 8) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->ev_num, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        delete c;
+        kfc_set_error("kf_chain_create: hipMalloc failed");
+        return nullptr;
+    }
+    hipMemset(c->stats, 0, (size_t)max_seqs * 32);
+    return c;
+}
+extern "C" void kf_chain_free(KfChain *c) { delete c; }
+
+extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChainOpts *opts,
+                                const void *nnet_output, long long ld, long long num_rows, int nseq,
+                                const int32_t *seq_row0, const int32_t *seq_frames, int stride,
+                                void *out_grad, long long ldg) {
+    if (!c || !num || !opts || !nnet_output || !out_grad || !seq_row0 || !seq_frames) {
+        kfc_set_error("kf_chain_compute: NULL argument");
+        return -1;
+    }
+    const int P = c->den->t->dev.P;
+    if (nseq <= 0 || nseq > c->max_seqs || nseq != (int)num->nd->desc.size() || stride <= 0 ||
+        ld < P || ldg < P) {
+        kfc_set_error("kf_chain_compute: nseq %d (max %d, batch %zu), stride %d, ld %lld/%lld vs P %d",
+                      nseq, c->max_seqs, num->nd->desc.size(), stride, ld, ldg, P);
+        return -1;
+    }
+    hipStream_t st = kf_stream();
+    bool same = c->last_num == num && c->last_nseq == nseq && c->last_stride == stride &&
+                c->last_nnet == nnet_output && c->last_ld == ld && c->last_rows == num_rows &&
+                std::equal(seq_row0, seq_row0 + nseq, c->last_row0.begin(), c->last_row0.end()) &&
+                std::equal(seq_frames, seq_frames + nseq, c->last_frames.begin(),
+                           c->last_frames.end());
+    if (!same) {
+        for (int i = 0; i < nseq; ++i)
+            if (seq_frames[i] < 0 || seq_frames[i] > c->max_frames || seq_row0[i] < 0 ||
+                (seq_frames[i] > 0 &&
+                 seq_row0[i] + (long long)(seq_frames[i] - 1) * stride >= num_rows)) {
+                kfc_set_error("kf_chain_compute: sequence %d: %d frames (max %d), row0 %d, "
+                              "stride %d outside %lld rows", i, seq_frames[i], c->max_frames,
+                              seq_row0[i], stride, num_rows);
+                return -1;
+            }
+        hipStreamSynchronize(st);  // the staging vectors may still feed a copy
+        size_t ab = 0, ps = 0;
+        for (int i = 0; i < nseq; ++i) {
+            ab += 2 * (size_t)(seq_frames[i] + 1) * num->S[i];
+            ps += (size_t)seq_frames[i] * num->nd->G[i];
+        }
+        if (ab > c->num_ab_cap) {
+            if (c->num_ab) hipFree(c->num_ab);
+            c->num_ab = nullptr;
+            if (hipMalloc(&c->num_ab, ab * 4) != hipSuccess) {
+                c->num_ab_cap = 0;
+                kfc_set_error("kf_chain_compute: hipMalloc failed");
+                return -1;
+            }
+            c->num_ab_cap = ab;
+        }
+        if (ps > c->num_post_cap) {
+            if (c->num_post) hipFree(c->num_post);
+            c->num_post = nullptr;
+            if (hipMalloc(&c->num_post, std::max<size_t>(ps, 1) * 4) != hipSuccess) {
+                c->num_post_cap = 0;
+                kfc_set_error("kf_chain_compute: hipMalloc failed");
+                return -1;
+            }
+            c->num_post_cap = ps;
+        }
+        c->host_desc = num->nd->desc;
+        float *ab_p = c->num_ab, *ps_p = c->num_post;
+        std::vector<long long> r0(nseq);
+        for (int i = 0; i < nseq; ++i) {
+            LogFstDev &f = c->host_desc[i];
+            f.T = seq_frames[i];
+            f.mode = LF_FB | LF_POST;
+            f.stride = stride;
+            f.row0 = seq_row0[i];
+            f.alpha = ab_p;
+            ab_p += (size_t)(f.T + 1) * f.S;
+            f.beta = ab_p;
+            ab_p += (size_t)(f.T + 1) * f.S;
+            f.post_sparse = ps_p;
+            ps_p += (size_t)f.T * f.G;
+            f.post_dense = nullptr;
+            f.total = c->d_num_total + i;
+            r0[i] = seq_row0[i];
+        }
+        size_t lds = 0;
+        bool fits = true;
+        for (int i = 0; i < nseq; ++i) {
+            const LogFstDev &f = c->host_desc[i];
+            int Ag = (int)num->nd->Ag[i];
+            lds = std::max(lds, (size_t)num_lds_layout(f.S, f.A, f.G, Ag).words * 4);
+            fits = fits && f.S <= NUM_PRE * NUM_THREADS && f.G <= NUM_PRE * NUM_THREADS;
+        }
+        c->num_lds = (fits && lds <= 64 * 1024) ? lds : 0;
+        hipMemcpy(c->d_desc, c->host_desc.data(), nseq * sizeof(LogFstDev), hipMemcpyHostToDevice);
+        hipMemcpy(c->d_row0, r0.data(), nseq * 8, hipMemcpyHostToDevice);
+        hipMemcpy(c->d_frames, seq_frames, nseq * 4, hipMemcpyHostToDevice);
+        c->last_num = num;
+        c->last_nseq = nseq;
+        c->last_stride = stride;
+        c->last_nnet = nnet_output;
+        c->last_ld = ld;
+        c->last_rows = num_rows;
+        c->last_row0.assign(seq_row0, seq_row0 + nseq);
+        c->last_frames.assign(seq_frames, seq_frames + nseq);
+    }
+    double num_arcs = 0, frames = 0;
+    for (int i = 0; i < nseq; ++i) {
+        num_arcs += (double)c->host_desc[i].A * seq_frames[i];
+        frames += seq_frames[i];
+    }
+    // numerator on the side stream, overlapping the denominator forward
+    hipEventRecord(c->ev_in, st);
+    hipStreamWaitEvent(c->side, c->ev_in, 0);
+    {
+        hipStream_t saved = kf_stream();
+        kf_set_stream((void *)c->side);
+        int pn = kf_prof_start(KF_PROF_CHAIN_NUM, num_arcs);
+        if (c->num_lds)
+            hipLaunchKernelGGL(k_num_fb, dim3(nseq), dim3(NUM_THREADS), c->num_lds, c->side,
+                               (const LogFstDev *)c->d_desc, (const h16 *)nnet_output, ld, P);
+        else
+            hipLaunchKernelGGL(k_logfb, dim3(nseq), dim3(256), 0, c->side,
+                               (const LogFstDev *)c->d_desc, (const h16 *)nnet_output, ld, P);
+        kf_prof_stop(pn);
+        kf_set_stream((void *)saved);
+    }
+    hipEventRecord(c->ev_num, c->side);
+    DenRun r{};
+    r.nnet = nnet_output;
+    r.ld = ld;
+    r.row0 = c->d_row0;
+    r.frames = c->d_frames;
+    r.stride = stride;
+    r.max_frames = c->max_frames;
+    r.leaky = opts->leaky_hmm_coefficient;
+    r.backward = 1;
+    r.alpha_store = c->alpha_store;
+    r.asum_store = c->asum_store;
+    r.stats = c->stats;
+    r.den_out = c->den_out;
+    r.trace = c->trace;
+    r.nums = c->d_desc;
+    r.out_grad = (h16 *)out_grad;
+    r.ldg = ldg;
+    r.opts = *opts;
+    // algorithmic bytes: per frame three streamed passes over the
+    // packed arc records, alpha' stored and re-read, the output row read twice
+    // and the gradient row written once
+    const DenDev &dd = c->den->t->dev;
+    double bytes = frames * (3.0 * 8.0 * c->den->num_arcs + 8.0 * dd.S + 6.0 * dd.P);
+    int pd = kf_prof_start(KF_PROF_CHAIN_DEN, bytes);
+    DenX X{};
+    if (!c->xbuf.make(dd, nseq, den_pick_G(nseq), X)) {
+        kfc_set_error("kf_chain_compute: hipMalloc failed");
+        return -1;
+    }
+    launch_den_fwd(dd, r, X, c->xbuf, false);
+    hipStreamWaitEvent(st, c->ev_num, 0);
+    launch_den_bwd(dd, r, X, c->xbuf, false, DEN_PRODUCT);
+    kf_prof_stop(pd);
+    if (hipGetLastError() != hipSuccess) {
+        kfc_set_error("kf_chain_compute: launch failed");
+        return -1;
+    }
+    return 0;
+}
+
+// Diagnostics: when `buf` (device, 32*8 u64) is non-null, the den forward kernel of
+// sequence 0 / block 0 records 8 phase timestamps (wall_clock64, 100 MHz) for frames
+// 16..47 of every later compute. Not part of the product contract.
+extern "C" void kf_chain_trace(KfChain *c, unsigned long long *buf) {
+    if (c) c->trace = buf;
+}
+
+extern "C" const float *kf_chain_seq_stats(const KfChain *c) { return c ? c->stats : nullptr; }
+
+extern "C" int kf_chain_result(KfChain *c, KfChainResult *out) {
+    if (!c || !out) return -1;
+    const int n = c->last_nseq;
+    std::vector<float> s((size_t)n * 8);
+    hipStream_t st = kf_stream();
+    if (n) hipMemcpyAsync(s.data(), c->stats, s.size() * 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        kfc_set_error("kf_chain_result: stream error");
+        return -1;
+    }
+    if (n && c->xbuf.cnt && c->xbuf.timed_out(st, n)) {
+        kfc_set_error("kf_chain_result: den cross-workgroup exchange timed out (blocks not resident)");
+        return -1;
+    }
+    memset(out, 0, sizeof(*out));
+    for (int i = 0; i < n; ++i) {
+        const float *v = &s[(size_t)i * 8];
+        out->num_logprob += v[0];
+        out->den_logprob += v[1];
+        out->objf += v[2];
+        out->l2_term += v[3];
+        out->total_weight += v[4];
+        out->frames += (int)v[5];
+        out->out_of_range += (int)v[6];
+        out->num_ok += v[7] > 0.5f;
+    }
+    out->num_seqs = n;
+    return 0;
+}

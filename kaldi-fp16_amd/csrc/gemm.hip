@@ -605,6 +605,24 @@ hipEvent_t prof_event() {
 }  // namespace
 enum { KF_PROF_FUSED = 0, KF_PROF_WGRAD = 1, KF_PROF_NCLS = 2 };
 
+// generic bracket for other kernel classes (kf_common.h): returns a record
+// index, or -1 when profiling is off
+int kf_prof_start(int cls, double work) {
+    if (!g_prof) return -1;
+    ProfRec rec{};
+    rec.a = prof_event();
+    rec.b = prof_event();
+    rec.cls = cls;
+    rec.flops = work;
+    hipEventRecord(rec.a, kf_stream());
+    g_prof_recs.push_back(rec);
+    return (int)g_prof_recs.size() - 1;
+}
+void kf_prof_stop(int idx) {
+    if (idx < 0 || idx >= (int)g_prof_recs.size()) return;
+    hipEventRecord(g_prof_recs[idx].b, kf_stream());
+}
+
 extern "C" void kf_prof_enable(int on) { g_prof = on != 0; }
 // sums per class since the last collect: count, milliseconds, flops
 extern "C" int kf_prof_collect(int cls, long long *count, double *ms, double *flops) {

@@ -38,6 +38,12 @@ struct KfErr {
 // current stream (kf_ops.h: kf_set_stream)
 hipStream_t kf_stream();
 
+// kf_prof_* timing of a launch bracket on the current stream (gemm.hip);
+// classes: 0 fused GEMM, 1 wgrad GEMM, 2 chain numerator, 3 chain denominator
+enum { KF_PROF_CHAIN_NUM = 2, KF_PROF_CHAIN_DEN = 3 };
+int kf_prof_start(int cls, double work);
+void kf_prof_stop(int idx);
+
 // persistent per-device scratch (never freed; grows monotonically)
 void *kf_workspace(size_t bytes, int slot);
 

@@ -118,3 +118,58 @@ def trunc_fp16(a: np.ndarray) -> np.ndarray:
                           sign | ((np.clip(exp, -14, 15) + 15).astype(np.uint16) << 10)
                           | (frac >> 13).astype(np.uint16))).astype(np.uint16)
     return h.view(np.float16).astype(np.float32)
+
+
+# ---------------------------------------------------------------- chain supervision
+# the reference's den.fst / cegs archives are not in its repository,
+# so the objective runs on a fixed synthetic supervision of the same shape.
+
+def make_den_graph(num_states: int = 7052, num_arcs: int = 113380, num_pdfs: int = 3080,
+                   seed: int = 99) -> dict:
+    """Denominator graph: a ring s -> s+1 plus uniformly random arcs, labels
+    U[1, num_pdfs], tropical weights U[0.5, 5]; arcs listed state by state as an
+    FST stores them. Returned in the NativeDenominator form (denominator.go:78-95):
+    pdf0 = label - 1, tp = float32(exp(-weight)); start state 0."""
+    rng = np.random.default_rng(seed)
+    S, A = num_states, num_arcs
+    nr = A - S
+    src = np.concatenate([np.arange(S), rng.integers(0, S, size=nr)]).astype(np.int32)
+    dst = np.concatenate([(np.arange(S) + 1) % S, rng.integers(0, S, size=nr)]).astype(np.int32)
+    label = rng.integers(1, num_pdfs + 1, size=A).astype(np.int32)
+    weight = rng.uniform(0.5, 5.0, size=A).astype(np.float32)
+    order = np.argsort(src, kind="stable")
+    src, dst, label, weight = src[order], dst[order], label[order], weight[order]
+    tp = np.exp(-weight.astype(np.float64)).astype(np.float32)
+    return dict(S=S, P=num_pdfs, A=A, src=src, dst=dst, pdf0=(label - 1).astype(np.int32),
+                tp=tp, start=0)
+
+
+def make_num_fst(eg: int, num_states: int = 250, num_pdfs: int = 3080) -> dict:
+    """Numerator FST of eg `eg` (seed 7+eg): a self-loop and a forward arc per
+    state (the last state has only its self-loop), tropical weight 0.6931 on every
+    arc, labels U[1, num_pdfs], final state num_states-1 with weight 0. CSR with
+    negated (log) weights, as sparse.FstToCSR does (sparse.go:54-91)."""
+    rng = np.random.default_rng(7 + eg)
+    S = num_states
+    row_ptr, dst = [0], []
+    for s in range(S):
+        dst.append(s)
+        if s + 1 < S:
+            dst.append(s + 1)
+        row_ptr.append(len(dst))
+    A = len(dst)
+    pdf1 = rng.integers(1, num_pdfs + 1, size=A).astype(np.int32)
+    logw = np.full(A, -np.float32(0.6931), dtype=np.float32)
+    return dict(S=S, A=A, row_ptr=np.array(row_ptr, np.int32), dst=np.array(dst, np.int32),
+                pdf1=pdf1, logw=logw, final_state=np.array([S - 1], np.int32),
+                final_w=np.zeros(1, np.float32), start=0)
+
+
+def chain_layout(num_egs: int, frames_per_eg: int = 1500, left_context: int = 30,
+                 subsample: int = 3):
+    """Rows of the concatenated output that carry supervision: eg i frame k sits
+    at row i*frames_per_eg + left_context + k*subsample (chain_loss.go:243-259);
+    (frames_per_eg - left_context) // subsample = 490 frames per eg."""
+    fps = (frames_per_eg - left_context) // subsample
+    row0 = (np.arange(num_egs) * frames_per_eg + left_context).astype(np.int32)
+    return row0, np.full(num_egs, fps, np.int32), subsample

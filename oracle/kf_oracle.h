@@ -98,6 +98,52 @@ void orc_net_free(OrcNet *net);
 /* v = mom*v + g; w32 -= lr*v (backward_wrappers.cu:129-142) */
 void orc_sgd(float *w32, const float *g, float *v, float lr, float mom, long long n);
 
+/* ------------------------------------------------------------------------- */
+/* Chain LF-MMI objective (kf_oracle_chain.c)                                */
+/* ------------------------------------------------------------------------- */
+/* Denominator graph, prob space (cpp/cuda/chain_den.cu, internal/nnet/denominator.go). */
+typedef struct {
+    int S, P, A;
+    const int *src, *dst, *pdf0;   /* pdf0: 0-indexed (label - 1, denominator.go:83) */
+    const float *tp;               /* exp(-tropical weight) (denominator.go:87) */
+    const float *init;             /* [S] initial probs (orc_den_initial_probs) */
+} OrcDen;
+
+/* Numerator FST in CSR, log domain (internal/sparse/sparse.go:54-91, chain.h:23-35). */
+typedef struct {
+    int S, A, nfinal, start;
+    const int *row_ptr, *dst, *pdf1;  /* pdf1: 1-indexed, 0 = epsilon (skipped) */
+    const float *logw;                /* negated tropical weights */
+    const int *final_state;
+    const float *final_w;
+} OrcNum;
+
+/* Mirrors ChainTrainingOpts (internal/nnet/backward.go:114-140). */
+typedef struct {
+    float l2_regularize, out_of_range_regularize, leaky_hmm_coefficient, xent_regularize,
+        supervision_weight;
+} OrcChainOpts;
+
+typedef struct {
+    double objf, l2_term, total_weight, num_logprob, den_logprob;
+    int frames, out_of_range, ok;
+} OrcChainResult;
+
+/* 100 float64 iterations from the start state, averaged (denominator.go:131-171). */
+void orc_den_initial_probs(int S, int A, const int *src, const int *dst, const float *tp,
+                           int start, float *init_out);
+/* den_forward / den_forward_backward (chain_den.cu:371-472, :496-706). nnet [T x P];
+ * post [T x P] (NULL = forward only). Returns the log-prob. */
+float orc_den_forward_backward(const OrcDen *den, const float *nnet, int T, float leaky,
+                               float *post);
+/* Deterministic log-domain numerator (chain_det.cu:55-237): nnet values are used as
+ * given (the caller rounds to fp16, as chain_backward.cu:372-379 does). post [T x P]
+ * is overwritten (NULL = skip). Returns the total log-prob. */
+float orc_num_forward_backward(const OrcNum *num, const float *nnet, int T, int P, float *post);
+/* ComputeChainObjfAndDeriv for one sequence (backward.go:224-371): deriv [T x P]. */
+int orc_chain_objf(const OrcChainOpts *opts, const OrcDen *den, const OrcNum *num,
+                   const float *nnet, int T, float *deriv, OrcChainResult *res);
+
 #ifdef __cplusplus
 }
 #endif

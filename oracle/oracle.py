@@ -299,3 +299,122 @@ class OracleNet:
             self.close()
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------- chain objective
+_ip = C.POINTER(C.c_int)
+
+
+class OrcDen(C.Structure):
+    _fields_ = [("S", C.c_int), ("P", C.c_int), ("A", C.c_int), ("src", _ip), ("dst", _ip),
+                ("pdf0", _ip), ("tp", _fp), ("init", _fp)]
+
+
+class OrcNum(C.Structure):
+    _fields_ = [("S", C.c_int), ("A", C.c_int), ("nfinal", C.c_int), ("start", C.c_int),
+                ("row_ptr", _ip), ("dst", _ip), ("pdf1", _ip), ("logw", _fp),
+                ("final_state", _ip), ("final_w", _fp)]
+
+
+class OrcChainOpts(C.Structure):
+    _fields_ = [("l2_regularize", C.c_float), ("out_of_range_regularize", C.c_float),
+                ("leaky_hmm_coefficient", C.c_float), ("xent_regularize", C.c_float),
+                ("supervision_weight", C.c_float)]
+
+
+class OrcChainResult(C.Structure):
+    _fields_ = [("objf", C.c_double), ("l2_term", C.c_double), ("total_weight", C.c_double),
+                ("num_logprob", C.c_double), ("den_logprob", C.c_double), ("frames", C.c_int),
+                ("out_of_range", C.c_int), ("ok", C.c_int)]
+
+
+def _chain_sigs(L):
+    if getattr(L, "_chain_sigs", False):
+        return L
+    L.orc_den_initial_probs.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_int, C.c_void_p]
+    L.orc_den_forward_backward.restype = C.c_float
+    L.orc_den_forward_backward.argtypes = [C.POINTER(OrcDen), C.c_void_p, C.c_int, C.c_float,
+                                           C.c_void_p]
+    L.orc_num_forward_backward.restype = C.c_float
+    L.orc_num_forward_backward.argtypes = [C.POINTER(OrcNum), C.c_void_p, C.c_int, C.c_int,
+                                           C.c_void_p]
+    L.orc_chain_objf.argtypes = [C.POINTER(OrcChainOpts), C.POINTER(OrcDen), C.POINTER(OrcNum),
+                                 C.c_void_p, C.c_int, C.c_void_p, C.POINTER(OrcChainResult)]
+    L._chain_sigs = True
+    return L
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def den_initial_probs(g: dict) -> np.ndarray:
+    """denominator.go:131-171 on a synth.make_den_graph dict."""
+    L = _chain_sigs(lib())
+    src, dst, tp = _c(g["src"], np.int32), _c(g["dst"], np.int32), _c(g["tp"], np.float32)
+    out = np.empty(int(g["S"]), np.float32)
+    L.orc_den_initial_probs(int(g["S"]), int(g["A"]), src.ctypes.data, dst.ctypes.data,
+                            tp.ctypes.data, int(g["start"]), out.ctypes.data)
+    return out
+
+
+def _den_struct(g, init):
+    keep = [_c(g["src"], np.int32), _c(g["dst"], np.int32), _c(g["pdf0"], np.int32),
+            _c(g["tp"], np.float32), _c(init, np.float32)]
+    d = OrcDen(int(g["S"]), int(g["P"]), int(g["A"]), _ptr(keep[0], C.c_int), _ptr(keep[1], C.c_int),
+               _ptr(keep[2], C.c_int), _ptr(keep[3], C.c_float), _ptr(keep[4], C.c_float))
+    return d, keep
+
+
+def _num_struct(f):
+    keep = [_c(f["row_ptr"], np.int32), _c(f["dst"], np.int32), _c(f["pdf1"], np.int32),
+            _c(f["logw"], np.float32), _c(f["final_state"], np.int32), _c(f["final_w"], np.float32)]
+    n = OrcNum(int(f["S"]), int(f["A"]), len(keep[4]), int(f.get("start", 0)),
+               _ptr(keep[0], C.c_int), _ptr(keep[1], C.c_int), _ptr(keep[2], C.c_int),
+               _ptr(keep[3], C.c_float), _ptr(keep[4], C.c_int), _ptr(keep[5], C.c_float))
+    return n, keep
+
+
+def den_forward_backward(g: dict, init, nnet: np.ndarray, leaky=1e-5, posteriors=True):
+    """chain_den.cu:496-706 (den_forward when posteriors=False). Returns (logprob, post)."""
+    L = _chain_sigs(lib())
+    d, keep = _den_struct(g, init)
+    x = _c(nnet, np.float32)
+    T = x.shape[0]
+    post = np.empty_like(x) if posteriors else None
+    lp = L.orc_den_forward_backward(C.byref(d), x.ctypes.data, T, leaky,
+                                    post.ctypes.data if posteriors else None)
+    return float(lp), post
+
+
+def num_forward_backward(f: dict, nnet: np.ndarray, posteriors=True):
+    """chain_det.cu:55-237 on nnet values used as given. Returns (logprob, post)."""
+    L = _chain_sigs(lib())
+    n, keep = _num_struct(f)
+    x = _c(nnet, np.float32)
+    T, P = x.shape
+    post = np.empty_like(x) if posteriors else None
+    lp = L.orc_num_forward_backward(C.byref(n), x.ctypes.data, T, P,
+                                    post.ctypes.data if posteriors else None)
+    return float(lp), post
+
+
+def chain_objf(g: dict, init, f: dict, nnet: np.ndarray, l2=0.0, oor=0.01, leaky=1e-5, weight=1.0):
+    """ComputeChainObjfAndDeriv for one sequence (backward.go:224-371).
+    Returns (deriv [T x P], result dict)."""
+    L = _chain_sigs(lib())
+    d, k1 = _den_struct(g, init)
+    n, k2 = _num_struct(f)
+    x = _c(nnet, np.float32)
+    T = x.shape[0]
+    deriv = np.empty_like(x)
+    r = OrcChainResult()
+    o = OrcChainOpts(l2, oor, leaky, 0.0, weight)
+    L.orc_chain_objf(C.byref(o), C.byref(d), C.byref(n), x.ctypes.data, T, deriv.ctypes.data, C.byref(r))
+    res = {k: getattr(r, k) for k, _ in OrcChainResult._fields_}
+    return deriv, res

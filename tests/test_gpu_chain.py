@@ -1,0 +1,232 @@
+"""HIP chain objective vs the CPU oracle (oracle/kf_oracle_chain.c), through the C-ABI.
+
+Tolerances: objective |Δ objf/frame| <= 1e-3 (chainverify/main.go:169);
+numerator log-prob |Δ| <= 1e-2 vs the deterministic FP32 oracle. Posteriors and
+output-gradient elements: |Δ| <= 1e-4 + one fp16 ulp of the value (float32
+summation order differs between the GPU tree and the oracle's sequential sums).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def den():
+    from kfp16 import synth
+    g = synth.make_den_graph()
+    return g, oracle.den_initial_probs(g)
+
+
+def _x(T, P, seed, scale=2.0):
+    return (np.random.default_rng(seed).standard_normal((T, P)) * scale).astype(np.float16)
+
+
+def test_den_abi_matches_oracle(gpu, den):
+    from kfp16 import chain
+    g, init = den
+    T = 490
+    x = _x(T, g["P"], 11).astype(np.float32)
+    x[5, :7] = [45.0, -45.0, 30.5, -30.5, 29.0, 0.0, -29.0]  # clamp edges
+    fst = chain.DenFstGPU()
+    rc = gpu.core.den_fst_upload(C.byref(fst), g["src"].ctypes.data, g["dst"].ctypes.data,
+                                 g["pdf0"].ctypes.data, g["tp"].ctypes.data, g["A"], g["S"], g["P"])
+    assert rc == 0, gpu.core.den_last_error()
+    post = np.empty_like(x)
+    lp = gpu.core.den_forward_backward(C.byref(fst), x.ctypes.data, init.ctypes.data, T, 1e-5,
+                                       post.ctypes.data)
+    lpf = gpu.core.den_forward(C.byref(fst), x.ctypes.data, init.ctypes.data, T, 1e-5)
+    gpu.core.den_fst_free(C.byref(fst))
+    rlp, rpost = oracle.den_forward_backward(g, init, x)
+    assert lp == lpf
+    assert abs(lp - rlp) / T <= 1e-5, (lp, rlp)
+    np.testing.assert_allclose(post, rpost, atol=1e-5)
+    np.testing.assert_allclose(post.sum(1), 1.0, atol=1e-4)
+
+
+def test_den_abi_rejects_unknown_fst(gpu):
+    from kfp16 import chain
+    fst = chain.DenFstGPU()
+    x = np.zeros((2, 4), np.float32)
+    assert gpu.core.den_forward(C.byref(fst), x.ctypes.data, x.ctypes.data, 2, 1e-5) == np.float32(-1e30)
+    assert gpu.core.den_last_error()
+
+
+def _device_fst(gpu, f, keep):
+    from kfp16 import chain
+    def up(a, dt):
+        a = np.ascontiguousarray(a, dt)
+        b = gpu.DeviceBuffer(a.nbytes)
+        gpu.check(gpu.core.bridge_transfer_int32(b.ptr, a.view(np.int32).ctypes.data, a.size))
+        keep.append(b)
+        return b.ptr
+    return chain.ChainFstGPU(up(f["row_ptr"], np.int32), up(f["dst"], np.int32),
+                             up(f["pdf1"], np.int32), up(f["logw"], np.float32),
+                             up(f["final_state"], np.int32), up(f["final_w"], np.float32),
+                             f["S"], f["A"], len(f["final_state"]), f.get("start", 0))
+
+
+def test_num_abi_matches_oracle(gpu):
+    from kfp16 import synth
+    f = synth.make_num_fst(3)
+    T, P = 490, 3080
+    x32 = (np.random.default_rng(5).standard_normal((T, P)) * 2).astype(np.float32)
+    keep = []
+    fst = _device_fst(gpu, f, keep)
+    dx = gpu.upload_f32(x32)
+    post = gpu.DeviceBuffer(T * P * 4)
+    lp = gpu.core.chain_num_forward_backward(fst.row_ptr, fst.col_idx, fst.weights, fst.labels,
+                                             fst.final_states, fst.final_weights, f["S"], f["A"], 1,
+                                             dx.ptr, post.ptr, T, P, None)
+    got = gpu.read_f32(post.ptr, (T, P))
+    rlp, rpost = oracle.num_forward_backward(f, x32.astype(np.float16).astype(np.float32))
+    assert abs(lp - rlp) <= 1e-2, (lp, rlp)
+    np.testing.assert_allclose(got, rpost, atol=1e-4)
+
+
+def test_chain_compute_loss_abi(gpu):
+    """C1 path: log-domain FB on both FSTs, grad16 = clamp(den - num, +-30)."""
+    from kfp16 import chain, synth
+    T, P = 60, 3080
+    f = synth.make_num_fst(1, num_states=30)
+    d = synth.make_num_fst(2, num_states=45)      # a second FST standing in for "den as FST"
+    d["final_state"] = np.arange(d["S"], dtype=np.int32)
+    d["final_w"] = np.zeros(d["S"], np.float32)
+    keep = []
+    nf, df = _device_fst(gpu, f, keep), _device_fst(gpu, d, keep)
+    x = _x(T, P, 8)
+    dx = gpu.upload_fp16(x)
+    g = gpu.DeviceBuffer(T * P * 2)
+    res = chain.ChainLossResult()
+    rc = gpu.core.chain_compute_loss(dx.ptr, C.byref(nf), C.byref(df), T, P, g.ptr, C.byref(res))
+    assert rc == 0, gpu.core.chain_last_error()
+    xf = x.astype(np.float32)
+    nl, npost = oracle.num_forward_backward(f, xf)
+    dl, dpost = oracle.num_forward_backward(d, xf)
+    assert abs(res.num_logprob - nl) <= 1e-2 and abs(res.den_logprob - dl) <= 1e-2
+    assert abs(res.loss + (nl - dl)) <= 2e-2
+    got = gpu.read_fp16(g.ptr, (T, P)).astype(np.float32)
+    ref = np.clip(dpost - npost, -30, 30)
+    assert np.all(np.abs(got - ref) <= 1e-4 + np.abs(ref) * 2 ** -10)
+
+
+def test_objective_pieces_abi(gpu):
+    rng = np.random.default_rng(4)
+    T, P = 7, 33
+    x = (rng.standard_normal((T, P)) * 20).astype(np.float32)
+    g0 = rng.standard_normal((T, P)).astype(np.float32)
+    num, den = rng.random((T, P)).astype(np.float32), rng.random((T, P)).astype(np.float32)
+    dx, dg, dn, dd = (gpu.upload_f32(a) for a in (x, g0, num, den))
+    n = gpu.core.chain_penalize_out_of_range(dx.ptr, dg.ptr, 30.0, 0.02, T, P)
+    ref = g0.copy()
+    even = (np.arange(T) % 2 == 0)[:, None]
+    lo, hi = even & (x < -30), even & (x > 30)
+    ref[lo] += (-30 - x[lo]) * 0.02
+    ref[hi] += (30 - x[hi]) * 0.02
+    assert n == int(lo.sum() + hi.sum())
+    np.testing.assert_allclose(gpu.read_f32(dg.ptr, (T, P)), ref, rtol=1e-6, atol=1e-6)
+    term = gpu.core.chain_l2_regularize(dx.ptr, dg.ptr, 0.5, T * P)
+    ref = ref - 0.5 * x
+    assert abs(term + 0.25 * float(np.sum(x.astype(np.float64) ** 2))) <= 1e-3 * abs(term)
+    assert gpu.core.chain_add_posterior_gradient(dn.ptr, dd.ptr, dg.ptr, 2.0, T * P) == 0
+    ref = ref + 2.0 * (num - den)
+    np.testing.assert_allclose(gpu.read_f32(dg.ptr, (T, P)), ref, rtol=1e-5, atol=1e-5)
+    h = gpu.DeviceBuffer(T * P * 2)
+    assert gpu.core.chain_combine_gradient(dn.ptr, dd.ptr, 1.5, T, P, h.ptr) == 0
+    np.testing.assert_array_equal(gpu.read_fp16(h.ptr, (T, P)), (1.5 * (num - den)).astype(np.float16))
+    assert gpu.core.chain_grad_fp32_to_fp16(dg.ptr, h.ptr, T * P) == 0
+    gpu.sync()
+    np.testing.assert_array_equal(gpu.read_fp16(h.ptr, (T, P)),
+                                  gpu.read_f32(dg.ptr, (T, P)).astype(np.float16))
+
+
+def _batch_setup(gpu, den, negs, frames_per_eg=1500, seed=21):
+    from kfp16 import chain, synth
+    g, init = den
+    P = g["P"]
+    row0, frames, stride = synth.chain_layout(negs, frames_per_eg)
+    fsts = [synth.make_num_fst(i) for i in range(negs)]
+    x = _x(negs * frames_per_eg, P, seed)
+    return g, init, P, row0, frames, stride, fsts, x
+
+
+def test_batched_objective_matches_oracle(gpu, den):
+    from kfp16 import chain
+    negs = 3
+    g, init, P, row0, frames, stride, fsts, x = _batch_setup(gpu, den, negs)
+    frames = frames.copy()
+    frames[1] = 301              # ragged: a shorter sequence
+    x[row0[2] + 6 * stride, 100] = 40.0   # even frame: penalised
+    x[row0[2] + 7 * stride, 101] = -40.0  # odd frame: not penalised
+    dx = gpu.upload_fp16(x)
+    og = gpu.upload_fp16(np.full(x.shape, 7.0, np.float16))  # sentinel
+    dg = chain.DenGraph(g)
+    np.testing.assert_allclose(dg.initial_probs(), init, rtol=0, atol=0)
+    ch = chain.Chain(dg, max_seqs=8, max_frames=490)
+    nb = chain.NumBatch(fsts)
+    ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+    res = ch.result()
+    got = gpu.read_fp16(og.ptr, x.shape).astype(np.float32)
+    stats = ch.seq_stats(negs)
+    xf = x.astype(np.float32)
+    sup = np.zeros(x.shape[0], bool)
+    tot_objf = 0.0
+    for i in range(negs):
+        rows = row0[i] + np.arange(frames[i]) * stride
+        sup[rows] = True
+        deriv, r = oracle.chain_objf(g, init, fsts[i], xf[rows])
+        assert abs(stats[i, 0] - r["num_logprob"]) <= 1e-2
+        assert abs(stats[i, 1] - r["den_logprob"]) / frames[i] <= 1e-4
+        assert abs(stats[i, 2] - r["objf"]) / frames[i] <= 1e-3
+        assert int(stats[i, 6]) == r["out_of_range"] and stats[i, 7] == 1.0
+        tot_objf += r["objf"]
+        ref = -deriv
+        err = np.abs(got[rows] - ref) - (1e-4 + np.abs(ref) * 2 ** -10)
+        assert np.all(err <= 0), (i, float(err.max()))
+    assert int(stats[2, 6]) == 1
+    assert np.all(got[~sup] == 7.0)          # rows without supervision are not touched
+    assert res.num_seqs == negs and res.num_ok == negs and res.frames == int(frames.sum())
+    assert abs(res.objf - tot_objf) / res.frames <= 1e-3
+
+
+def test_batched_objective_nan_rule(gpu, den):
+    from kfp16 import chain
+    negs = 2
+    g, init, P, row0, frames, stride, fsts, x = _batch_setup(gpu, den, negs, seed=5)
+    # +inf on the numerator path of eg 1 at frame 0 (its first arc's pdf)
+    x[row0[1], fsts[1]["pdf1"][0] - 1] = np.inf
+    dx = gpu.upload_fp16(x)
+    og = gpu.upload_fp16(np.full(x.shape, 7.0, np.float16))
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=2, max_frames=490)
+    nb = chain.NumBatch(fsts)
+    ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+    res = ch.result()
+    got = gpu.read_fp16(og.ptr, x.shape).astype(np.float32)
+    rows1 = row0[1] + np.arange(frames[1]) * stride
+    assert not np.any(got[rows1])
+    assert res.num_ok == 1
+    stats = ch.seq_stats(negs)
+    assert stats[1, 7] == 0.0 and stats[1, 2] == -10.0 * frames[1]
+    rows0 = row0[0] + np.arange(frames[0]) * stride
+    assert np.any(got[rows0] != 0)
+
+
+def test_batched_objective_repeatable(gpu, den):
+    """Fixed arc order + fixed-point den accumulation: bit-identical reruns."""
+    from kfp16 import chain
+    negs = 2
+    g, init, P, row0, frames, stride, fsts, x = _batch_setup(gpu, den, negs, seed=9)
+    dx = gpu.upload_fp16(x)
+    og = gpu.DeviceBuffer(x.size * 2)
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=2, max_frames=490)
+    nb = chain.NumBatch(fsts)
+    outs = []
+    for _ in range(2):
+        ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+        ch.result()
+        outs.append(gpu.read_fp16(og.ptr, x.shape))
+    np.testing.assert_array_equal(outs[0], outs[1])
