@@ -100,6 +100,10 @@ const float *kf_chain_seq_stats(const KfChain *c);
 /* Synchronises the stream and sums the per-sequence statistics. */
 int kf_chain_result(KfChain *c, KfChainResult *out);
 
+/* diagnostics: phase timestamps of the den forward kernel (sequence 0, block 0,
+ * frames 16..47, 8 u64 each, 100 MHz wall clock) into a device buffer; NULL = off */
+void kf_chain_trace(KfChain *c, unsigned long long *dev_buf);
+
 const char *kf_chain_last_error(void);
 void kf_chain_clear_error(void);
 

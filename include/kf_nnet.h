@@ -71,6 +71,12 @@ float *nnet_master_buffer(KfNet *net); /* device fp32 [num_params] */
 void *nnet_weight_buffer(KfNet *net);  /* device fp16 [num_params] */
 int nnet_sgd(KfNet *net, float lr, float momentum);
 
+/* diagnostics (tests): back-propagate through the top n layers only; device
+ * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott", "aux", "mask",
+ * "bn_scale", "bn2_scale"; `layer` selects the per-layer ones), NULL if unknown */
+int nnet_backward_n(KfNet *net, const void *out_grad_dev, int n);
+const void *nnet_debug_tensor(KfNet *net, const char *what, int layer);
+
 #ifdef __cplusplus
 }
 #endif

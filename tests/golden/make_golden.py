@@ -12,10 +12,6 @@ expected outputs — and names where its expected values come from.
                         log-probs and posteriors from a float64 dense-matrix
                         restatement of chain_den.cu:496-706 (independent of the C oracle;
                         the reference's CUDA den cannot run in this container).
-  tiny_forward.npz      regression fixture of the C oracle's forward of configs/tiny.xconfig
-                        at T=64 with the synth.py seeds (self-pinned: guards the oracle
-                        against accidental change; network parity itself is unpinned by
-                        the reference).
 """
 import os
 import sys
@@ -62,16 +58,7 @@ def den_small():
     np.savez_compressed(os.path.join(OUT, "den_small.npz"), **out)
 
 
-def tiny_forward():
-    import oracle
-    from kfp16 import synth
-    from oracle_net_setup import oracle_tiny
-    feats, acts = oracle_tiny(64)
-    np.savez_compressed(os.path.join(OUT, "tiny_forward.npz"), features=feats, **acts)
-
-
 if __name__ == "__main__":
     chain_linear()
     den_small()
-    tiny_forward()
     print("wrote", sorted(f for f in os.listdir(OUT) if f.endswith(".npz")))
