@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void k_logfb(const LogFstDev *fsts, const h16 
 // output row are fetched, one frame ahead. Same arithmetic and order as k_logfb.
 // ---------------------------------------------------------------------------
 #define NUM_THREADS 256
-#define NUM_PRE 16  // S, G <= 4096
+#define NUM_PRE 4  // S, G <= 1024 (larger FSTs use k_logfb)
 
 struct NumLds {  // word offsets into dynamic LDS
     int a0, a1, ar0, ar1, xg0, xg1, in_ptr, in_src, in_g, in_w, row_ptr, arc_dst, arc_g, arc_w,
@@ -289,10 +289,11 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
     auto fetch_x = [&](int t) {
         const h16 *xr = row_of(t);
 #pragma unroll
-        for (int i = 0; i < NUM_PRE; ++i) {
+        for (int i = 0; i < NUM_PRE; ++i) {  // unconditional (clamped) loads, then select
             int q = tid + i * NUM_THREADS;
             int p = q < G ? I[L.gpdf + q] : 0;
-            pre[i] = (p > 0 && p <= P) ? (float)xr[p - 1] : 0.0f;
+            float v = (float)xr[min(max(p, 1), P) - 1];
+            pre[i] = (p > 0 && p <= P) ? v : 0.0f;
         }
     };
     auto store_x = [&](float *xg) {
@@ -351,7 +352,8 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
 #pragma unroll
         for (int i = 0; i < NUM_PRE; ++i) {
             int s = tid + i * NUM_THREADS;
-            apre[i] = s < S ? ar[s] : 0.0f;
+            float v = ar[min(s, S - 1)];
+            apre[i] = s < S ? v : 0.0f;
         }
     };
     auto store_alpha = [&](float *dst) {
@@ -428,7 +430,8 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
 struct SellDev {  // sliced ELL, 64 rows per slice, rows sorted by degree
     int nsl;
     const int *perm, *len, *off;
-    const uint2 *arc;  // {f1 | f2 << 16, tp}
+    const uint2 *arc;     // {f1 | f2 << 16, tp}
+    const float *initp;   // init[perm[c]] in slice order (0 for padding rows), f and b only
 };
 struct DenDev {
     int S, P;
@@ -449,6 +452,7 @@ struct DenRun {
     float *den_out;         // [nseq][2] {total_prob, log-prob} from k_den_fwd
     unsigned long long *trace;  // optional phase timestamps (kf_chain_trace), null = off
     float *alpha_store;     // [nseq][(max_frames+1) x S]
+    float *beta_store;      // [nseq][(max_frames+1) x S]
     float *asum_store;      // [nseq][max_frames+1]
     float *stats;           // [nseq][8]
     // ABI mode
@@ -512,11 +516,15 @@ struct StatePre {  // alpha' row prefetch (S <= DEN_MAXS * DEN_THREADS)
     }
 };
 
-static size_t den_fwd_lds_bytes(int S, int P, int nsl) {
-    return (size_t)4 * (64 + 2 * (size_t)S + P + (size_t)nsl * 66);
+// fwd / bwd: fixed part (va or vb, xe, len/off/coff); the rest of the 160 KiB LDS
+// holds resident arc records
+#define DEN_LDS_TOTAL (160 * 1024)
+static size_t den_rec_fixed_bytes(int S, int P, int nsl) {
+    return (size_t)4 * (64 + (size_t)S + P + (P & 1) + 2 * (size_t)nsl + 128 * (size_t)nsl +
+                        nsl + 2) + 64;
 }
-static size_t den_lds_bytes(int S, int P, int nsl, int nslq) {
-    return (size_t)4 * (64 + 2 * (size_t)S + 3 * (size_t)P + (size_t)(nsl + nslq) * 66);
+static size_t den_post_lds_bytes(int S, int P, int nslq) {
+    return (size_t)4 * (64 + 2 * (size_t)S + 3 * (size_t)P + (size_t)nslq * 66);
 }
 
 // ---------------------------------------------------------------------------
@@ -542,6 +550,8 @@ struct DenX {
     float *buf;     // [nseq][2][G][blk]; blk = spg*64 + 64 (tail: lane 0 = partial sum)
     unsigned *cnt;  // [nseq] arrivals, then [1] timeout word (zeroed before each launch)
     int G, lgG, spg, blk, nseq;
+    unsigned cache_f, cache_b;  // LDS bytes for resident arc records (fwd / bwd kernels)
+    unsigned lds_f, lds_b;      // dynamic LDS of the fwd / bwd kernels
 };
 
 // seq / slice-owner of this block; the G blocks of a sequence share an XCD when
@@ -604,27 +614,28 @@ __device__ __forceinline__ float den_gather_psum(const DenX &X, int seq, int buf
 }
 // all exchanged slices of buffer `buf`, scattered to their states: f(state, value)
 template <class F>
-__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, int nsl, const int *perml,
-                                            F f) {
-    const int tid = threadIdx.x;
+__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, int nsl,
+                                            const int *perm, const float *initp, F f) {
+    const int tid = threadIdx.x, n = nsl * 64;
     const float *xb = X.buf + ((size_t)seq * 2 + buf) * X.G * X.blk;
     float v[DEN_MAXS];
 #pragma unroll
     for (int m = 0; m < DEN_MAXS; ++m) {  // all loads in flight at once, unconditionally
-        const int c = min(tid + m * DEN_THREADS, nsl * 64 - 1), j = c >> 6;
+        const int c = min(tid + m * DEN_THREADS, n - 1), j = c >> 6;
         v[m] = ld_sc1(xb + (size_t)(j & (X.G - 1)) * X.blk + (j >> X.lgG) * 64 + (c & 63));
     }
 #pragma unroll
     for (int m = 0; m < DEN_MAXS; ++m) {
         const int c = tid + m * DEN_THREADS;
-        if (c < nsl * 64) {
-            const int st = perml[c];
-            if (st >= 0) f(st, v[m], (c >> 6) & (X.G - 1));
+        if (c < n) {
+            const int st = perm[c];
+            if (st >= 0) f(st, v[m], initp[c], (c >> 6) & (X.G - 1));
         }
     }
 }
 
-// gather-sum over one slice of a SELL table (fixed arc order)
+// gather-sum over one slice of a SELL table (fixed arc order); arcs may be a
+// global table or the LDS cache (callers branch, so each call's space is static)
 template <class Term>
 __device__ __forceinline__ float sell_slice(const uint2 *arcs, int len, int off, int lane, Term term) {
     const uint2 *e = arcs + (size_t)off * 64 + lane;
@@ -641,13 +652,49 @@ __device__ __forceinline__ float sell_slice(const uint2 *arcs, int len, int off,
     return acc;
 }
 
-// SELL meta (perm, len, off) staged in LDS: perm [nsl*64] then len [nsl], off [nsl]
-__device__ __forceinline__ void stage_sell(const SellDev &T, int *dst) {
-    for (int i = threadIdx.x; i < T.nsl * 64; i += DEN_THREADS) dst[i] = T.perm[i];
+// Per-block SELL state in LDS: len/off of every slice, and the arc records of this
+// block's first `kc` owned slices (slices gi, gi+G, ...), which then never leave
+// LDS for the whole launch (the rest are streamed from L2 every frame).
+struct SellLds {
+    const int *len, *off;  // [nsl] each
+    const int *perm;       // [nsl*64]
+    const float *initp;    // [nsl*64]
+    const int *coff;       // [nk] record offset of owned slice k in the cache
+    const uint2 *cache;
+    int kc;
+};
+__device__ __forceinline__ SellLds stage_sell(const SellDev &T, int gi, int G, int nk,
+                                              unsigned char *base, size_t cache_bytes) {
+    int *lenl = reinterpret_cast<int *>(base), *offl = lenl + T.nsl;
+    int *perml = offl + T.nsl;
+    float *initl = reinterpret_cast<float *>(perml + T.nsl * 64);
+    int *coff = reinterpret_cast<int *>(initl + T.nsl * 64);
+    uint2 *cache = reinterpret_cast<uint2 *>(coff + ((nk + 1) & ~1));
     for (int i = threadIdx.x; i < T.nsl; i += DEN_THREADS) {
-        dst[T.nsl * 64 + i] = T.len[i];
-        dst[T.nsl * 65 + i] = T.off[i];
+        lenl[i] = T.len[i];
+        offl[i] = T.off[i];
     }
+    for (int i = threadIdx.x; i < T.nsl * 64; i += DEN_THREADS) {
+        perml[i] = T.perm[i];
+        initl[i] = T.initp[i];
+    }
+    int kc = 0;
+    size_t used = 0;
+    for (int k = 0; k < nk; ++k) {  // every thread, same answer
+        const size_t rec = (size_t)T.len[gi + G * k] * 64;
+        if ((used + rec) * 8 > cache_bytes) break;
+        if (threadIdx.x == 0) coff[k] = (int)(used / 64);  // in 64-record rows, like T.off
+        used += rec;
+        kc = k + 1;
+    }
+    for (int k = 0, o = 0; k < kc; ++k) {
+        const int j = gi + G * k, n = T.len[j] * 64;
+        const uint2 *src = T.arc + (size_t)T.off[j] * 64;
+        for (int i = threadIdx.x; i < n; i += DEN_THREADS) cache[o + i] = src[i];
+        o += n;
+    }
+    SellLds L{lenl, offl, perml, initl, coff, cache, kc};
+    return L;
 }
 
 // Forward pass (chain_den.cu:583-620), G blocks per sequence: block gi computes
@@ -664,10 +711,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     float *red = reinterpret_cast<float *>(smem);          // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;        // [32]
     float *va = reinterpret_cast<float *>(smem) + 64;      // [S] alpha'[t]
-    float *initl = va + S;                                 // [S]
-    float *xe = initl + S;                                 // [P] exp(clamp(x))
-    int *meta = reinterpret_cast<int *>(xe + P);           // perm, len, off of g.f
-    const int *perml = meta, *lenl = meta + nsl * 64, *offl = meta + nsl * 65;
+    float *xe = va + S;                                    // [P] exp(clamp(x))
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + P + (P & 1));
+    const int nk = (nsl - gi + G - 1) / G;                 // slices owned by this block
 
     const int T = r.frames[seq];
     const long long row0 = r.row0[seq];
@@ -676,16 +722,12 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
     const float leaky = r.leaky;
 
-    stage_sell(g.f, meta);
+    const SellLds F = stage_sell(g.f, gi, G, nk, sbase, X.cache_f);
     float part = 0.f;
-    for (int s = tid; s < S; s += DEN_THREADS) {
-        float v = g.init[s];
-        initl[s] = v;
-        part += v;
-    }
+    for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
     float as = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
     for (int s = tid; s < S; s += DEN_THREADS) {
-        float v = initl[s] + as * leaky * initl[s];
+        float v = g.init[s] + as * leaky * g.init[s];
         va[s] = v;
         if (gi == 0) astore[s] = v;
     }
@@ -704,7 +746,6 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
         }
     }
     __syncthreads();
-    const int nk = (nsl - gi + G - 1) / G;  // slices owned by this block
     const bool tr = r.trace && seq == 0 && gi == 0 && tid == 0;
 #define DEN_TP(i) \
     if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
@@ -715,12 +756,12 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
         const bool scale = as > 0.0f;
         const float inv = scale ? 1.0f / as : 1.0f;
         part = 0.f;
+        auto term = [&](int src, int pdf, float tp) { return va[src] * tp * xe[pdf]; };
         for (int k = wave; k < nk; k += DEN_WAVES) {
             const int j = gi + G * k;
-            const int st = perml[j * 64 + lane];
-            float acc = sell_slice(g.f.arc, lenl[j], offl[j], lane, [&](int src, int pdf, float tp) {
-                return va[src] * tp * xe[pdf];
-            });
+            const int st = F.perm[j * 64 + lane];
+            const float acc = (k < F.kc) ? sell_slice(F.cache, F.len[j], F.coff[k], lane, term)
+                                         : sell_slice(g.f.arc, F.len[j], F.off[j], lane, term);
             float v = (st >= 0) ? (scale ? acc * inv : acc) : 0.0f;
             st_sc1(blk + k * 64 + lane, v);
             part += v;
@@ -737,8 +778,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
         const float as1 = den_gather_psum(X, seq, buf);
         DEN_TP(5);
         float *an = astore + (size_t)(t + 1) * S;
-        den_consume(X, seq, buf, nsl, perml, [&](int st, float v, int owner) {
-            float a = v + as1 * leaky * initl[st];
+        den_consume(X, seq, buf, nsl, F.perm, F.initp, [&](int st, float v, float ip, int owner) {
+            float a = v + as1 * leaky * ip;
             va[st] = a;
             if (owner == gi) __builtin_nontemporal_store(a, an + st);  // keep L2 for the arcs
         });
@@ -776,41 +817,126 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     }
 }
 
-// Backward pass + posteriors (chain_den.cu:632-684), G blocks per sequence. Per
-// frame: beta'[t] over the source rows of this block's slices (exchanged), gamma[t]
-// over this block's pdf rows (summed per pdf in arc order, no atomics), and in the
-// product mode the objective assembly of backward.go:224-371 for those pdfs into
-// the fp16 gradient row. The whole pass always runs; a non-finite objective only
-// zeroes what is written.
-template <typename XT, int MODE>
+// Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per
+// sequence: beta'[t] over the source rows of this block's slices (exchanged),
+// beta[t] = beta'[t] + leaky*<init, beta'[t]>; beta[t] for t >= 1 goes to HBM for
+// k_den_post.
+template <typename XT>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const DenRun r, const DenX X) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int seq, gi;
     den_map(X, seq, gi);
-    const int G = X.G, nsl = g.b.nsl, nslq = g.q.nsl;
+    const int G = X.G, nsl = g.b.nsl;
     float *red = reinterpret_cast<float *>(smem);      // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;    // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;  // [S] alpha'[t]
-    float *vb = va + S;                                // [S] beta[t+1]
+    float *vb = reinterpret_cast<float *>(smem) + 64;  // [S] beta[t+1]
     float *xe = vb + S;                                // [P] exp(clamp(x))
-    float *xr = xe + P;                                // [P] raw x
-    float *numrow = xr + P;                            // [P]
-    int *metab = reinterpret_cast<int *>(numrow + P);  // perm, len, off of g.b
-    int *metaq = metab + nsl * 66;                     // ... of g.q
-    const int *permb = metab, *lenb = metab + nsl * 64, *offb = metab + nsl * 65;
-    const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + P + (P & 1));
+    const int nk = (nsl - gi + G - 1) / G;
 
     const int T = r.frames[seq];
     const long long row0 = r.row0[seq];
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * S;
     const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
+    float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * S;
     const float leaky = r.leaky;
     const float total = r.den_out[seq * 2 + 0];
-    const float den_lp = r.den_out[seq * 2 + 1];
 
-    float *st8 = r.stats + (size_t)seq * 8;
+    const SellLds B = stage_sell(g.b, gi, G, nk, sbase, X.cache_b);
+    const float inv_tot = total > 0.0f ? 1.0f / total : 0.0f;  // BetaDashLastFrame
+    float part = 0.f;
+    for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s] * inv_tot;
+    float tb = leaky * block_sum<DEN_WAVES>(part, red);
+    for (int s = tid; s < S; s += DEN_THREADS) {
+        vb[s] = inv_tot + tb;
+        if (gi == 0) __builtin_nontemporal_store(inv_tot + tb, bstore + (size_t)T * S + s);
+    }
+    RowPre<XT> pre;
+    if (T > 0) {
+        pre.fetch(nnet + (row0 + (long long)(T - 1) * r.stride) * r.ld, P);
+#pragma unroll
+        for (int i = 0; i < DEN_MAXPT; ++i) {
+            int p = tid + i * DEN_THREADS;
+            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+        }
+    }
+    __syncthreads();
+    for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
+        const int buf = t & 1;
+        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        const float at = asum[t];
+        const bool scale = at > 0.0f;
+        const float inv = scale ? 1.0f / at : 1.0f;
+        part = 0.f;
+        auto term = [&](int dst, int pdf, float tp) { return vb[dst] * tp * xe[pdf]; };
+        for (int k = wave; k < nk; k += DEN_WAVES) {  // kernel_den_backward_transitions
+            const int j = gi + G * k;
+            const int st = B.perm[j * 64 + lane];
+            const float acc = (k < B.kc) ? sell_slice(B.cache, B.len[j], B.coff[k], lane, term)
+                                         : sell_slice(g.b.arc, B.len[j], B.off[j], lane, term);
+            float bd = (st >= 0) ? (scale ? acc * inv : acc) : 0.0f;
+            st_sc1(blk + k * 64 + lane, bd);
+            part += B.initp[j * 64 + lane] * bd;
+        }
+        part = wave_sum(part);
+        if (lane == 0) red[wave] = part;
+        den_publish(X, blk + X.spg * 64, red, seq);
+        if (t > 0) pre.fetch(nnet + (row0 + (long long)(t - 1) * r.stride) * r.ld, P);
+        if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
+        tb = leaky * den_gather_psum(X, seq, buf);
+        float *bt = bstore + (size_t)t * S;
+        den_consume(X, seq, buf, nsl, B.perm, B.initp, [&](int st, float v, float, int owner) {
+            const float b = v + tb;
+            vb[st] = b;
+            if (t > 0 && owner == gi) __builtin_nontemporal_store(b, bt + st);
+        });
+        if (t > 0) {
+#pragma unroll
+            for (int i = 0; i < DEN_MAXPT; ++i) {
+                int p = tid + i * DEN_THREADS;
+                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Posteriors (kernel_den_posteriors, chain_den.cu:253-280) for every (sequence,
+// frame) in parallel — gamma[t] needs only the stored alpha'[t] and beta[t+1] — by
+// pdf rows in arc order (no atomics), and in the product mode the objective
+// assembly of backward.go:224-371 into the fp16 gradient row. The whole pass always
+// runs; a non-finite objective only zeroes what is written.
+#define POST_FRAMES 4  // frames per block
+template <typename XT, int MODE>
+__global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const DenRun r, int nfb) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int seq = blockIdx.x / nfb, fb = blockIdx.x % nfb;
+    const int nslq = g.q.nsl;
+    float *red = reinterpret_cast<float *>(smem);      // [32]
+    float *va = reinterpret_cast<float *>(smem) + 64;  // [S] alpha'[t]
+    float *vb = va + S;                                // [S] beta[t+1]
+    float *xe = vb + S;                                // [P]
+    float *xr = xe + P;                                // [P]
+    float *numrow = xr + P;                            // [P]
+    int *metaq = reinterpret_cast<int *>(numrow + P);
+    const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
+    for (int i = tid; i < nslq * 64; i += DEN_THREADS) metaq[i] = g.q.perm[i];
+    for (int i = tid; i < nslq; i += DEN_THREADS) {
+        metaq[nslq * 64 + i] = g.q.len[i];
+        metaq[nslq * 65 + i] = g.q.off[i];
+    }
+
+    const int T = r.frames[seq];
+    const int t0 = fb * POST_FRAMES, t1 = min(T, t0 + POST_FRAMES);
+    if (t0 >= t1) return;
+    const long long row0 = r.row0[seq];
+    const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
+    const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * S;
+    const float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * S;
+    const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
+
     int ok = 1;
     float w = 1.0f;
     const LogFstDev *nf = nullptr;
@@ -820,9 +946,11 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
         NG = nf->G;
         w = r.opts.supervision_weight;
         const float num_lp = *nf->total;
+        const float den_lp = r.den_out[seq * 2 + 1];
         double objf = (double)w * ((double)num_lp - (double)den_lp);
         ok = !(isnan(objf) || isinf(objf));
-        if (gi == 0 && tid == 0) {
+        if (fb == 0 && tid == 0) {
+            float *st8 = r.stats + (size_t)seq * 8;
             st8[0] = num_lp;
             st8[1] = den_lp;
             st8[2] = ok ? (float)objf : (float)(-10.0 * w * T);  // backward.go:356-363
@@ -831,40 +959,25 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
             st8[7] = ok ? 1.0f : 0.0f;
         }
     }
-    stage_sell(g.b, metab);
-    stage_sell(g.q, metaq);
-    const float inv_tot = total > 0.0f ? 1.0f / total : 0.0f;
-    float part = 0.f;
-    for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s] * inv_tot;
-    float tb = leaky * block_sum<DEN_WAVES>(part, red);
-    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = inv_tot + tb;
     for (int p = tid; p < P; p += DEN_THREADS) numrow[p] = 0.0f;
-
     const float l2s = r.opts.supervision_weight * r.opts.l2_regularize;
     const float oscale = 2.0f * r.opts.out_of_range_regularize;
     const bool do_oor = MODE == DEN_PRODUCT && r.opts.out_of_range_regularize > 0.0f;
     const bool do_l2 = MODE == DEN_PRODUCT && r.opts.l2_regularize > 0.0f;
     float oor = 0.f, sq = 0.f;
-    RowPre<XT> pre;
-    StatePre apre;
-    auto fetch = [&](int t) {
-        pre.fetch(nnet + (row0 + (long long)t * r.stride) * r.ld, P);
-        apre.fetch(astore + (size_t)t * S, S);
-    };
-    auto put = [&](int t) {  // same thread <-> element map as the reads in the gradient loop
-#pragma unroll
-        for (int i = 0; i < DEN_MAXPT; ++i) {
-            int p = tid + i * DEN_THREADS;
-            if (p < P) {
-                const float x = pre.get(i);
-                xr[p] = x;
-                xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, x)));
-            }
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+        // stage alpha'[t], beta[t+1], the output row and the numerator posteriors
+        const float *ar = astore + (size_t)t * S, *br = bstore + (size_t)(t + 1) * S;
+        for (int s = tid; s < S; s += DEN_THREADS) {
+            va[s] = __builtin_nontemporal_load(ar + s);
+            vb[s] = __builtin_nontemporal_load(br + s);
         }
-#pragma unroll
-        for (int i = 0; i < DEN_MAXS; ++i) {
-            int s = tid + i * DEN_THREADS;
-            if (s < S) va[s] = apre.v[i];
+        const XT *xrow = nnet + (row0 + (long long)t * r.stride) * r.ld;
+        for (int p = tid; p < P; p += DEN_THREADS) {
+            const float x = (float)xrow[p];
+            xr[p] = x;
+            xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, x)));
         }
         if (MODE == DEN_PRODUCT) {  // the numerator's pdf set is the same every frame
             const float *nps = nf->post_sparse + (size_t)t * NG;
@@ -873,43 +986,19 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
                 if (p > 0 && p <= P) numrow[p - 1] = nps[q];
             }
         }
-    };
-    __syncthreads();  // numrow zeroed before the first scatter
-    if (T > 0) {
-        fetch(T - 1);
-        put(T - 1);
-    }
-    __syncthreads();
-    const int nk = (nsl - gi + G - 1) / G, nkq = (nslq - gi + G - 1) / G;
-    for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
-        const int buf = t & 1;
-        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
         const float at = asum[t];
         const bool scale = at > 0.0f;
         const float inv = scale ? 1.0f / at : 1.0f;
-        part = 0.f;
-        // beta'[t] by source state (kernel_den_backward_transitions)
-        for (int k = wave; k < nk; k += DEN_WAVES) {
-            const int j = gi + G * k;
-            const int st = permb[j * 64 + lane];
-            float acc = sell_slice(g.b.arc, lenb[j], offb[j], lane, [&](int dst, int pdf, float tp) {
-                return vb[dst] * tp * xe[pdf];
-            });
-            float bd = (st >= 0) ? (scale ? acc * inv : acc) : 0.0f;
-            st_sc1(blk + k * 64 + lane, bd);
-            if (st >= 0) part += g.init[st] * bd;
-        }
-        // gamma[t] by pdf (kernel_den_posteriors) and the gradient of those pdfs
+        __syncthreads();
         h16 *orow = (MODE == DEN_PRODUCT) ? r.out_grad + (row0 + (long long)t * r.stride) * r.ldg : nullptr;
         const bool even = (t & 1) == 0;
-        for (int k = wave; k < nkq; k += DEN_WAVES) {
-            const int j = gi + G * k;
+        for (int j = wave; j < nslq; j += DEN_WAVES) {
             const int pdf = permq[j * 64 + lane];
             float acc = sell_slice(g.q.arc, lenq[j], offq[j], lane, [&](int src, int dst, float tp) {
                 return va[src] * tp * vb[dst];
             });
             if (pdf < 0) continue;
-            float gv = acc * xe[pdf];
+            const float gv = acc * xe[pdf];
             const float den = scale ? gv * inv : gv;
             if (MODE == DEN_ABI) {
                 r.post_dense[(size_t)t * P + pdf] = den;
@@ -934,14 +1023,6 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
                 orow[pdf] = ok ? (h16)(-d) : (h16)0.0f;  // loss gradient = -deriv
             }
         }
-        part = wave_sum(part);
-        if (lane == 0) red[wave] = part;
-        den_publish(X, blk + X.spg * 64, red, seq);
-        if (t > 0) fetch(t - 1);
-        if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
-        tb = leaky * den_gather_psum(X, seq, buf);
-        den_consume(X, seq, buf, nsl, permb, [&](int st, float v, int) { vb[st] = v + tb; });
-        if (t > 0) put(t - 1);
         __syncthreads();
     }
     if (MODE == DEN_PRODUCT) {
@@ -949,10 +1030,18 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
         __syncthreads();
         float q = block_sum<DEN_WAVES>(sq, red);
         if (tid == 0) {
+            float *st8 = r.stats + (size_t)seq * 8;
             if (o > 0.0f) atomicAdd(&st8[6], o);
             if (do_l2 && ok) atomicAdd(&st8[3], -0.5f * l2s * q);
         }
     }
+}
+
+// initp[c] = init[perm[c]] (0 for padding rows): the initial probabilities in a
+// SELL table's slice order, so the exchange consumers load them with the payload
+__global__ void k_perm_gather(const int *perm, const float *init, float *out, int n) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < n) out[c] = perm[c] >= 0 ? init[perm[c]] : 0.0f;
 }
 
 // ===========================================================================
@@ -1042,8 +1131,8 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         *why = "num_pdfs > 4096 not supported";
         return nullptr;
     }
-    if (den_lds_bytes(S, P, (S + 63) / 64, (P + 63) / 64) > 160 * 1024 ||
-        den_fwd_lds_bytes(S, P, (S + 63) / 64) > 160 * 1024 || S > DEN_MAXS * DEN_THREADS) {
+    if (den_post_lds_bytes(S, P, (P + 63) / 64) > DEN_LDS_TOTAL ||
+        den_rec_fixed_bytes(S, P, (S + 63) / 64) > DEN_LDS_TOTAL || S > DEN_MAXS * DEN_THREADS) {
         *why = "den graph too large for the LDS-resident kernels (S <= 8192, ~12*S + 14*P B)";
         return nullptr;
     }
@@ -1072,12 +1161,25 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
     put(d.f, sf);
     put(d.b, sb);
     put(d.q, sq);
+    std::vector<float> zf(sf.perm.size(), 0.0f), zb(sb.perm.size(), 0.0f);
+    d.f.initp = dev_upload(zf, t->owned);  // filled by den_tables_set_init
+    d.b.initp = dev_upload(zb, t->owned);
+    ok = ok && d.f.initp && d.b.initp;
     if (!ok) {
         delete t;
         *why = "hipMalloc failed for den tables";
         return nullptr;
     }
     return t;
+}
+
+// (re)derive the slice-ordered initial probabilities from a device init vector
+void den_tables_set_init(const DenDev &d, const float *d_init, hipStream_t st) {
+    const int nf = d.f.nsl * 64, nb = d.b.nsl * 64;
+    hipLaunchKernelGGL(k_perm_gather, dim3((nf + 255) / 256), dim3(256), 0, st, d.f.perm, d_init,
+                       (float *)d.f.initp, nf);
+    hipLaunchKernelGGL(k_perm_gather, dim3((nb + 255) / 256), dim3(256), 0, st, d.b.perm, d_init,
+                       (float *)d.b.initp, nb);
 }
 
 // denominator.go:131-171
@@ -1134,6 +1236,19 @@ struct DenXBuf {
         X.lgG = G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
         X.spg = (g.f.nsl + G - 1) / G;
         X.blk = X.spg * 64 + 64;
+        const size_t fixed_f = den_rec_fixed_bytes(g.S, g.P, g.f.nsl);
+        const size_t fixed_b = den_rec_fixed_bytes(g.S, g.P, g.b.nsl);
+        // resident arc records are opt-in (KF_DEN_CACHE=1): measured on MI355X they do not
+        // shorten the recursion (it is bound by the LDS gathers, not the L2 stream) and the
+        // full-LDS request keeps the numerator kernel off those CUs
+        X.cache_f = X.cache_b = 0;
+        if (const char *e = getenv("KF_DEN_CACHE"))
+            if (atoi(e)) {
+                X.cache_f = fixed_f < DEN_LDS_TOTAL ? (unsigned)(DEN_LDS_TOTAL - fixed_f) : 0u;
+                X.cache_b = fixed_b < DEN_LDS_TOTAL ? (unsigned)(DEN_LDS_TOTAL - fixed_b) : 0u;
+            }
+        X.lds_f = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_f + X.cache_f);
+        X.lds_b = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_b + X.cache_b);
         size_t nb = (size_t)nseq * 2 * G * X.blk * 4;
         size_t nc = (((size_t)nseq + 1) * 4 + 15) / 16 * 16;
         if (nb > buf_cap) {
@@ -1164,7 +1279,7 @@ struct DenXBuf {
 };
 
 void launch_den_fwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb, bool fp32_in) {
-    size_t lds = den_fwd_lds_bytes(g.S, g.P, g.f.nsl);
+    size_t lds = X.lds_f;
     hipStream_t st = kf_stream();
     xb.zero(st);
     dim3 grid(X.nseq * X.G);
@@ -1175,16 +1290,26 @@ void launch_den_fwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb
 }
 void launch_den_bwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb, bool fp32_in,
                     int mode) {
-    size_t lds = den_lds_bytes(g.S, g.P, g.b.nsl, g.q.nsl);
     hipStream_t st = kf_stream();
     xb.zero(st);
     dim3 grid(X.nseq * X.G);
-    if (mode == DEN_PRODUCT)
-        hipLaunchKernelGGL((k_den_bwd<h16, DEN_PRODUCT>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
-    else if (fp32_in)
-        hipLaunchKernelGGL((k_den_bwd<float, DEN_ABI>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+    size_t lds = X.lds_b;
+    if (fp32_in)
+        hipLaunchKernelGGL((k_den_bwd<float>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
     else
-        hipLaunchKernelGGL((k_den_bwd<h16, DEN_ABI>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+        hipLaunchKernelGGL((k_den_bwd<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+}
+void launch_den_post(const DenDev &g, const DenRun &r, const DenX &X, bool fp32_in, int mode) {
+    hipStream_t st = kf_stream();
+    const int nfb = (r.max_frames + POST_FRAMES - 1) / POST_FRAMES;
+    dim3 pgrid(X.nseq * nfb);
+    size_t plds = den_post_lds_bytes(g.S, g.P, g.q.nsl);
+    if (mode == DEN_PRODUCT)
+        hipLaunchKernelGGL((k_den_post<h16, DEN_PRODUCT>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb);
+    else if (fp32_in)
+        hipLaunchKernelGGL((k_den_post<float, DEN_ABI>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb);
+    else
+        hipLaunchKernelGGL((k_den_post<h16, DEN_ABI>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb);
 }
 
 // ---- numerator FST host preparation (reverse CSR + pdf groups) -------------
@@ -1812,8 +1937,9 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     }
     const int S = t->dev.S, P = t->dev.P;
     const size_t TP = (size_t)T * P;
-    DevBuf x, init, as, ast, stats, post, row0, frames, dout;
+    DevBuf x, init, as, bs, ast, stats, post, row0, frames, dout;
     if (!x.alloc(TP * 4) || !init.alloc(S * 4) || !as.alloc((size_t)(T + 1) * S * 4) ||
+        (h_post && !bs.alloc((size_t)(T + 1) * S * 4)) ||
         !ast.alloc((T + 1) * 4) || !stats.alloc(32) || !row0.alloc(8) || !frames.alloc(4) ||
         !dout.alloc(8) ||
         (h_post && !post.alloc(TP * 4))) {
@@ -1828,6 +1954,7 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     hipMemcpyAsync(frames.p, &T, 4, hipMemcpyHostToDevice, st);
     DenDev g = t->dev;
     g.init = (const float *)init.p;
+    den_tables_set_init(g, g.init, st);
     DenRun r{};
     r.nnet = x.p;
     r.ld = P;
@@ -1838,6 +1965,7 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     r.leaky = leaky;
     r.backward = h_post != nullptr;
     r.alpha_store = (float *)as.p;
+    r.beta_store = (float *)bs.p;
     r.asum_store = (float *)ast.p;
     r.stats = (float *)stats.p;
     r.post_dense = (float *)post.p;
@@ -1849,7 +1977,10 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
         return -1e30f;
     }
     launch_den_fwd(g, r, X, xbuf, true);
-    if (h_post) launch_den_bwd(g, r, X, xbuf, true, DEN_ABI);
+    if (h_post) {
+        launch_den_bwd(g, r, X, xbuf, true, DEN_ABI);
+        launch_den_post(g, r, X, true, DEN_ABI);
+    }
     float st8[8] = {0};
     hipMemcpyAsync(st8, stats.p, 32, hipMemcpyDeviceToHost, st);
     if (h_post) hipMemcpyAsync(h_post, post.p, TP * 4, hipMemcpyDeviceToHost, st);
@@ -1902,7 +2033,7 @@ struct KfNumBatch {
 struct KfChain {
     const KfDenGraph *den = nullptr;
     int max_seqs = 0, max_frames = 0;
-    float *alpha_store = nullptr, *asum_store = nullptr, *stats = nullptr;
+    float *alpha_store = nullptr, *beta_store = nullptr, *asum_store = nullptr, *stats = nullptr;
     float *num_ab = nullptr;      // numerator alpha/beta
     size_t num_ab_cap = 0;
     float *num_post = nullptr;    // sparse numerator posteriors
@@ -1929,7 +2060,7 @@ struct KfChain {
         if (ev_in) hipEventDestroy(ev_in);
         if (ev_num) hipEventDestroy(ev_num);
         if (den_out) hipFree(den_out);
-        for (void *p : {(void *)alpha_store, (void *)asum_store, (void *)stats, (void *)num_ab,
+        for (void *p : {(void *)alpha_store, (void *)beta_store, (void *)asum_store, (void *)stats, (void *)num_ab,
                         (void *)num_post, (void *)d_desc, (void *)d_row0, (void *)d_frames,
                         (void *)d_num_total})
             if (p) hipFree(p);
@@ -1966,6 +2097,12 @@ extern "C" KfDenGraph *kf_den_graph_create(int S, int P, int A, const int32_t *s
         return nullptr;
     }
     g->t->dev.init = g->d_init;
+    den_tables_set_init(g->t->dev, g->d_init, kf_stream());
+    if (hipStreamSynchronize(kf_stream()) != hipSuccess) {
+        delete g;
+        kfc_set_error("kf_den_graph_create: initial-probability gather failed");
+        return nullptr;
+    }
     return g;
 }
 
@@ -2032,6 +2169,7 @@ extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max
     c->max_frames = max_frames;
     const int S = den->t->dev.S;
     bool ok = hipMalloc(&c->alpha_store, (size_t)max_seqs * (max_frames + 1) * S * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->beta_store, (size_t)max_seqs * (max_frames + 1) * S * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->asum_store, (size_t)max_seqs * (max_frames + 1) * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->stats, (size_t)max_seqs * 8 * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->d_desc, (size_t)max_seqs * sizeof(LogFstDev)) == hipSuccess;
@@ -2181,6 +2319,7 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
     r.leaky = opts->leaky_hmm_coefficient;
     r.backward = 1;
     r.alpha_store = c->alpha_store;
+    r.beta_store = c->beta_store;
     r.asum_store = c->asum_store;
     r.stats = c->stats;
     r.den_out = c->den_out;
@@ -2201,8 +2340,9 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
         return -1;
     }
     launch_den_fwd(dd, r, X, c->xbuf, false);
-    hipStreamWaitEvent(st, c->ev_num, 0);
     launch_den_bwd(dd, r, X, c->xbuf, false, DEN_PRODUCT);
+    hipStreamWaitEvent(st, c->ev_num, 0);  // the numerator is needed from here on
+    launch_den_post(dd, r, X, false, DEN_PRODUCT);
     kf_prof_stop(pd);
     if (hipGetLastError() != hipSuccess) {
         kfc_set_error("kf_chain_compute: launch failed");
