@@ -92,7 +92,7 @@ def main():
     torch.cuda.set_device(local)
 
     import kfp16
-    from kfp16 import synth
+    from kfp16 import dp, synth
     kfp16.check(kfp16.core.bridge_gpu_init(local), "bridge_gpu_init")
     stream = torch.cuda.current_stream()
     kfp16.set_stream(stream.cuda_stream)
@@ -114,7 +114,7 @@ def main():
     from kfp16 import chain
     den_g = synth.make_den_graph(num_pdfs=P)
     dgraph = chain.DenGraph(den_g)
-    fsts = [synth.make_num_fst(rank * a.egs + e, num_pdfs=P) for e in range(a.egs)]
+    fsts = [synth.make_num_fst(dp.eg_index(rank, a.egs, e), num_pdfs=P) for e in range(a.egs)]
     nbatch = chain.NumBatch(fsts)
     row0, nfr, stride = synth.chain_layout(a.egs, FRAMES_PER_EG)
     objective = chain.Chain(dgraph, max_seqs=a.egs, max_frames=int(nfr.max()))
@@ -126,9 +126,7 @@ def main():
         net.forward(fbuf.data_ptr(), T)
         objective.compute(nbatch, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
         net.backward(gbuf.data_ptr())
-        if world > 1:
-            dist.all_reduce(grad)
-            grad.mul_(1.0 / world)
+        dp.allreduce_mean_(grad, world)   # the one data-path collective (RCCL)
         net.sgd(a.lr, a.momentum)
 
     for _ in range(a.warmup):
@@ -151,10 +149,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kfp16.core.kf_prof_enable(0)
-    if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = dp.max_over_ranks(elapsed, "cuda")
 
     prof, chain_prof = {}, {}
     if not a.no_prof:
@@ -165,10 +160,8 @@ def main():
             chain_prof[name] = kfp16.prof_collect(cls)
         kfp16.core.kf_prof_reset()
     res = objective.result()
-    stats = torch.tensor([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
-                         dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(stats)
+    stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
+                              "cuda")
 
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
