@@ -451,8 +451,8 @@ struct DenRun {
     int backward;           // 0: forward only
     float *den_out;         // [nseq][2] {total_prob, log-prob} from k_den_fwd
     unsigned long long *trace;  // optional phase timestamps (kf_chain_trace), null = off
-    float *alpha_store;     // [nseq][(max_frames+1) x S]
-    float *beta_store;      // [nseq][(max_frames+1) x S]
+    float *alpha_store;     // [nseq][max_frames+1][nsl_f*64], forward-table slice order
+    float *beta_store;      // [nseq][max_frames+1][nsl_b*64], backward-table slice order
     float *asum_store;      // [nseq][max_frames+1]
     float *stats;           // [nseq][8]
     // ABI mode
@@ -629,7 +629,7 @@ __device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, int
         const int c = tid + m * DEN_THREADS;
         if (c < n) {
             const int st = perm[c];
-            if (st >= 0) f(st, v[m], initp[c], (c >> 6) & (X.G - 1));
+            if (st >= 0) f(st, v[m], initp[c], (c >> 6) & (X.G - 1), c);
         }
     }
 }
@@ -718,7 +718,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     const int T = r.frames[seq];
     const long long row0 = r.row0[seq];
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * S;
+    const int rs = nsl * 64;  // stored rows are in slice order: contiguous, whole lines
+    float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rs;
     float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
     const float leaky = r.leaky;
 
@@ -726,11 +727,10 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
     float as = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
-    for (int s = tid; s < S; s += DEN_THREADS) {
-        float v = g.init[s] + as * leaky * g.init[s];
-        va[s] = v;
-        if (gi == 0) astore[s] = v;
-    }
+    for (int s = tid; s < S; s += DEN_THREADS) va[s] = g.init[s] + as * leaky * g.init[s];
+    if (gi == 0)
+        for (int c = tid; c < rs; c += DEN_THREADS)
+            __builtin_nontemporal_store(F.initp[c] + as * leaky * F.initp[c], astore + c);
     if (gi == 0 && tid == 0) {
         asum[0] = as;
         r.stats[(size_t)seq * 8 + 3] = 0.0f;  // accumulated by k_den_bwd
@@ -777,11 +777,11 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
         DEN_TP(4);
         const float as1 = den_gather_psum(X, seq, buf);
         DEN_TP(5);
-        float *an = astore + (size_t)(t + 1) * S;
-        den_consume(X, seq, buf, nsl, F.perm, F.initp, [&](int st, float v, float ip, int owner) {
+        float *an = astore + (size_t)(t + 1) * rs;
+        den_consume(X, seq, buf, nsl, F.perm, F.initp, [&](int st, float v, float ip, int owner, int c) {
             float a = v + as1 * leaky * ip;
             va[st] = a;
-            if (owner == gi) __builtin_nontemporal_store(a, an + st);  // keep L2 for the arcs
+            if (owner == gi) __builtin_nontemporal_store(a, an + c);  // keep L2 for the arcs
         });
         DEN_TP(6);
         if (t + 1 < T) {
@@ -839,7 +839,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
     const long long row0 = r.row0[seq];
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
-    float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * S;
+    const int rs = nsl * 64;
+    float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rs;
     const float leaky = r.leaky;
     const float total = r.den_out[seq * 2 + 0];
 
@@ -848,10 +849,10 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s] * inv_tot;
     float tb = leaky * block_sum<DEN_WAVES>(part, red);
-    for (int s = tid; s < S; s += DEN_THREADS) {
-        vb[s] = inv_tot + tb;
-        if (gi == 0) __builtin_nontemporal_store(inv_tot + tb, bstore + (size_t)T * S + s);
-    }
+    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = inv_tot + tb;
+    if (gi == 0)
+        for (int c = tid; c < rs; c += DEN_THREADS)
+            __builtin_nontemporal_store(inv_tot + tb, bstore + (size_t)T * rs + c);
     RowPre<XT> pre;
     if (T > 0) {
         pre.fetch(nnet + (row0 + (long long)(T - 1) * r.stride) * r.ld, P);
@@ -885,11 +886,11 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
         if (t > 0) pre.fetch(nnet + (row0 + (long long)(t - 1) * r.stride) * r.ld, P);
         if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
         tb = leaky * den_gather_psum(X, seq, buf);
-        float *bt = bstore + (size_t)t * S;
-        den_consume(X, seq, buf, nsl, B.perm, B.initp, [&](int st, float v, float, int owner) {
+        float *bt = bstore + (size_t)t * rs;
+        den_consume(X, seq, buf, nsl, B.perm, B.initp, [&](int st, float v, float, int owner, int c) {
             const float b = v + tb;
             vb[st] = b;
-            if (t > 0 && owner == gi) __builtin_nontemporal_store(b, bt + st);
+            if (t > 0 && owner == gi) __builtin_nontemporal_store(b, bt + c);
         });
         if (t > 0) {
 #pragma unroll
@@ -933,8 +934,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     if (t0 >= t1) return;
     const long long row0 = r.row0[seq];
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * S;
-    const float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * S;
+    const int rsf = g.f.nsl * 64, rsb = g.b.nsl * 64;  // slice-ordered rows (k_den_fwd / k_den_bwd)
+    const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rsf;
+    const float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rsb;
     const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
 
     int ok = 1;
@@ -968,10 +970,16 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
         // stage alpha'[t], beta[t+1], the output row and the numerator posteriors
-        const float *ar = astore + (size_t)t * S, *br = bstore + (size_t)(t + 1) * S;
-        for (int s = tid; s < S; s += DEN_THREADS) {
-            va[s] = __builtin_nontemporal_load(ar + s);
-            vb[s] = __builtin_nontemporal_load(br + s);
+        const float *ar = astore + (size_t)t * rsf, *br = bstore + (size_t)(t + 1) * rsb;
+        for (int c = tid; c < rsf; c += DEN_THREADS) {
+            const int st = g.f.perm[c];
+            const float v = __builtin_nontemporal_load(ar + c);
+            if (st >= 0) va[st] = v;
+        }
+        for (int c = tid; c < rsb; c += DEN_THREADS) {
+            const int st = g.b.perm[c];
+            const float v = __builtin_nontemporal_load(br + c);
+            if (st >= 0) vb[st] = v;
         }
         const XT *xrow = nnet + (row0 + (long long)t * r.stride) * r.ld;
         for (int p = tid; p < P; p += DEN_THREADS) {
@@ -1057,7 +1065,7 @@ struct Sell {
 // rows = key states; each row lists (other | pdf<<16, tp) in arc order
 // rows = values of key[] in [0, nrows); each row lists {f1 | f2<<16, tp} in arc order
 Sell build_sell(int nrows, int A, const int32_t *key, const int32_t *f1, const int32_t *f2,
-                const float *tp) {
+                const float *tp, int n1, int n2) {
     Sell s;
     std::vector<int> deg(nrows, 0);
     for (int a = 0; a < A; ++a) deg[key[a]]++;
@@ -1086,15 +1094,62 @@ Sell build_sell(int nrows, int A, const int32_t *key, const int32_t *f1, const i
         tot += mx;
     }
     s.arcs.assign((size_t)tot * 64, make_uint2(0u, 0u));  // tp = 0 padding
-    std::vector<int> fill(nrows, 0);
-    for (int a = 0; a < A; ++a) {
-        int r = rowpos[key[a]];
-        int j = r / 64, l = r % 64;
-        int k = fill[key[a]]++;
-        uint32_t tpu;
-        memcpy(&tpu, &tp[a], 4);
-        s.arcs[((size_t)s.off[j] + k) * 64 + l] =
-            make_uint2((uint32_t)f1[a] | ((uint32_t)f2[a] << 16), tpu);
+    // arcs of every row, in arc order
+    std::vector<std::vector<int>> rows(nrows);
+    for (int a = 0; a < A; ++a) rows[key[a]].push_back(a);
+    // Place each row's arcs into the slice's steps so that, per step and per
+    // 32-lane half-wave, the two LDS gathers (f1 and f2 indices) fall in distinct
+    // banks ((index) mod 32 for ds_read_b32) as far as possible; padding records
+    // (tp = 0) take indices of free banks. Summation order per row changes, but
+    // stays fixed. KF_SELL_PLAIN=1 keeps plain arc order.
+    const bool plain = getenv("KF_SELL_PLAIN") && atoi(getenv("KF_SELL_PLAIN"));
+    for (int j = 0; j < nsl; ++j) {
+        for (int half = 0; half < 2; ++half) {
+            std::vector<std::vector<int>> rem(32);
+            for (int l = 0; l < 32; ++l) {
+                int r = j * 64 + half * 32 + l;
+                if (r < nrows) rem[l] = rows[s.perm[r]];
+            }
+            for (int k = 0; k < s.len[j]; ++k) {
+                bool used1[32] = {false}, used2[32] = {false};
+                // rows with the most remaining arcs choose first
+                int order[32];
+                for (int l = 0; l < 32; ++l) order[l] = l;
+                std::stable_sort(order, order + 32,
+                                 [&](int x, int y) { return rem[x].size() > rem[y].size(); });
+                for (int oi = 0; oi < 32; ++oi) {
+                    const int l = order[oi];
+                    uint2 rec = make_uint2(0u, 0u);
+                    if (!rem[l].empty()) {
+                        size_t best = 0;
+                        int bestc = 3;
+                        if (!plain)
+                            for (size_t q = 0; q < rem[l].size() && bestc > 0; ++q) {
+                                const int a = rem[l][q];
+                                int c = (used1[f1[a] & 31] ? 1 : 0) + (used2[f2[a] & 31] ? 1 : 0);
+                                if (c < bestc) {
+                                    bestc = c;
+                                    best = q;
+                                }
+                            }
+                        const int a = rem[l][best];
+                        rem[l].erase(rem[l].begin() + best);
+                        used1[f1[a] & 31] = used2[f2[a] & 31] = true;
+                        uint32_t tpu;
+                        memcpy(&tpu, &tp[a], 4);
+                        rec = make_uint2((uint32_t)f1[a] | ((uint32_t)f2[a] << 16), tpu);
+                    } else if (!plain) {  // padding: valid indices on free banks
+                        const int m1 = std::min(32, n1) - 1, m2 = std::min(32, n2) - 1;
+                        int b1 = 0, b2 = 0;
+                        while (b1 < m1 && used1[b1]) ++b1;
+                        while (b2 < m2 && used2[b2]) ++b2;
+                        used1[b1] = used2[b2] = true;
+                        rec = make_uint2((uint32_t)b1 | ((uint32_t)b2 << 16), 0u);
+                    }
+                    s.arcs[((size_t)s.off[j] + k) * 64 + half * 32 + l] = rec;
+                }
+            }
+        }
     }
     return s;
 }
@@ -1142,9 +1197,9 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
             *why = "den transition out of range (state, pdf or negative probability)";
             return nullptr;
         }
-    Sell sf = build_sell(S, A, dst, src, pdf0, tp);
-    Sell sb = build_sell(S, A, src, dst, pdf0, tp);
-    Sell sq = build_sell(P, A, pdf0, src, dst, tp);
+    Sell sf = build_sell(S, A, dst, src, pdf0, tp, S, P);
+    Sell sb = build_sell(S, A, src, dst, pdf0, tp, S, P);
+    Sell sq = build_sell(P, A, pdf0, src, dst, tp, S, S);
     auto *t = new DenTables();
     DenDev &d = t->dev;
     d.S = S;
@@ -1938,8 +1993,9 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     const int S = t->dev.S, P = t->dev.P;
     const size_t TP = (size_t)T * P;
     DevBuf x, init, as, bs, ast, stats, post, row0, frames, dout;
-    if (!x.alloc(TP * 4) || !init.alloc(S * 4) || !as.alloc((size_t)(T + 1) * S * 4) ||
-        (h_post && !bs.alloc((size_t)(T + 1) * S * 4)) ||
+    const size_t rs = (size_t)t->dev.f.nsl * 64;  // slice-ordered rows
+    if (!x.alloc(TP * 4) || !init.alloc(S * 4) || !as.alloc((size_t)(T + 1) * rs * 4) ||
+        (h_post && !bs.alloc((size_t)(T + 1) * rs * 4)) ||
         !ast.alloc((T + 1) * 4) || !stats.alloc(32) || !row0.alloc(8) || !frames.alloc(4) ||
         !dout.alloc(8) ||
         (h_post && !post.alloc(TP * 4))) {
@@ -2168,8 +2224,9 @@ extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max
     c->max_seqs = max_seqs;
     c->max_frames = max_frames;
     const int S = den->t->dev.S;
-    bool ok = hipMalloc(&c->alpha_store, (size_t)max_seqs * (max_frames + 1) * S * 4) == hipSuccess;
-    ok = ok && hipMalloc(&c->beta_store, (size_t)max_seqs * (max_frames + 1) * S * 4) == hipSuccess;
+    const size_t rs = (size_t)den->t->dev.f.nsl * 64;  // slice-ordered state rows
+    bool ok = hipMalloc(&c->alpha_store, (size_t)max_seqs * (max_frames + 1) * rs * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->beta_store, (size_t)max_seqs * (max_frames + 1) * rs * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->asum_store, (size_t)max_seqs * (max_frames + 1) * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->stats, (size_t)max_seqs * 8 * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->d_desc, (size_t)max_seqs * sizeof(LogFstDev)) == hipSuccess;

@@ -15,7 +15,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIBDIR = os.path.normpath(os.path.join(_HERE, "..", "..", "lib"))
+# KFP16_LIBDIR: load another in-tree build (A/B timing of kernel variants)
+LIBDIR = os.environ.get("KFP16_LIBDIR") or os.path.normpath(os.path.join(_HERE, "..", "..", "lib"))
 INCDIR = os.path.normpath(os.path.join(_HERE, "..", "..", "..", "include"))
 
 
