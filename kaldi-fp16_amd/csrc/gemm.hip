@@ -155,9 +155,10 @@ __device__ __forceinline__ unsigned op_boff(const OpD &d, int t, int h, int kk, 
     return off < 0 ? BAD : (unsigned)(off * 2);
 }
 
-template <bool KC, int TR, int MODE>
+template <bool KC, int TR, int MODE, int NW>
 struct Stager {
-    static constexpr int NC = TR / 32;  // 1 KiB pieces (= chunks) per thread, 4 waves
+    static constexpr int NC = TR / (8 * NW);  // 1 KiB pieces (= chunks) per thread
+    static_assert(NC * 8 * NW == TR, "tile rows must split evenly over the waves");
     unsigned o0[NC];                    // KC: part-0 row byte offset; MN: fixed byte offset base
     unsigned o1[MODE == OP_P2 && KC ? NC : 1];  // KC/P2: part-1 row byte offset
     int th[MODE == OP_GEN ? NC : 1];    // GEN: KC packed (t<<8)|h ; MN packed part info
@@ -377,20 +378,21 @@ struct SmemSize {
 };
 
 template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE>
-__global__ __launch_bounds__(256, 1) void gemm_kernel(int M, int N, int K, OpD A, OpD B,
-                                                      KfEpilogue E, WgradArgs G, int n_mtiles,
-                                                      int n_ntiles) {
-    static_assert(WM * WN == 4, "4 waves");
+__global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int K, OpD A, OpD B,
+                                                               KfEpilogue E, WgradArgs G,
+                                                               int n_mtiles, int n_ntiles) {
+    constexpr int NW = WM * WN, NTH = 64 * NW;
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     static_assert(TM * 16 == WTM && TN * 16 == WTN, "wave tile multiple of 16");
     constexpr int A_STAGE = BM * BK * 2, B_STAGE = BN * BK * 2;
     constexpr int STAGE = A_STAGE + B_STAGE;
-    using SA = Stager<AKC, BM, AM>;
-    using SB = Stager<BKC, BN, BMODE>;
+    using SA = Stager<AKC, BM, AM, NW>;
+    using SB = Stager<BKC, BN, BMODE, NW>;
     constexpr int LPT = SA::NC + SB::NC;  // LDS-DMA instructions per thread per stage
-    static_assert(ST == 2 || ST == 3, "stages");
-    static_assert(4 * BN * 4 + (32 * (WTN + 4) * 4) * 4 <= SmemSize<BM, BN, ST>::bytes,
+    static_assert(ST >= 2 && ST <= 4, "stages");
+    static_assert(4 * BN * 4 + (32 * (WTN + 4) * 4) * NW <= SmemSize<BM, BN, ST>::bytes,
                   "epilogue staging");
 
     __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, ST>::bytes];
@@ -435,10 +437,15 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(int M, int N, int K, OpD A
     const bool do_bsum = WGRAD && G.bias_slab != nullptr && mt == 0 && !BKC;
     float bsum = 0.f;
 
+    // ST-stage LDS ring: stages kt .. kt+ST-2 are in flight while kt is consumed;
+    // the counted wait retires only stage kt (never vmcnt(0) in steady state)
+    // (plain statements: a lambda around `issue` makes the stager's offset arrays
+    // address-taken and sends them to scratch)
     if (nk > 0) issue(0, kbeg);
-    if (ST == 3 && nk > 1) issue(1, kbeg + BK);
+    if (ST >= 3 && nk > 1) issue(1, kbeg + BK);
+    if (ST >= 4 && nk > 2) issue(2, kbeg + 2 * BK);
     for (int kt = 0; kt < nk; ++kt) {
-        if (ST == 3 && kt + 1 < nk) wait_vmcnt<LPT>();
+        if (kt + ST - 2 < nk) wait_vmcnt<LPT * (ST - 2)>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -487,7 +494,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(int M, int N, int K, OpD A
         wait_vmcnt<0>();
         __syncthreads();
         float *prm = reinterpret_cast<float *>(smem);
-        for (int c = tid; c < BN; c += 256) {
+        for (int c = tid; c < BN; c += NTH) {
             const int n = n0 + c;
             const bool in = n < N;
             prm[c] = (E.bias && in) ? (float)((const h16 *)E.bias)[n] : 0.f;
@@ -743,7 +750,7 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
         hipEventRecord(rec.a, kf_stream());
     }
     gemm_kernel<BM, BN, WM, WN, AKC, BKC, WGRAD, ST, AM, BMODE>
-        <<<grid, 256, 0, kf_stream()>>>(M, N, K, A, B, E, G, mt, nt);
+        <<<grid, 64 * WM * WN, 0, kf_stream()>>>(M, N, K, A, B, E, G, mt, nt);
     if (g_prof) {
         hipEventRecord(rec.b, kf_stream());
         g_prof_recs.push_back(rec);
@@ -754,6 +761,11 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
         return -1;
     }
     return 0;
+}
+
+static int gemm_big() {
+    const char *e = getenv("KF_GEMM_BIG");
+    return e ? atoi(e) : 1;
 }
 
 extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
@@ -778,9 +790,13 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
     }
     WgradArgs G{nullptr, nullptr, 0};
     const int am = op_mode(a), bm = op_mode(b);
-    const int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : 0);
+    // 8-wave 256-row tiles halve the staged bytes per MFMA flop against the 4-wave
+    // 128-row ones; KF_GEMM_BIG=0 selects the 4-wave family for A/B.
+    static const int big = gemm_big();
+    const int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : (big && N >= 256 ? 3 : 0));
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
+        if (tile == 3) return launch<256, 256, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 1) return launch<128, 160, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 2) return launch<256, 64, 4, 1, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);  \
         return launch<128, 128, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);               \
@@ -809,8 +825,10 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         return -1;
     }
     if (!mn_gen_ok(a, "A") || !mn_gen_ok(b, "B")) return -1;
+    static const int wbig = getenv("KF_GEMM_WBIG") ? atoi(getenv("KF_GEMM_WBIG")) : 1;
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
     if (BNc == 64) BMc = 256;
+    if (wbig && BNc == 128) BMc = 256, BNc = 256;
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
     int splits = (512 + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
@@ -832,7 +850,17 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     KfEpilogue E{};
     const int am = op_mode(a), bm = op_mode(b);
     int rc;
-#define KF_WG(AM_, BM_)                                                                                do {                                                                                                   if (BNc == 160) rc = launch<128, 160, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits);         else if (BNc == 64) rc = launch<256, 64, 4, 1, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits);         else rc = launch<128, 128, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits);     } while (0)
+#define KF_WG(AM_, BM_)                                                                          \
+    do {                                                                                         \
+        if (BMc == 256 && BNc == 256)                                                            \
+            rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BNc == 160)                                                                     \
+            rc = launch<128, 160, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BNc == 64)                                                                      \
+            rc = launch<256, 64, 4, 1, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else                                                                                     \
+            rc = launch<128, 128, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+    } while (0)
     if (bm == OP_SIMPLE && am == OP_SIMPLE) KF_WG(OP_SIMPLE, OP_SIMPLE);
     else if (bm == OP_SIMPLE && am == OP_P2) KF_WG(OP_P2, OP_SIMPLE);
     else if (bm == OP_SIMPLE) KF_WG(OP_GEN, OP_SIMPLE);
