@@ -30,6 +30,12 @@ KF_DECLARE_ERR(kf)
 
 extern "C" const char *kf_last_error(void) { return kf_err_.get(); }
 extern "C" void kf_clear_error(void) { kf_err_.clear(); }
+void kf_report_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    kf_err_.set(fmt, ap);
+    va_end(ap);
+}
 
 // ---------------------------------------------------------------------------
 // operand addressing (device form of KfOperand, see kf_ops.h)

@@ -38,6 +38,9 @@ struct KfErr {
 // current stream (kf_ops.h: kf_set_stream)
 hipStream_t kf_stream();
 
+// sets the kf_last_error() text from another module (gemm.hip owns the slot)
+void kf_report_error(const char *fmt, ...);
+
 // kf_prof_* timing of a launch bracket on the current stream (gemm.hip);
 // classes: 0 fused GEMM, 1 wgrad GEMM, 2 chain numerator, 3 chain denominator
 enum { KF_PROF_CHAIN_NUM = 2, KF_PROF_CHAIN_DEN = 3 };
