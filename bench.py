@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "kaldi-fp16_amd", "python"))
 import numpy as np  # noqa: E402
 
 METRIC = "frames/sec CNN-TDNN fwd+bwd, 40-dim×1500-frame egs, 1/2/4/8 MI355X"
+METRIC_FWD = "frames/sec CNN-TDNN forward only, 40-dim×1500-frame egs, 1 MI355X"
 PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16 MFMA (MI355X_MICROARCH.md)
 FRAMES_PER_EG = 1500
 
@@ -48,7 +49,25 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=1500)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-prof", action="store_true")
+    p.add_argument("--mode", choices=("train", "forward"), default="train",
+                   help="train: the metric's fwd+bwd+SGD step; forward: configs[1], forward only")
     return p.parse_args()
+
+
+def pmc_traffic(kernel_class):
+    """HBM bytes per launch of a kernel class from the newest committed rocprofv3
+    PMC summary (profiles/r*_pmc_traffic.json, scripts/pmc_traffic.sh), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as fh:
+            rec = json.load(fh).get(kernel_class)
+        return None if rec is None else {"bytes_per_launch": round(rec["hbm_bytes_per_launch"]),
+                                         "source": os.path.relpath(files[-1], ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
@@ -124,6 +143,8 @@ def main():
 
     def step():
         net.forward(fbuf.data_ptr(), T)
+        if a.mode == "forward":
+            return
         objective.compute(nbatch, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
         net.backward(gbuf.data_ptr())
         dp.allreduce_mean_(grad, world)   # the one data-path collective (RCCL)
@@ -159,27 +180,33 @@ def main():
         for cls, name in ((2, "chain_num"), (3, "chain_den")):
             chain_prof[name] = kfp16.prof_collect(cls)
         kfp16.core.kf_prof_reset()
-    res = objective.result()
-    stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
-                              "cuda")
+    stats = [0.0] * 5
+    if a.mode == "train":
+        res = objective.result()
+        stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
+                                  "cuda")
 
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
         frames = T * world * a.steps
         value = frames / elapsed
+        fwd_only = a.mode == "forward"
+        workload = ("cnn_tdnn_17f forward only (configs[1])" if fwd_only else
+                    "cnn_tdnn_17f train step (fwd+bwd+SGD)") + f", {a.egs} egs x 1500 frames per GPU"
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
+            "metric": METRIC_FWD if fwd_only else METRIC, "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
             "data": "synthetic",
-            "config": {"workload": "cnn_tdnn_17f train step (fwd+bwd+SGD), 64 egs x 1500 frames per GPU",
+            "config": {"workload": workload,
                        "xconfig": a.xconfig, "egs_per_gpu": a.egs, "frames_per_eg": FRAMES_PER_EG,
                        "global_batch_egs": a.egs * world, "parallelism": f"dp{world}",
                        "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)"},
-            "objf_per_frame": round(float(stats[0]) / max(float(stats[3]), 1.0), 5),
-            "objective_finite_seqs": f"{int(stats[4])}/{a.egs * world}",
         }
-        if chain_prof:
+        if not fwd_only:
+            out["objf_per_frame"] = round(float(stats[0]) / max(float(stats[3]), 1.0), 5)
+            out["objective_finite_seqs"] = f"{int(stats[4])}/{a.egs * world}"
+        if chain_prof and not fwd_only:
             (nn, nms, _), (dn, dms, dbytes) = chain_prof["chain_num"], chain_prof["chain_den"]
             out["chain"] = {"num_ms_per_step": round(nms / a.steps, 3),
                             "den_ms_per_step": round(dms / a.steps, 3),
@@ -190,11 +217,12 @@ def main():
             n, ms, fl = prof[dom]
             ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
             out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP16_TFLOPS,
-                               "unit": "TFLOP/s", "frac": round(ach / PEAK_FP16_TFLOPS, 4), "traffic": None,
+                               "unit": "TFLOP/s", "frac": round(ach / PEAK_FP16_TFLOPS, 4),
+                               "traffic": pmc_traffic(dom),
                                "kernel": dom, "launches": n, "kernel_ms_per_step": round(ms / a.steps, 3),
                                "all_gemm_tflops": round(sum(v[2] for v in prof.values()) /
                                                         (sum(v[1] for v in prof.values()) * 1e-3) / 1e12, 2)}
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and not fwd_only:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
             den = (den_g, oracle.den_initial_probs(den_g))

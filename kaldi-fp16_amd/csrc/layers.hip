@@ -53,29 +53,39 @@ struct ConvC1 {
     int dt[9], dh[9];
 };
 
-__global__ void k_conv_c1_fwd(ConvC1 c, const h16 *x, const h16 *W, const h16 *bias,
-                              const float *scale, const float *shift, h16 *y, uint8_t *mask) {
-    __shared__ float sw[9 * 256];
-    __shared__ float sb[256];
-    for (int i = threadIdx.x; i < c.noff * c.fout; i += blockDim.x) sw[i] = h2f(W[i]);
-    for (int i = threadIdx.x; i < c.fout; i += blockDim.x) sb[i] = bias ? h2f(bias[i]) : 0.f;
-    __syncthreads();
+__global__ __launch_bounds__(256) void k_conv_c1_fwd(ConvC1 c, const h16 *x, const h16 *W,
+                                                     const h16 *bias, const float *scale,
+                                                     const float *shift, h16 *y, uint8_t *mask) {
+    // the grid stride is a multiple of `groups`, so each thread keeps one filter
+    // group for its whole loop: its 9x8 weights live in registers
     const int groups = c.fout / 8;
-    const long long total = (long long)c.T * c.hout * groups;
-    for (long long it = (long long)blockIdx.x * blockDim.x + threadIdx.x; it < total;
-         it += (long long)gridDim.x * blockDim.x) {
-        const long long row = it / groups;
-        const int g = (int)(it - row * groups);
-        const int t = (int)(row / c.hout), h = (int)(row - (long long)t * c.hout);
+    const int first = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = first % groups;
+    float w[9][8], b[8], sc[8], sf[8];
+#pragma unroll
+    for (int o = 0; o < 9; ++o)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[o][e] = o < c.noff ? h2f(W[o * c.fout + 8 * g + e]) : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        b[e] = bias ? h2f(bias[8 * g + e]) : 0.f;
+        sc[e] = scale ? scale[8 * g + e] : 1.f;
+        sf[e] = scale ? shift[8 * g + e] : 0.f;
+    }
+    const int total = c.T * c.hout * groups;  // < 2^31, checked on the host
+    for (int it = first; it < total; it += gridDim.x * blockDim.x) {
+        const int row = it / groups;
+        const int t = row / c.hout, h = row - t * c.hout;
         float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = sb[8 * g + e];
-        for (int o = 0; o < c.noff; ++o) {
-            const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
-            if (ts < 0 || ts >= c.T || hs < 0 || hs >= c.hin) continue;
-            const float xv = h2f(x[(long long)ts * c.hin + hs]);
+        for (int e = 0; e < 8; ++e) v[e] = b[e];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += xv * sw[o * c.fout + 8 * g + e];
+        for (int o = 0; o < 9; ++o) {
+            const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
+            const bool ok = o < c.noff && ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin;
+            const float xv = ok ? h2f(x[ok ? ts * c.hin + hs : 0]) : 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaf(xv, w[o][e], v[e]);
         }
         unsigned bits = 0;
         half8 out;
@@ -84,10 +94,10 @@ __global__ void k_conv_c1_fwd(ConvC1 c, const h16 *x, const h16 *W, const h16 *b
             float a = v[e];
             if (a > 0.f) bits |= 1u << e;
             else a = 0.f;
-            if (scale) a = fmaf(a, scale[8 * g + e], shift[8 * g + e]);
+            if (scale) a = fmaf(a, sc[e], sf[e]);
             out[e] = f2h(a);
         }
-        const long long idx = row * c.fout + 8 * g;
+        const long long idx = (long long)row * c.fout + 8 * g;
         store_h8(y + idx, out);
         if (mask) mask[idx >> 3] = (uint8_t)bits;
     }
@@ -103,33 +113,31 @@ __global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, const h16 *x, c
     extern __shared__ __attribute__((aligned(16))) float red[];  // [256][10*8]
     const int fg = c.fout / 8;                 // threads per row
     const int lane_f = threadIdx.x % fg, rg = threadIdx.x / fg, nrg = blockDim.x / fg;
-    const long long rows = (long long)c.T * c.hout;
-    const long long r0 = (long long)blockIdx.x * rows_per_block;
-    const long long r1 = min(rows, r0 + rows_per_block);
+    const int rows = c.T * c.hout;             // < 2^31, checked on the host
+    const int r0 = blockIdx.x * rows_per_block;
+    const int r1 = min(rows, r0 + rows_per_block);
     float acc[10][8];
 #pragma unroll
     for (int o = 0; o < 10; ++o)
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[o][e] = 0.f;
-    for (long long rb = r0 + rg; rb < r1; rb += (long long)nrg * C1_UNROLL) {
+    for (int rb = r0 + rg; rb < r1; rb += nrg * C1_UNROLL) {
         half8 g[C1_UNROLL];
         float xv[C1_UNROLL][9];
 #pragma unroll
         for (int u = 0; u < C1_UNROLL; ++u) {
-            const long long r = rb + (long long)u * nrg;
-            g[u] = half8{};
+            const int r = rb + u * nrg;
+            const bool live = r < r1;
+            const int rr = live ? r : r0;  // clamped: every load is issued, dead rows add zero
+            g[u] = load_h8(dz + (long long)rr * c.fout + 8 * lane_f);
+            if (!live) g[u] = half8{};
+            const int t = rr / c.hout, h = rr - t * c.hout;
 #pragma unroll
-            for (int o = 0; o < 9; ++o) xv[u][o] = 0.f;
-            if (r < r1) {
-                g[u] = load_h8(dz + r * c.fout + 8 * lane_f);
-                const int t = (int)(r / c.hout), h = (int)(r - (long long)t * c.hout);
-#pragma unroll
-                for (int o = 0; o < 9; ++o) {
-                    if (o >= c.noff) break;
-                    const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
-                    if (ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin)
-                        xv[u][o] = h2f(x[(long long)ts * c.hin + hs]);
-                }
+            for (int o = 0; o < 9; ++o) {
+                const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
+                const bool ok = o < c.noff && ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin;
+                const float v = h2f(x[ok ? ts * c.hin + hs : 0]);
+                xv[u][o] = ok ? v : 0.f;
             }
         }
 #pragma unroll
@@ -160,14 +168,24 @@ __global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, const h16 *x, c
     }
 }
 
+// one 256-thread block per output: thread j sums slabs j, j+256, ... then a
+// fixed-order tree over the block (deterministic)
 __global__ void k_conv_c1_reduce(const float *slab, int nblk, int n, float *dW, float *db,
                                  int wcount) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    __shared__ float sh[256];
+    const int i = blockIdx.x;
     float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += slab[(long long)b * n + i];
-    if (i < wcount) dW[i] = s;
-    else if (db) db[i - wcount] = s;
+    for (int b = threadIdx.x; b < nblk; b += blockDim.x) s += slab[(long long)b * n + i];
+    sh[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (i < wcount) dW[i] = sh[0];
+        else if (db) db[i - wcount] = sh[0];
+    }
 }
 
 // flat SGD with momentum and fp32 master weights; fp32 gradient
@@ -241,8 +259,10 @@ int kf_bn_apply(const void *x, void *y, long long rows, int D, const float *scal
 int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
                        const int *dh, const void *x, const void *W, const void *bias,
                        const float *scale, const float *shift, void *y, uint8_t *mask) {
-    if (noff > 9 || fout % 8 || fout > 256) {
-        lay_set_error("conv_c1_forward: noff=%d fout=%d unsupported", noff, fout);
+    if (noff > 9 || fout % 8 || fout > 256 || 256 % (fout / 8) ||
+        (long long)T * hout * fout >= (1LL << 31)) {
+        lay_set_error("conv_c1_forward: noff=%d fout=%d T*hout=%lld unsupported", noff, fout,
+                      (long long)T * hout);
         return -1;
     }
     ConvC1 c{T, hin, hout, sub, fout, noff, {0}, {0}};
@@ -258,8 +278,10 @@ int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, co
 
 int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
                      const int *dh, const void *x, const void *dz, float *dW, float *db) {
-    if (noff > 9 || fout % 8 || fout > 256 || 256 % (fout / 8)) {
-        lay_set_error("conv_c1_wgrad: noff=%d fout=%d unsupported", noff, fout);
+    if (noff > 9 || fout % 8 || fout > 256 || 256 % (fout / 8) ||
+        (long long)T * hout * fout >= (1LL << 31)) {
+        lay_set_error("conv_c1_wgrad: noff=%d fout=%d T*hout=%lld unsupported", noff, fout,
+                      (long long)T * hout);
         return -1;
     }
     ConvC1 c{T, hin, hout, sub, fout, noff, {0}, {0}};
@@ -280,7 +302,7 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
     }
     k_conv_c1_wgrad<<<nblk, 256, 256 * 80 * 4, kf_stream()>>>(c, (const h16 *)x, (const h16 *)dz,
                                                               slab, rpb);
-    k_conv_c1_reduce<<<(n + 255) / 256, 256, 0, kf_stream()>>>(slab, nblk, n, dW, db, noff * fout);
+    k_conv_c1_reduce<<<n, 256, 0, kf_stream()>>>(slab, nblk, n, dW, db, noff * fout);
     return lay_check("conv_c1_wgrad");
 }
 
