@@ -28,6 +28,14 @@
  * Orientation: an operand is "k-contiguous" when its columns run along the
  * GEMM reduction index (row-major A[M][K], or B stored [N][K]); otherwise its
  * rows run along the reduction (A stored [K][M], B stored [K][N]).
+ *
+ * MXFP8 operands (fmt = KF_FMT_MXFP8, the OCP microscaling format): elements are
+ * OCP e4m3 bytes and every 32 consecutive elements of a source row share one
+ * E8M0 scale byte (value 2^(byte-127)) at scales[st*lds + c/32], st and c the
+ * source row and column of the rule above. Only k-contiguous operands with
+ * hout = 1 are accepted, ncols and part_width multiples of 128, ld multiple of
+ * 16; both operands of a GEMM must then be MXFP8 (kf_gemm_fused runs the CDNA4
+ * v_mfma_scale_f32_16x16x128_f8f6f4, twice the fp16 MFMA rate).
  */
 #ifndef KALDI_FP16_AMD_KF_OPS_H
 #define KALDI_FP16_AMD_KF_OPS_H
@@ -54,7 +62,13 @@ typedef struct {
     int dh[KF_MAX_PARTS];
     int edge_t[KF_MAX_PARTS];
     int edge_row[KF_MAX_PARTS];
+    int fmt;                   /* KF_FMT_FP16 (0) or KF_FMT_MXFP8 (1) */
+    const uint8_t *scales;     /* MXFP8: E8M0 block scales */
+    long long lds;             /* MXFP8: bytes between the scale rows of consecutive source rows */
 } KfOperand;
+
+#define KF_FMT_FP16 0
+#define KF_FMT_MXFP8 1
 
 /*
  * Fused epilogue, applied per output element (m, n) to the fp32 accumulator:
@@ -83,6 +97,9 @@ typedef struct {
     long long ldo2;
     const float *scale2;   /* fp32 [N] or NULL (= 1) */
     const uint8_t *mask_in;/* or NULL (= all ones) */
+    void *out8;            /* e4m3 [M x ldo8], or NULL */
+    long long ldo8;
+    uint8_t *scale8;       /* E8M0 [M x ldo8/32] (required with out8) */
 } KfEpilogue;
 
 /* current stream for every launch made by this library on the calling thread
@@ -102,6 +119,18 @@ int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
  */
 int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW,
                   long long ldw, float *bias_grad, int accumulate);
+
+/*
+ * MXFP8 quantisation (OCP MX): per block of 32 consecutive values of a row,
+ * amax = max |v|, scale = 2^(floor(log2 amax) - 8) (E8M0 byte = exponent + 127,
+ * clamped to [1, 253]; amax = 0 gives byte 127), q = e4m3_rne(clamp(v / scale, +-448)).
+ *   transpose = 0: src [rows x cols] fp16 (ld_src); transpose = 1: q row r is
+ *   column r of src [cols x rows] (weights W[K][N] -> W8[N][K]).
+ * q: [rows x ldq] bytes, scales: [rows][lds]; columns cols .. roundup(cols, 128)-1
+ * of q and their scale bytes are written as zero / 127 (padding read by the GEMM).
+ */
+int kf_quant_mxfp8(const void *src, long long ld_src, int rows, int cols, int transpose,
+                   void *q, long long ldq, uint8_t *scales, long long lds);
 
 /* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols
  * (edge may be a spare row of src's own allocation) */

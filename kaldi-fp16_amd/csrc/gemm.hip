@@ -51,6 +51,11 @@ struct OpD {
     unsigned ldb, pwb;  // ld and part_width in bytes (32-bit addressing is checked on the host)
     int edges;          // any edge rows
     int dt[KF_MAX_PARTS], dh[KF_MAX_PARTS], et[KF_MAX_PARTS], er[KF_MAX_PARTS];
+    // MXFP8: geometry above is in 2-byte units (so the fp16 stagers move the bytes),
+    // the E8M0 scales are addressed per source row (lds bytes) and element / 32
+    const uint8_t *sc;
+    unsigned lds;
+    int pw8;            // part width in fp8 elements
 };
 
 // compile-time loop: body(I) with I a std::integral_constant (forces full unrolling,
@@ -117,6 +122,7 @@ __device__ __forceinline__ int mn_off(int r, int u) {
 }
 
 typedef __attribute__((address_space(3))) short4v lds_s4;
+typedef int v4i_t __attribute__((ext_vector_type(4)));
 
 // v_mfma_f32_16x16x32_f16 fragment: lane l holds Op[idx0 + (l&15)][k = 32s + 8(l>>4) + j]
 template <bool KC, int W>
@@ -376,32 +382,137 @@ struct WgradArgs {
     int k_per_split;    // multiple of BK
 };
 
-template <int BM, int BN, int ST>
+template <int BM, int BN, int ST, int SCB = 0>
 struct SmemSize {
-    static constexpr int stage = (BM + BN) * BK * 2;
+    static constexpr int stage = (BM + BN) * BK * 2 + SCB;
     static constexpr int pipe = ST * stage;
     static constexpr int bytes = pipe;
 };
 
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE>
+// ---------------------------------------------------------------------------
+// MXFP8 scale staging: per K-step of 128 fp8 elements every tile row needs the
+// 4 E8M0 bytes of its 4 blocks, one dword. Slot s of [A rows | B rows | unused]
+// is lane s%64 of LDS-DMA instruction s/64; each wave issues SPW of them, so
+// the vmcnt bookkeeping stays uniform. Instructions never straddle A and B
+// (BM % 64 == 0), so each has one buffer resource.
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int NW, int AM>
+struct ScaleStager {
+    static constexpr int SLOTS = BM + BN;
+    static constexpr int SPW = (SLOTS + 64 * NW - 1) / (64 * NW);
+    static constexpr int BYTES = SPW * NW * 64 * 4;
+    static_assert(BM % 64 == 0, "A scale rows fill whole instructions");
+    unsigned b0[SPW], b1[SPW];  // A: part-0 / part-1 row offsets; B: row offset (b1 unused)
+    __device__ __forceinline__ void init(const OpD &A, const OpD &B, int m0, int n0, int wave,
+                                         int lane) {
+        static_for<SPW>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const int slot = (wave * SPW + i) * 64 + lane;
+            b0[i] = b1[i] = BAD;
+            if (slot < BM) {
+                const int r = m0 + slot;
+                if (r < A.nrows) {
+                    if constexpr (AM == OP_SIMPLE) {
+                        b0[i] = (unsigned)r * A.lds;
+                    } else {
+                        for (int p = 0; p < 2 && p < A.nparts; ++p) {
+                            int st = r + A.dt[p];
+                            bool ok = true;
+                            if (A.tclamp) st = min(max(st, 0), A.T - 1);
+                            else ok = (unsigned)st < (unsigned)A.T;
+                            if (ok) (p ? b1[i] : b0[i]) = (unsigned)st * A.lds;
+                        }
+                    }
+                }
+            } else if (slot < SLOTS) {
+                const int n = n0 + slot - BM;
+                if (n < B.nrows) b0[i] = (unsigned)n * B.lds;
+            }
+        });
+    }
+    // k0 in 2-byte units (the fp16 stagers' unit): fp8 element 2*k0 starts the step
+    __device__ __forceinline__ void issue(const OpD &A, const OpD &B, __amdgpu_buffer_rsrc_t ra,
+                                          __amdgpu_buffer_rsrc_t rb, int k0, char *dst, int wave,
+                                          int lane) {
+        const int k8 = 2 * k0;
+        static_for<SPW>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            const int ins = wave * SPW + i;  // wave-uniform
+            const int slot = ins * 64 + lane;
+            unsigned voff = BAD;
+            const bool isA = ins * 64 < BM;
+            if (isA) {
+                if (k8 < 2 * A.ncols) {
+                    if constexpr (AM == OP_SIMPLE) {
+                        if (b0[i] != BAD) voff = b0[i] + (unsigned)(k8 >> 5);
+                    } else {
+                        const int p = k8 >= A.pw8 ? 1 : 0;
+                        const unsigned b = p ? b1[i] : b0[i];
+                        if (b != BAD) voff = b + (unsigned)((k8 - p * A.pw8) >> 5);
+                    }
+                }
+            } else if (slot < SLOTS && k8 < 2 * B.ncols && b0[i] != BAD) {
+                voff = b0[i] + (unsigned)(k8 >> 5);
+            }
+            // a wave-uniform branch, not a select: a selected 128-bit resource goes to scratch
+            auto *ldst = (__attribute__((address_space(3))) void *)(dst + ins * 256);
+            if (isA) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, ldst, 4, voff, 0, 0, 0);
+            else __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, ldst, 4, voff, 0, 0, 0);
+        });
+    }
+};
+
+// e4m3 (OCP) of 8 values already divided by the block scale; clamp at 448 first
+// (v_cvt_pk_fp8_f32 rounds 464..479 to 448 but 480 and above to NaN)
+__device__ __forceinline__ uint2 pack_e4m3x8(const float *v) {
+    uint2 r;
+    unsigned w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        float c[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) c[e] = fminf(fmaxf(v[4 * h + e], -448.f), 448.f);
+        unsigned x = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+        x = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], x, true);
+        w[h] = x;
+    }
+    r.x = w[0];
+    r.y = w[1];
+    return r;
+}
+
+// E8M0 exponent of a block with max magnitude amax: floor(log2 amax) - 8,
+// clamped so that 2^-e stays a normal float; amax = 0 -> 0
+__device__ __forceinline__ int mx_exponent(float amax) {
+    if (!(amax > 0.f)) return 0;
+    const int ex = (int)((__float_as_uint(amax) >> 23) & 0xFF) - 127;
+    return min(max(ex - 8, -126), 126);
+}
+
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE,
+          int F8 = 0>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int K, OpD A, OpD B,
                                                                KfEpilogue E, WgradArgs G,
                                                                int n_mtiles, int n_ntiles) {
     constexpr int NW = WM * WN, NTH = 64 * NW;
+    using SCS = ScaleStager<BM, BN, NW, AM>;
+    constexpr int SCB = F8 ? SCS::BYTES : 0;
+    static_assert(!F8 || (AKC && BKC && !WGRAD && BMODE == OP_SIMPLE && AM != OP_GEN),
+                  "MXFP8: k-contiguous plain / spliced A, plain B");
     static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     static_assert(TM * 16 == WTM && TN * 16 == WTN, "wave tile multiple of 16");
     constexpr int A_STAGE = BM * BK * 2, B_STAGE = BN * BK * 2;
-    constexpr int STAGE = A_STAGE + B_STAGE;
+    constexpr int STAGE = A_STAGE + B_STAGE + SCB;
     using SA = Stager<AKC, BM, AM, NW>;
     using SB = Stager<BKC, BN, BMODE, NW>;
-    constexpr int LPT = SA::NC + SB::NC;  // LDS-DMA instructions per thread per stage
+    constexpr int LPT = SA::NC + SB::NC + (F8 ? SCS::SPW : 0);  // LDS-DMA per thread per stage
     static_assert(ST >= 2 && ST <= 4, "stages");
-    static_assert(4 * BN * 4 + (32 * (WTN + 4) * 4) * NW <= SmemSize<BM, BN, ST>::bytes,
+    static_assert(4 * BN * 4 + (32 * (WTN + 4) * 4) * NW <= SmemSize<BM, BN, ST, SCB>::bytes,
                   "epilogue staging");
 
-    __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, ST>::bytes];
+    __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, ST, SCB>::bytes];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -426,13 +537,21 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
 
     SA sa;
     SB sb;
+    SCS ss;
     sa.init(A, m0, wave, lane);
     sb.init(B, n0, wave, lane);
+    if constexpr (F8) ss.init(A, B, m0, n0, wave, lane);
     const __amdgpu_buffer_rsrc_t ra = make_rsrc(A.base), rb = make_rsrc(B.base);
+    __amdgpu_buffer_rsrc_t rsa = ra, rsb = rb;
+    if constexpr (F8) {
+        rsa = make_rsrc(A.sc);
+        rsb = make_rsrc(B.sc);
+    }
     auto issue = [&](int stage, int k0) {
         char *base = smem + stage * STAGE;
         sa.issue(A, ra, k0, kend, base, wave, lane);
         sb.issue(B, rb, k0, kend, base + A_STAGE, wave, lane);
+        if constexpr (F8) ss.issue(A, B, rsa, rsb, k0, base + A_STAGE + B_STAGE, wave, lane);
     };
 
     float4v acc[TM][TN];
@@ -458,6 +577,38 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
         if (kt + ST - 1 < nk) issue((kt + ST - 1) % ST, kbeg + (kt + ST - 1) * BK);
         const char *ta = smem + (kt % ST) * STAGE;
         const char *tb = ta + A_STAGE;
+        if constexpr (F8) {
+            // one v_mfma_scale_f32_16x16x128_f8f6f4 per (I, J) per K-step: lane l holds
+            // bytes [16g, 16g+16) and [64+16g, 64+16g+16) of its row (g = l>>4) — the
+            // chunks the fp16 fragment loads of s = 0, 1 return — and supplies the
+            // E8M0 scale of block g of row l&15 (lane maps measured on the MI355X,
+            // scripts/probe_mx.py)
+            const unsigned *sct = reinterpret_cast<const unsigned *>(tb + B_STAGE);
+            const int g8 = 8 * (lane >> 4);
+            typedef int v8i __attribute__((ext_vector_type(8)));
+            v8i fa[TM], fb[TN];
+            int sca[TM], scb[TN];
+            static_for<TM>([&](auto I) {
+                const int r = wm * WTM + I * 16;
+                half8 lo = load_frag<true, BM>(ta, r, 0, lane), hi = load_frag<true, BM>(ta, r, 1, lane);
+                fa[I] = __builtin_shufflevector(__builtin_bit_cast(v4i_t, lo), __builtin_bit_cast(v4i_t, hi),
+                                                0, 1, 2, 3, 4, 5, 6, 7);
+                sca[I] = (int)((sct[r + (lane & 15)] >> g8) & 0xFF);
+            });
+            static_for<TN>([&](auto J) {
+                const int c = wn * WTN + J * 16;
+                half8 lo = load_frag<true, BN>(tb, c, 0, lane), hi = load_frag<true, BN>(tb, c, 1, lane);
+                fb[J] = __builtin_shufflevector(__builtin_bit_cast(v4i_t, lo), __builtin_bit_cast(v4i_t, hi),
+                                                0, 1, 2, 3, 4, 5, 6, 7);
+                scb[J] = (int)((sct[BM + c + (lane & 15)] >> g8) & 0xFF);
+            });
+            static_for<TM>([&](auto I) {
+                static_for<TN>([&](auto J) {
+                    acc[I][J] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                        fa[I], fb[J], acc[I][J], 0, 0, 0, sca[I], 0, scb[J]);
+                });
+            });
+        } else
         static_for<BK / 32>([&](auto S) {
             constexpr int s = decltype(S)::value;
             half8 fa[TM], fb[TN];
@@ -550,8 +701,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
                 const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
                 const int nl = wn * WTN + 8 * cg;
                 const int m = m0 + wm * WTM + ic * 32 + r, n = n0 + nl;
-                if (m < M && n < N) {
-                    float v[8];
+                const bool live = m < M && n < N;
+                float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                if (live) {
                     float4v x0 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg);
                     float4v x1 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg + 4);
 #pragma unroll
@@ -560,6 +712,26 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
                         v[e + 4] = x1[e];
                     }
                     epilogue8(E, P, m, n, nl, v, cold[k], rres[k], mb[k]);
+                }
+                if constexpr (CG % 4 == 0) {
+                    // MXFP8 copy: the 4 lanes l..l+3 (l % 4 == 0) hold one 32-column block
+                    if (E.out8) {
+                        float amax = 0.f;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+                        amax = fmaxf(amax, __shfl_xor(amax, 1));
+                        amax = fmaxf(amax, __shfl_xor(amax, 2));
+                        const int ex = mx_exponent(amax);
+                        const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
+                        float q[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) q[e] = v[e] * inv;
+                        const uint2 pk = pack_e4m3x8(q);
+                        if (live) {
+                            *reinterpret_cast<uint2 *>((uint8_t *)E.out8 + (long long)m * E.ldo8 + n) = pk;
+                            if ((lane & 3) == 0) E.scale8[(long long)m * (E.ldo8 >> 5) + (n >> 5)] = (uint8_t)(ex + 127);
+                        }
+                    }
                 }
             });
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -686,20 +858,36 @@ static bool to_dev(const KfOperand &d, OpD &o, const char *name) {
         kf_set_error("operand %s: hout %d too large", name, d.hout);
         return false;
     }
+    const bool f8 = d.fmt == KF_FMT_MXFP8;
+    if (d.fmt != KF_FMT_FP16 && !f8) {
+        kf_set_error("operand %s: unknown format %d", name, d.fmt);
+        return false;
+    }
+    if (f8 && (!d.kcontig || d.hout != 1 || d.ncols % 128 || d.part_width % 128 || d.ld % 16 ||
+               !d.scales || d.lds <= 0 || d.nparts > 2)) {
+        kf_set_error("operand %s: MXFP8 needs a k-contiguous operand with hout 1, <= 2 parts, "
+                     "ncols / part_width multiples of 128, ld multiple of 16 and scales", name);
+        return false;
+    }
     memset(&o, 0, sizeof o);
     o.base = (const h16 *)d.base;
-    o.ld = d.ld;
+    // MXFP8: 2-byte units for the byte movers (ld, ncols, part width halved)
+    const int u = f8 ? 2 : 1;
+    o.ld = d.ld / u;
     o.nrows = d.nrows;
-    o.ncols = d.ncols;
+    o.ncols = d.ncols / u;
     o.nparts = d.nparts;
-    o.pw = d.part_width;
+    o.pw = d.part_width / u;
+    o.sc = f8 ? d.scales : nullptr;
+    o.lds = f8 ? (unsigned)d.lds : 0;
+    o.pw8 = f8 ? d.part_width : 0;
     o.T = d.T;
     o.hout = d.hout;
     o.hsrc = d.hsrc;
     o.hmul = d.hmul;
     o.hshift = d.hdiv == 1 ? 0 : d.hdiv == 2 ? 1 : d.hdiv == 4 ? 2 : 3;
     o.tclamp = d.tpolicy == KF_CLAMP;
-    o.p64 = d.part_width % BK == 0;
+    o.p64 = o.pw % BK == 0;
     o.inv_hout = (65536u + d.hout - 1) / d.hout;
     bool edges = false;
     for (int i = 0; i < KF_MAX_PARTS; ++i) {
@@ -711,8 +899,8 @@ static bool to_dev(const KfOperand &d, OpD &o, const char *name) {
     }
     o.simple = d.nparts == 1 && d.hout == 1 && d.dt[0] == 0 && !edges;
     o.edges = edges;
-    o.ldb = (unsigned)(d.ld * 2);
-    o.pwb = (unsigned)(d.part_width * 2);
+    o.ldb = (unsigned)(d.ld * 2 / u);
+    o.pwb = (unsigned)(d.part_width * 2 / u);
     // 32-bit byte offsets (buffer addressing): the largest source row must fit
     long long rows = d.nrows;
     if (!o.simple) {
@@ -720,7 +908,7 @@ static bool to_dev(const KfOperand &d, OpD &o, const char *name) {
         for (int i = 0; i < d.nparts; ++i)
             if (d.edge_t[i] >= 0 && d.edge_row[i] + 1 > rows) rows = d.edge_row[i] + 1;
     }
-    if (rows * d.ld * 2 >= (1LL << 32) - 64) {
+    if (rows * d.ld * 2 / u >= (1LL << 32) - 64 || (f8 && rows * d.lds >= (1LL << 32) - 64)) {
         kf_set_error("operand %s: %lld x %lld elements exceed 32-bit buffer addressing", name, rows,
                      d.ld);
         return false;
@@ -742,7 +930,8 @@ static bool mn_gen_ok(const OpD &o, const char *name) {
     return true;
 }
 
-template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE>
+template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE,
+          int F8 = 0>
 static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilogue &E,
                   const WgradArgs &G, int splits) {
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
@@ -752,10 +941,10 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
         rec.a = prof_event();
         rec.b = prof_event();
         rec.cls = WGRAD ? KF_PROF_WGRAD : KF_PROF_FUSED;
-        rec.flops = 2.0 * M * N * (double)K;
+        rec.flops = 2.0 * M * N * (double)K * (F8 ? 2 : 1);  // K counts 2-byte units
         hipEventRecord(rec.a, kf_stream());
     }
-    gemm_kernel<BM, BN, WM, WN, AKC, BKC, WGRAD, ST, AM, BMODE>
+    gemm_kernel<BM, BN, WM, WN, AKC, BKC, WGRAD, ST, AM, BMODE, F8>
         <<<grid, 64 * WM * WN, 0, kf_stream()>>>(M, N, K, A, B, E, G, mt, nt);
     if (g_prof) {
         hipEventRecord(rec.b, kf_stream());
@@ -794,12 +983,38 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         kf_set_error("kf_gemm_fused: leading dimensions must be multiples of 8");
         return -1;
     }
+    if (E.out8 && (N % 32 || E.ldo8 % 32 || !E.scale8)) {
+        kf_set_error("kf_gemm_fused: out8 needs N and ldo8 multiples of 32 and scale8");
+        return -1;
+    }
     WgradArgs G{nullptr, nullptr, 0};
     const int am = op_mode(a), bm = op_mode(b);
+    const bool f8 = A->fmt == KF_FMT_MXFP8;
+    if (f8 != (B->fmt == KF_FMT_MXFP8)) {
+        kf_set_error("kf_gemm_fused: both operands must be MXFP8, or neither");
+        return -1;
+    }
+    if (f8) {
+        if (K % 128 || am == OP_GEN || a.edges || bm != OP_SIMPLE) {
+            kf_set_error("kf_gemm_fused: MXFP8 needs K %% 128 == 0, a plain or time-spliced A and a "
+                         "plain B (K=%d)", K);
+            return -1;
+        }
+        const int K2 = K / 2;  // the kernel counts the reduction in 2-byte units
+        if (N >= 256) {
+            if (am == OP_SIMPLE)
+                return launch<256, 256, 2, 4, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
+            return launch<256, 256, 2, 4, true, true, false, 2, OP_P2, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
+        }
+        if (am == OP_SIMPLE)
+            return launch<128, 128, 2, 2, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
+        return launch<128, 128, 2, 2, true, true, false, 2, OP_P2, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
+    }
     // 8-wave 256-row tiles halve the staged bytes per MFMA flop against the 4-wave
     // 128-row ones; KF_GEMM_BIG=0 selects the 4-wave family for A/B.
     static const int big = gemm_big();
-    const int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : (big && N >= 256 ? 3 : 0));
+    int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : (big && N >= 256 ? 3 : 0));
+    if (E.out8 && tile == 1) tile = 0;  // out8 needs 32-column blocks inside one wave's tile
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
         if (tile == 3) return launch<256, 256, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
@@ -947,6 +1162,59 @@ __global__ void k_gemm_small(int M, int N, int K, float alpha, const h16 *A, int
         if (beta != 0.f) v += beta * h2f(C[(long long)m * ldc + n]);
         C[(long long)m * ldc + n] = f2h(v);
     }
+}
+
+// ---------------------------------------------------------------------------
+// MXFP8 quantisation (kf_ops.h): one thread per (row, 32-element block)
+// ---------------------------------------------------------------------------
+__global__ void k_quant_mxfp8(const h16 *src, long long ld_src, int rows, int cols, int cols_pad,
+                              int transpose, uint8_t *q, long long ldq, uint8_t *scales,
+                              long long lds) {
+    const int nblk = cols_pad / 32;
+    const long long total = (long long)rows * nblk;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int r = (int)(i / nblk), b = (int)(i - (long long)r * nblk);
+        float v[32];
+        float amax = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const int c = 32 * b + j;
+            float x = 0.f;
+            if (c < cols) x = h2f(transpose ? src[(long long)c * ld_src + r] : src[(long long)r * ld_src + c]);
+            v[j] = x;
+            amax = fmaxf(amax, fabsf(x));
+        }
+        const int ex = mx_exponent(amax);
+        const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) v[j] *= inv;
+        uint8_t *qr = q + (long long)r * ldq + 32 * b;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) *reinterpret_cast<uint2 *>(qr + 8 * w) = pack_e4m3x8(v + 8 * w);
+        scales[(long long)r * lds + b] = (uint8_t)(ex + 127);
+    }
+}
+
+extern "C" int kf_quant_mxfp8(const void *src, long long ld_src, int rows, int cols, int transpose,
+                              void *q, long long ldq, uint8_t *scales, long long lds) {
+    if (rows <= 0 || cols <= 0) return 0;
+    const int cols_pad = (cols + 127) / 128 * 128;
+    if (!src || !q || !scales || ldq < cols_pad || ldq % 16 || lds < cols_pad / 32 ||
+        ((uintptr_t)q & 7)) {
+        kf_set_error("kf_quant_mxfp8: bad arguments (rows=%d cols=%d ldq=%lld lds=%lld)", rows,
+                     cols, ldq, lds);
+        return -1;
+    }
+    const long long total = (long long)rows * (cols_pad / 32);
+    k_quant_mxfp8<<<kf_blocks(total, 256, 16384), 256, 0, kf_stream()>>>(
+        (const h16 *)src, ld_src, rows, cols, cols_pad, transpose, (uint8_t *)q, ldq, scales, lds);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        kf_set_error("kf_quant_mxfp8: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
 }
 
 int kf_ops_gemm_impl(int M, int N, int K, float alpha, const void *A, int lda, const void *B,

@@ -325,18 +325,26 @@ class KfOperand(C.Structure):
     _fields_ = [("base", _vp), ("ld", _ll), ("nrows", _i), ("ncols", _i), ("kcontig", _i),
                 ("nparts", _i), ("part_width", _i), ("T", _i), ("hout", _i), ("hsrc", _i),
                 ("hmul", _i), ("hdiv", _i), ("tpolicy", _i), ("dt", _i * MAXP), ("dh", _i * MAXP),
-                ("edge_t", _i * MAXP), ("edge_row", _i * MAXP)]
+                ("edge_t", _i * MAXP), ("edge_row", _i * MAXP), ("fmt", _i), ("scales", _vp),
+                ("lds", _ll)]
+
+
+FMT_FP16, FMT_MXFP8 = 0, 1
 
 
 class KfEpilogue(C.Structure):
     _fields_ = [("out", _vp), ("ldo", _ll), ("alpha", _f), ("beta", _f), ("bias", _vp), ("relu", _i),
                 ("mask_out", _vp), ("scale", _vp), ("shift", _vp), ("resid", _vp), ("ldr", _ll),
-                ("resid_alpha", _f), ("out2", _vp), ("ldo2", _ll), ("scale2", _vp), ("mask_in", _vp)]
+                ("resid_alpha", _f), ("out2", _vp), ("ldo2", _ll), ("scale2", _vp), ("mask_in", _vp),
+                ("out8", _vp), ("ldo8", _ll), ("scale8", _vp)]
 
 
 def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, hout=1, hsrc=1,
-            hmul=0, hdiv=1, tpolicy=0, dt=(), dh=(), edges=()):
+            hmul=0, hdiv=1, tpolicy=0, dt=(), dh=(), edges=(), scales=None, lds=0):
+    """scales != None makes an MXFP8 operand (base: e4m3 bytes, scales: E8M0, lds bytes/row)"""
     o = KfOperand()
+    if scales is not None:
+        o.fmt, o.scales, o.lds = FMT_MXFP8, scales, lds
     o.base, o.ld, o.nrows, o.ncols, o.kcontig = base, ld, rows, cols, kcontig
     o.nparts, o.part_width = nparts, part_width if part_width is not None else cols
     o.T = T if T is not None else rows
@@ -356,3 +364,4 @@ def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, ho
 _sig(core, "kf_gemm_fused", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), C.POINTER(KfEpilogue))
 _sig(core, "kf_gemm_wgrad", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i)
 _sig(core, "kf_rows_sum", _i, _vp, _vp, _ll, _i, _i, _i)
+_sig(core, "kf_quant_mxfp8", _i, _vp, _ll, _i, _i, _i, _vp, _ll, _vp, _ll)
