@@ -31,6 +31,7 @@ import numpy as np  # noqa: E402
 METRIC = "frames/sec CNN-TDNN fwd+bwd, 40-dim×1500-frame egs, 1/2/4/8 MI355X"
 METRIC_FWD = "frames/sec CNN-TDNN forward only, 40-dim×1500-frame egs, 1 MI355X"
 PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0    # MI355X dense FP8 (MX-scaled K=128 MFMA)
 FRAMES_PER_EG = 1500
 
 
@@ -49,6 +50,8 @@ def parse():
     p.add_argument("--cpu-frames", type=int, default=1500)
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--no-prof", action="store_true")
+    p.add_argument("--fp8", action="store_true",
+                   help="MXFP8 forward GEMMs (configs[4]; use with --xconfig cnn_tdnn_17f_3072.xconfig)")
     p.add_argument("--mode", choices=("train", "forward"), default="train",
                    help="train: the metric's fwd+bwd+SGD step; forward: configs[1], forward only")
     return p.parse_args()
@@ -121,6 +124,8 @@ def main():
     xcfg = synth.load_xconfig(a.xconfig)
     net = kfp16.Network(xcfg, max_frames=T)
     params, bns = synth.init_network(net, seed=42)        # identical replicas on every rank
+    if a.fp8:
+        net.set_fp8(True)
     grad = torch.zeros(net.num_params, dtype=torch.float32, device="cuda")
     net.bind_grad_buffer(grad.data_ptr())
 
@@ -196,7 +201,8 @@ def main():
         out = {
             "metric": METRIC_FWD if fwd_only else METRIC, "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "mxfp8 GEMMs (e4m3 + E8M0), fp16 storage" if a.fp8 else "fp16",
             "data": "synthetic",
             "config": {"workload": workload,
                        "xconfig": a.xconfig, "egs_per_gpu": a.egs, "frames_per_eg": FRAMES_PER_EG,
@@ -216,9 +222,12 @@ def main():
             dom = max(prof, key=lambda k: prof[k][1])
             n, ms, fl = prof[dom]
             ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-            out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP16_TFLOPS,
-                               "unit": "TFLOP/s", "frac": round(ach / PEAK_FP16_TFLOPS, 4),
-                               "traffic": pmc_traffic(dom),
+            peak = PEAK_FP8_TFLOPS if a.fp8 else PEAK_FP16_TFLOPS
+            out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                               "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                               # the committed PMC summary is of the default configuration
+                               "traffic": pmc_traffic(dom) if (a.xconfig == "cnn_tdnn_17f.xconfig" and
+                                                              not a.fp8 and a.mode == "train") else None,
                                "kernel": dom, "launches": n, "kernel_ms_per_step": round(ms / a.steps, 3),
                                "all_gemm_tflops": round(sum(v[2] for v in prof.values()) /
                                                         (sum(v[1] for v in prof.values()) * 1e-3) / 1e12, 2)}

@@ -70,6 +70,11 @@ int nnet_bind_grad_buffer(KfNet *net, float *dev);
 float *nnet_master_buffer(KfNet *net); /* device fp32 [num_params] */
 void *nnet_weight_buffer(KfNet *net);  /* device fp16 [num_params] */
 int nnet_sgd(KfNet *net, float lr, float momentum);
+/* MXFP8 forward (BASELINE configs[4]): 1 = every TDNN-F / linear / prefinal / output
+ * GEMM whose input has an MXFP8 copy runs on the fp8 MFMA (kf_ops.h MXFP8 operands);
+ * the producing epilogues write those copies, weights are re-quantised on every
+ * parameter change. Backward stays fp16 (it reads the fp16 activations). 0 = off. */
+int nnet_set_fp8(KfNet *net, int on);
 
 /* diagnostics (tests): back-propagate through the top n layers only; device
  * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott", "aux", "mask",

@@ -35,6 +35,12 @@ struct ParamRef {
     long long off;
 };
 
+// an MXFP8 tensor: e4m3 [rows x ld] + E8M0 scales [rows x ld/32] (kf_ops.h)
+struct Mx {
+    uint8_t *q = nullptr, *s = nullptr;
+    int ld = 0;
+};
+
 struct NetLayer {
     Layer L;
     int input = -1;  // index into layers, -1 = network input (features)
@@ -52,6 +58,9 @@ struct NetLayer {
     void *idct = nullptr;     // fp16 [D x D]
     bool bypass = false;
     bool needs_dx = false;
+    // MXFP8 forward (nnet_set_fp8): output / aux copies written by the producing
+    // GEMM epilogue, and the weights quantised [N][K] with each splice part padded
+    Mx a8, x8, w8, w8b;
 };
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -153,6 +162,7 @@ struct KfNet {
     void *dz[2] = {nullptr, nullptr}, *g[2] = {nullptr, nullptr};
     void *dbott = nullptr, *edge = nullptr;
     size_t edge_half = 0;
+    int fp8 = 0;
     std::vector<void *> allocs;
 
     void *dalloc(size_t bytes) {
@@ -508,6 +518,7 @@ extern "C" int nnet_param_info(const KfNet *net, int idx, char *name, int namele
     return 0;
 }
 
+static bool quantise_weights(KfNet *net, bool alloc);
 extern "C" int nnet_set_params(KfNet *net, const float *host) {
     const long long P = net->nparams;
     std::vector<uint16_t> h(P, 0);
@@ -523,7 +534,7 @@ extern "C" int nnet_set_params(KfNet *net, const float *host) {
         return -1;
     }
     bridge_gpu_memset(net->vel, 0, P * 4);
-    return 0;
+    return net->fp8 && !quantise_weights(net, false) ? -1 : 0;
 }
 
 extern "C" int nnet_get_params(const KfNet *net, float *host) {
@@ -584,6 +595,147 @@ static const void *act_of(KfNet *net, int idx) {
 }
 
 // ---------------------------------------------------------------------------
+// MXFP8 forward (configs[4] of BASELINE.json: "OCP-FP8 MFMA GEMM path")
+// Every dense GEMM of TDNN-F / linear / prefinal / output layers runs on
+// v_mfma_scale_f32_16x16x128_f8f6f4 when its input has an MXFP8 copy; the
+// copies are written by the producing GEMM's epilogue (out8), the weights are
+// quantised after every parameter change. Widths are padded to 128 (zero
+// elements, zero scale bytes), so splice parts stay whole K-steps.
+// ---------------------------------------------------------------------------
+namespace {
+inline int pad128(int x) { return (x + 127) / 128 * 128; }
+
+bool mx_alloc(KfNet *net, Mx &m, size_t rows, int width) {
+    m.ld = pad128(width);
+    m.q = (uint8_t *)net->dalloc(rows * m.ld + 64);
+    m.s = (uint8_t *)net->dalloc(rows * (m.ld / 32) + 64);
+    if (!m.q || !m.s) return false;
+    bridge_gpu_memset(m.q, 0, rows * m.ld + 64);
+    bridge_gpu_memset(m.s, 0, rows * (m.ld / 32) + 64);
+    return true;
+}
+// W [nparts*rows x N] fp16 -> Mx [N x nparts*pad128(rows)]
+bool mx_weights(KfNet *net, Mx &m, int pi, int nparts, int rows, int N, bool alloc) {
+    const int part = pad128(rows);
+    if (alloc) {
+        m.ld = nparts * part;
+        m.q = (uint8_t *)net->dalloc((size_t)N * m.ld + 64);
+        m.s = (uint8_t *)net->dalloc((size_t)N * (m.ld / 32) + 64);
+        if (!m.q || !m.s) return false;
+    }
+    const uint16_t *W = (const uint16_t *)wptr(net, pi);
+    for (int p = 0; p < nparts; ++p)
+        if (!ck(kf_quant_mxfp8(W + (size_t)p * rows * N, N, N, rows, 1, m.q + p * part, m.ld,
+                               m.s + p * part / 32, m.ld / 32),
+                "quantise weights"))
+            return false;
+    return true;
+}
+bool gemm_layer(LayerType t) {
+    return t == LayerType::TDNNF || t == LayerType::Linear || t == LayerType::Prefinal ||
+           t == LayerType::Output;
+}
+// the layer's output can carry an MXFP8 copy (its epilogue has 32-column blocks)
+bool f8_producer(const NetLayer &nl) {
+    const Layer &L = nl.L;
+    // conv: the epilogue's [(t,h) x fout] view must be the consumer's [t x hout*fout]
+    if (L.type == LayerType::ConvReluBN) return L.fin != 1 && L.fout % 32 == 0 && L.out_dim % 128 == 0;
+    return L.type == LayerType::TDNNF || L.type == LayerType::Linear ||
+           (L.type == LayerType::Prefinal && L.small_dim % 32 == 0);
+}
+// MXFP8 operand over an Mx tensor of T rows: plain, or spliced [x(t+dt0) | x(t+dt1)]
+KfOperand op_mx(const Mx &m, int T, int nparts, int dt0, int dt1) {
+    KfOperand o = op_base(m.q, m.ld, T, nparts * m.ld, 1);
+    if (nparts == 2) {
+        o.nparts = 2;
+        o.part_width = m.ld;
+        o.dt[0] = dt0;
+        o.dt[1] = dt1;
+        o.tpolicy = KF_CLAMP;
+    }
+    o.fmt = KF_FMT_MXFP8;
+    o.scales = m.s;
+    o.lds = m.ld / 32;
+    return o;
+}
+KfOperand op_mxw(const Mx &m, int N) {
+    KfOperand o = op_base(m.q, m.ld, N, m.ld, 1);
+    o.fmt = KF_FMT_MXFP8;
+    o.scales = m.s;
+    o.lds = m.ld / 32;
+    return o;
+}
+void set_out8(KfEpilogue &E, const Mx &m) {
+    if (!m.q) return;
+    E.out8 = m.q;
+    E.ldo8 = m.ld;
+    E.scale8 = m.s;
+}
+}  // namespace
+
+// MXFP8 copy of a layer's input, or NULL (fp8 off / producer without one)
+static const Mx *in8(KfNet *net, const NetLayer &nl) {
+    if (!net->fp8 || nl.input < 0) return nullptr;
+    const NetLayer &p = net->layers[nl.input];
+    if (p.act_alias) return in8(net, p);
+    return p.a8.q ? &p.a8 : nullptr;
+}
+
+static bool quantise_weights(KfNet *net, bool alloc) {
+    for (auto &nl : net->layers) {
+        const Layer &L = nl.L;
+        bool ok = true;
+        switch (L.type) {
+            case LayerType::TDNNF: {
+                const int np = L.time_stride > 0 ? 2 : 1;
+                ok = mx_weights(net, nl.w8, nl.pW, np, L.in_dim, L.bottleneck, alloc) &&
+                     mx_weights(net, nl.w8b, nl.pW2, np, L.bottleneck, L.out_dim, alloc);
+                break;
+            }
+            case LayerType::Linear:
+            case LayerType::Output:
+                ok = mx_weights(net, nl.w8, nl.pW, 1, L.in_dim, L.out_dim, alloc);
+                break;
+            case LayerType::Prefinal:
+                ok = mx_weights(net, nl.w8, nl.pW, 1, L.in_dim, L.big_dim, alloc) &&
+                     mx_weights(net, nl.w8b, nl.pW2, 1, L.big_dim, L.small_dim, alloc);
+                break;
+            default:
+                break;
+        }
+        if (!ok) return false;
+    }
+    return true;
+}
+
+extern "C" int nnet_set_fp8(KfNet *net, int on) {
+    if (!on) {
+        net->fp8 = 0;
+        return 0;
+    }
+    if (!net->fp8) {
+        const size_t T = (size_t)net->max_T;
+        bool first = true;
+        for (auto &nl : net->layers) first = first && !nl.w8.q;
+        for (auto &nl : net->layers) {
+            const Layer &L = nl.L;
+            if (first && f8_producer(nl) && !mx_alloc(net, nl.a8, T, L.out_dim)) {
+                set_err("fp8: alloc " + L.name);
+                return -1;
+            }
+            if (first && (L.type == LayerType::TDNNF || L.type == LayerType::Prefinal) &&
+                !mx_alloc(net, nl.x8, T, L.type == LayerType::TDNNF ? L.bottleneck : L.big_dim)) {
+                set_err("fp8: alloc " + L.name);
+                return -1;
+            }
+        }
+        if (!quantise_weights(net, first)) return -1;
+    }
+    net->fp8 = 1;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
 // forward (Network.Forward, forward.go:148-202)
 // ---------------------------------------------------------------------------
 extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
@@ -633,22 +785,34 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
                 E.mask_out = nl.mask;
                 E.scale = nl.bn_scale;
                 E.shift = nl.bn_shift;
+                if (net->fp8 && nl.a8.q) {  // rows (t,h) of fout: the [t x hout*fout] copy
+                    E.out8 = nl.a8.q;
+                    E.ldo8 = L.fout;
+                    E.scale8 = nl.a8.s;
+                }
                 if (!ck(kf_gemm_fused(T * L.hout, L.fout, K, &A, &B, &E), "conv")) return -1;
                 break;
             }
             case LayerType::TDNNF: {
                 const int s = L.time_stride, bn = L.bottleneck;
                 const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
-                KfOperand A = s > 0 ? op_splice(x, T, din, -s, 0, KF_CLAMP, 1) : op_base(x, din, T, din, 1);
-                KfOperand B = op_base(wptr(net, nl.pW), bn, klin, bn, 0);
+                const int np = s > 0 ? 2 : 1;
+                const Mx *x8 = in8(net, nl);
+                KfOperand A = x8 ? op_mx(*x8, T, np, -s, 0)
+                                 : s > 0 ? op_splice(x, T, din, -s, 0, KF_CLAMP, 1) : op_base(x, din, T, din, 1);
+                KfOperand B = x8 ? op_mxw(nl.w8, bn) : op_base(wptr(net, nl.pW), bn, klin, bn, 0);
                 KfEpilogue E = epi0();
                 E.out = nl.aux;
                 E.ldo = bn;
-                if (!ck(kf_gemm_fused(T, bn, klin, &A, &B, &E), "tdnnf linear")) return -1;
-                KfOperand A2 = s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 1)
-                                     : op_base(nl.aux, bn, T, bn, 1);
-                KfOperand B2 = op_base(wptr(net, nl.pW2), dout, kaff, dout, 0);
+                if (net->fp8) set_out8(E, nl.x8);
+                if (!ck(kf_gemm_fused(T, bn, x8 ? nl.w8.ld : klin, &A, &B, &E), "tdnnf linear")) return -1;
+                const bool f8b = net->fp8 && nl.x8.q;
+                KfOperand A2 = f8b ? op_mx(nl.x8, T, np, 0, s)
+                                   : s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 1)
+                                           : op_base(nl.aux, bn, T, bn, 1);
+                KfOperand B2 = f8b ? op_mxw(nl.w8b, dout) : op_base(wptr(net, nl.pW2), dout, kaff, dout, 0);
                 KfEpilogue E2 = epi0();
+                if (net->fp8) set_out8(E2, nl.a8);
                 E2.out = nl.act;
                 E2.ldo = dout;
                 E2.bias = wptr(net, nl.pb2);
@@ -661,23 +825,28 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
                     E2.ldr = din;
                     E2.resid_alpha = (float)L.bypass_scale;
                 }
-                if (!ck(kf_gemm_fused(T, dout, kaff, &A2, &B2, &E2), "tdnnf affine")) return -1;
+                if (!ck(kf_gemm_fused(T, dout, f8b ? nl.w8b.ld : kaff, &A2, &B2, &E2), "tdnnf affine"))
+                    return -1;
                 break;
             }
             case LayerType::Linear: {
-                KfOperand A = op_base(x, din, T, din, 1);
-                KfOperand B = op_base(wptr(net, nl.pW), dout, din, dout, 0);
+                const Mx *x8 = in8(net, nl);
+                KfOperand A = x8 ? op_mx(*x8, T, 1, 0, 0) : op_base(x, din, T, din, 1);
+                KfOperand B = x8 ? op_mxw(nl.w8, dout) : op_base(wptr(net, nl.pW), dout, din, dout, 0);
                 KfEpilogue E = epi0();
                 E.out = nl.act;
                 E.ldo = dout;
-                if (!ck(kf_gemm_fused(T, dout, din, &A, &B, &E), "linear")) return -1;
+                if (net->fp8) set_out8(E, nl.a8);
+                if (!ck(kf_gemm_fused(T, dout, x8 ? nl.w8.ld : din, &A, &B, &E), "linear")) return -1;
                 break;
             }
             case LayerType::Prefinal: {
                 const int big = L.big_dim, small = L.small_dim;
-                KfOperand A = op_base(x, din, T, din, 1);
-                KfOperand B = op_base(wptr(net, nl.pW), big, din, big, 0);
+                const Mx *x8 = in8(net, nl);
+                KfOperand A = x8 ? op_mx(*x8, T, 1, 0, 0) : op_base(x, din, T, din, 1);
+                KfOperand B = x8 ? op_mxw(nl.w8, big) : op_base(wptr(net, nl.pW), big, din, big, 0);
                 KfEpilogue E = epi0();
+                if (net->fp8) set_out8(E, nl.x8);
                 E.out = nl.aux;
                 E.ldo = big;
                 E.bias = wptr(net, nl.pb);
@@ -685,27 +854,31 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
                 E.mask_out = nl.mask;
                 E.scale = nl.bn_scale;
                 E.shift = nl.bn_shift;
-                if (!ck(kf_gemm_fused(T, big, din, &A, &B, &E), "prefinal big")) return -1;
-                KfOperand A2 = op_base(nl.aux, big, T, big, 1);
-                KfOperand B2 = op_base(wptr(net, nl.pW2), small, big, small, 0);
+                if (!ck(kf_gemm_fused(T, big, x8 ? nl.w8.ld : din, &A, &B, &E), "prefinal big")) return -1;
+                const bool f8b = net->fp8 && nl.x8.q;
+                KfOperand A2 = f8b ? op_mx(nl.x8, T, 1, 0, 0) : op_base(nl.aux, big, T, big, 1);
+                KfOperand B2 = f8b ? op_mxw(nl.w8b, small) : op_base(wptr(net, nl.pW2), small, big, small, 0);
                 KfEpilogue E2 = epi0();
+                if (net->fp8) set_out8(E2, nl.a8);
                 E2.out = nl.act;
                 E2.ldo = small;
                 if (nl.has_bn2) {
                     E2.scale = nl.bn2_scale;
                     E2.shift = nl.bn2_shift;
                 }
-                if (!ck(kf_gemm_fused(T, small, big, &A2, &B2, &E2), "prefinal small")) return -1;
+                if (!ck(kf_gemm_fused(T, small, f8b ? nl.w8b.ld : big, &A2, &B2, &E2), "prefinal small"))
+                    return -1;
                 break;
             }
             case LayerType::Output: {
-                KfOperand A = op_base(x, din, T, din, 1);
-                KfOperand B = op_base(wptr(net, nl.pW), dout, din, dout, 0);
+                const Mx *x8 = in8(net, nl);
+                KfOperand A = x8 ? op_mx(*x8, T, 1, 0, 0) : op_base(x, din, T, din, 1);
+                KfOperand B = x8 ? op_mxw(nl.w8, dout) : op_base(wptr(net, nl.pW), dout, din, dout, 0);
                 KfEpilogue E = epi0();
                 E.out = nl.act;
                 E.ldo = dout;
                 E.bias = wptr(net, nl.pb);
-                if (!ck(kf_gemm_fused(T, dout, din, &A, &B, &E), "output")) return -1;
+                if (!ck(kf_gemm_fused(T, dout, x8 ? nl.w8.ld : din, &A, &B, &E), "output")) return -1;
                 if (L.include_log_softmax && !ck(ops_log_softmax(nl.act, T, dout), "log_softmax"))
                     return -1;
                 break;
@@ -978,10 +1151,10 @@ extern "C" float *nnet_master_buffer(KfNet *net) { return net->master; }
 extern "C" void *nnet_weight_buffer(KfNet *net) { return net->w16; }
 
 extern "C" int nnet_sgd(KfNet *net, float lr, float momentum) {
-    return ck(kf_sgd_flat(net->master, net->w16, net->grad, net->vel, lr, momentum, net->nparams),
-              "sgd")
-               ? 0
-               : -1;
+    if (!ck(kf_sgd_flat(net->master, net->w16, net->grad, net->vel, lr, momentum, net->nparams), "sgd"))
+        return -1;
+    // the MXFP8 weight copies follow every parameter change
+    return net->fp8 && !quantise_weights(net, false) ? -1 : 0;
 }
 
 // Parse + resolve only (no device work): one line per layer

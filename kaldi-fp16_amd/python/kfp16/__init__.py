@@ -87,6 +87,7 @@ _sig(nnet, "nnet_grad_buffer", _vp, _vp)
 _sig(nnet, "nnet_master_buffer", _vp, _vp)
 _sig(nnet, "nnet_weight_buffer", _vp, _vp)
 _sig(nnet, "nnet_sgd", _i, _vp, _f, _f)
+_sig(nnet, "nnet_set_fp8", _i, _vp, _i)
 _sig(nnet, "nnet_bind_grad_buffer", _i, _vp, _vp)
 _sig(nnet, "nnet_backward_n", _i, _vp, _vp, _i)
 _sig(nnet, "nnet_debug_tensor", _vp, _vp, C.c_char_p, _i)
@@ -290,6 +291,10 @@ class Network:
 
     def bind_grad_buffer(self, ptr):
         check(nnet.nnet_bind_grad_buffer(self.h, ptr), "nnet_bind_grad_buffer")
+
+    def set_fp8(self, on: bool = True):
+        """MXFP8 forward GEMMs (kf_nnet.h nnet_set_fp8)"""
+        check(nnet.nnet_set_fp8(self.h, int(on)), "nnet_set_fp8")
 
     def sgd(self, lr: float, momentum: float):
         check(nnet.nnet_sgd(self.h, float(lr), float(momentum)), "nnet_sgd")

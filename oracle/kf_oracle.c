@@ -319,6 +319,62 @@ static int layer_needs_dx(const OrcNet *net, int li) {
     return 0;
 }
 
+/* ---- OCP MXFP8 (e4m3 + E8M0, blocks of 32) quantise-dequantise ---------- */
+static float e4m3_rne(float a) { /* 0 <= a <= 448 */
+    if (a == 0.f) return 0.f;
+    int e;
+    frexpf(a, &e);           /* a = m 2^e, m in [0.5, 1) */
+    int ex = e - 1;          /* floor(log2 a) */
+    if (ex < -6) ex = -6;    /* subnormals: quantum 2^-9 */
+    const float q = ldexpf(1.f, ex - 3);
+    const float r = nearbyintf(a / q) * q; /* round to nearest even */
+    return r > 448.f ? 448.f : r;
+}
+static void mx_block(const float *x, long long xs, float *y, long long ys) {
+    float amax = 0.f;
+    for (int j = 0; j < 32; ++j) amax = fmaxf(amax, fabsf(x[j * xs]));
+    int ex = 0;
+    if (amax > 0.f) {
+        int e2;
+        frexpf(amax, &e2);
+        ex = e2 - 1 - 8;
+        if (ex < -126) ex = -126;
+        if (ex > 126) ex = 126;
+    }
+    const float sc = ldexpf(1.f, ex), inv = ldexpf(1.f, -ex);
+    for (int j = 0; j < 32; ++j) {
+        const float v = x[j * xs] * inv;
+        const float a = e4m3_rne(fminf(fabsf(v), 448.f));
+        y[j * ys] = (v < 0.f ? -a : a) * sc;
+    }
+}
+void orc_mx_qdq_rows(const float *x, float *y, long long rows, int cols) {
+    for (long long r = 0; r < rows; ++r)
+        for (int b = 0; b < cols / 32; ++b) mx_block(x + r * cols + 32 * b, 1, y + r * cols + 32 * b, 1);
+}
+static float *mx_rows_new(const float *x, long long rows, int cols) {
+    float *y = (float *)xalloc(sizeof(float) * (size_t)rows * cols);
+    orc_mx_qdq_rows(x, y, rows, cols);
+    return y;
+}
+/* weights W [K x N]: blocks of 32 along K for every column */
+static float *mx_cols_new(const float *W, int K, int N) {
+    float *y = (float *)xalloc(sizeof(float) * (size_t)K * N);
+    for (int n = 0; n < N; ++n)
+        for (int b = 0; b < K / 32; ++b) mx_block(W + (size_t)32 * b * N + n, N, y + (size_t)32 * b * N + n, N);
+    return y;
+}
+/* mirrors f8_producer of host/network.cpp */
+static int mx_producer(const OrcLayer *L) {
+    switch (L->type) {
+        case ORC_CONV: return L->fin != 1 && L->fout % 32 == 0 && L->out_dim % 128 == 0;
+        case ORC_TDNNF:
+        case ORC_LINEAR: return 1;
+        case ORC_PREFINAL: return L->small_dim % 32 == 0;
+        default: return 0;
+    }
+}
+
 static void alloc_net(OrcNet *net) {
     int n = net->nlayers;
     net->act = (float **)xalloc(sizeof(float *) * n);
@@ -329,17 +385,23 @@ static void alloc_net(OrcNet *net) {
     net->gW2 = (float **)xalloc(sizeof(float *) * n);
     net->gb2 = (float **)xalloc(sizeof(float *) * n);
     net->gact = (float **)xalloc(sizeof(float *) * n);
+    net->act8 = (float **)xalloc(sizeof(float *) * n);
 }
 
 #define FM(li) (net->force_mask ? net->force_mask[li] : NULL)
 int orc_net_forward(OrcNet *net, const float *features) {
-    const int T = net->T, mode = net->round_mode;
+    const int T = net->T, mode = net->round_mode, MX = net->mx8;
     if (!net->act) alloc_net(net);
     for (int li = 0; li < net->nlayers; ++li) {
         const OrcLayer *L = &net->layers[li];
         const float *x = L->input < 0 ? features : net->act[L->input];
         const int din = L->in_dim, dout = L->out_dim;
         float *y = (float *)xalloc(sizeof(float) * (size_t)T * dout);
+        /* MXFP8 GEMM input of this layer (the producer's copy), or NULL = fp16 GEMM */
+        const float *x8 = MX && L->input >= 0 ? net->act8[L->input] : NULL;
+        float *wq = NULL, *wq2 = NULL;
+#define MX_OUT(buf, rows, cols) \
+    do { if (MX && mx_producer(L)) net->act8[li] = mx_rows_new(buf, rows, cols); } while (0)
         switch (L->type) {
             case ORC_IDCT:
                 orc_matmul(T, dout, din, x, L->W, y);
@@ -355,23 +417,31 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 free(p);
                 net->mask[li] = (uint8_t *)xalloc((size_t)T * dout);
                 bias_relu_bn(y, T * L->hout, L->fout, L->b, &L->bn, net->mask[li], mode, 1, FM(li));
+                MX_OUT(y, T, dout);
                 if (mode) orc_round_f16(y, (long long)T * dout);
                 break;
             }
             case ORC_TDNNF: {
                 const int s = L->stride, bn = L->bn_dim;
-                const float *lin_in = x;
+                const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
+                const float *lin_src = x8 ? x8 : x, *Wl = L->W;
+                if (x8) Wl = wq = mx_cols_new(L->W, klin, bn);
+                const float *lin_in = lin_src;
                 float *tmp = NULL;
-                if (s > 0) lin_in = tmp = splice_minus(x, T, din, s);
+                if (s > 0) lin_in = tmp = splice_minus(lin_src, T, din, s);
                 float *bott = (float *)xalloc(sizeof(float) * (size_t)T * bn);
-                orc_matmul(T, bn, s > 0 ? 2 * din : din, lin_in, L->W, bott);
+                orc_matmul(T, bn, klin, lin_in, Wl, bott);
                 free(tmp);
+                float *bott8 = MX ? mx_rows_new(bott, T, bn) : NULL;
                 if (mode) orc_round_f16(bott, (long long)T * bn);
-                const float *aff_in = bott;
+                const float *aff_src = MX ? bott8 : bott, *Wa = L->W2;
+                if (MX) Wa = wq2 = mx_cols_new(L->W2, kaff, dout);
+                const float *aff_in = aff_src;
                 tmp = NULL;
-                if (s > 0) aff_in = tmp = splice_plus(bott, T, bn, s);
-                orc_matmul(T, dout, s > 0 ? 2 * bn : bn, aff_in, L->W2, y);
+                if (s > 0) aff_in = tmp = splice_plus(aff_src, T, bn, s);
+                orc_matmul(T, dout, kaff, aff_in, Wa, y);
                 free(tmp);
+                free(bott8);
                 net->mask[li] = (uint8_t *)xalloc((size_t)T * dout);
                 bias_relu_bn(y, T, dout, L->b2, &L->bn, net->mask[li], mode, 1, FM(li));
                 if (L->bypass > 0.f && din == dout) {
@@ -380,29 +450,38 @@ int orc_net_forward(OrcNet *net, const float *features) {
                         y[i] = mode == ORC_ROUND_REF ? rh(v) : v;
                     }
                 }
+                MX_OUT(y, T, dout);
                 if (mode) orc_round_f16(y, (long long)T * dout);
                 net->aux[li] = bott;
                 break;
             }
             case ORC_LINEAR:
-                orc_matmul(T, dout, din, x, L->W, y);
+                if (x8) wq = mx_cols_new(L->W, din, dout);
+                orc_matmul(T, dout, din, x8 ? x8 : x, x8 ? wq : L->W, y);
+                MX_OUT(y, T, dout);
                 if (mode) orc_round_f16(y, (long long)T * dout);
                 break;
             case ORC_PREFINAL: {
                 const int big = L->big_dim, small = L->small_dim;
                 float *bg = (float *)xalloc(sizeof(float) * (size_t)T * big);
-                orc_matmul(T, big, din, x, L->W, bg);
+                if (x8) wq = mx_cols_new(L->W, din, big);
+                orc_matmul(T, big, din, x8 ? x8 : x, x8 ? wq : L->W, bg);
                 net->mask[li] = (uint8_t *)xalloc((size_t)T * big);
                 bias_relu_bn(bg, T, big, L->b, &L->bn, net->mask[li], mode, 1, FM(li));
+                float *bg8 = MX ? mx_rows_new(bg, T, big) : NULL;
                 if (mode) orc_round_f16(bg, (long long)T * big);
-                orc_matmul(T, small, big, bg, L->W2, y);
+                if (MX) wq2 = mx_cols_new(L->W2, big, small);
+                orc_matmul(T, small, big, MX ? bg8 : bg, MX ? wq2 : L->W2, y);
+                free(bg8);
                 bias_relu_bn(y, T, small, NULL, &L->bn2, NULL, mode, 0, NULL);
+                MX_OUT(y, T, small);
                 if (mode) orc_round_f16(y, (long long)T * small);
                 net->aux[li] = bg;
                 break;
             }
             case ORC_OUTPUT:
-                orc_matmul(T, dout, din, x, L->W, y);
+                if (x8) wq = mx_cols_new(L->W, din, dout);
+                orc_matmul(T, dout, din, x8 ? x8 : x, x8 ? wq : L->W, y);
                 bias_relu_bn(y, T, dout, L->b, NULL, NULL, mode, 0, NULL);
                 if (mode) orc_round_f16(y, (long long)T * dout);
                 break;
@@ -410,6 +489,9 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 free(y);
                 return -1;
         }
+#undef MX_OUT
+        free(wq);
+        free(wq2);
         net->act[li] = y;
     }
     return 0;
@@ -612,6 +694,7 @@ void orc_net_free(OrcNet *net) {
         free(net->gW2[i]);
         free(net->gb2[i]);
         free(net->gact[i]);
+        if (net->act8) free(net->act8[i]);
     }
     free(net->act);
     free(net->mask);
@@ -621,6 +704,8 @@ void orc_net_free(OrcNet *net) {
     free(net->gW2);
     free(net->gb2);
     free(net->gact);
+    free(net->act8);
+    net->act8 = NULL;
     net->act = NULL;
 }
 

@@ -88,7 +88,17 @@ typedef struct {
      * gradients without the sqrt(flip-fraction) noise of near-zero
      * pre-activations that two fp16 paths legitimately decide differently. */
     const uint8_t **force_mask;
+    /* MXFP8 emulation of the GPU's nnet_set_fp8 forward (kf_nnet.h): the dense GEMMs
+     * of TDNN-F / linear / prefinal / output layers read quantise-dequantised
+     * (OCP MX, blocks of 32 along K) inputs and weights; act8 holds the
+     * quantised copies of producer outputs (taken before the fp16 rounding). */
+    int mx8;
+    float **act8;
 } OrcNet;
+
+/* OCP MXFP8 quantise-dequantise of rows of `cols` (cols % 32 == 0) values:
+ * the rule of kf_quant_mxfp8 (include/kf_ops.h) */
+void orc_mx_qdq_rows(const float *x, float *y, long long rows, int cols);
 
 int orc_net_forward(OrcNet *net, const float *features);
 /* out_grad [T x out_dim(last)], already fp16-representable */

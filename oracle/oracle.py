@@ -50,6 +50,7 @@ def lib(native: bool = False):
         _lib.orc_net_backward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         _lib.orc_net_free.argtypes = [C.c_void_p]
         _lib.orc_sgd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_longlong]
+        _lib.orc_mx_qdq_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_int]
     return _lib
 
 
@@ -79,7 +80,8 @@ class OrcNet(C.Structure):
                 ("act", C.POINTER(_fp)), ("mask", C.POINTER(C.POINTER(C.c_uint8))),
                 ("aux", C.POINTER(_fp)), ("gW", C.POINTER(_fp)), ("gb", C.POINTER(_fp)),
                 ("gW2", C.POINTER(_fp)), ("gb2", C.POINTER(_fp)), ("gact", C.POINTER(_fp)),
-                ("force_mask", C.POINTER(C.POINTER(C.c_uint8)))]
+                ("force_mask", C.POINTER(C.POINTER(C.c_uint8))), ("mx8", C.c_int),
+                ("act8", C.POINTER(_fp))]
 
 
 def parse_xconfig(text: str):
@@ -150,7 +152,8 @@ class OracleNet:
     params: name -> fp32 array, already fp16-representable (truncated) values;
     bns: (layer, which) -> (mean, var, gamma, beta)."""
 
-    def __init__(self, xconfig: str, params: dict, bns: dict, round_mode=ROUND_FUSED, threads=None):
+    def __init__(self, xconfig: str, params: dict, bns: dict, round_mode=ROUND_FUSED, threads=None,
+                 mx8=False):
         self.L = parse_xconfig(xconfig)
         self.keep = []
         index = {}
@@ -199,6 +202,7 @@ class OracleNet:
         self.arr = arr
         self.index = index
         self.round_mode = round_mode
+        self.mx8 = bool(mx8)   # emulate the GPU's MXFP8 forward GEMMs (kf_nnet.h nnet_set_fp8)
         if threads:
             lib().orc_set_threads(int(threads))
         self.net = None
@@ -234,6 +238,7 @@ class OracleNet:
         self.net.T = x.shape[0]
         self.net.feat_dim = x.shape[1]
         self.net.round_mode = self.round_mode
+        self.net.mx8 = int(self.mx8)
         if fm is not None:
             self.net.force_mask = fm
         rc = lib().orc_net_forward(C.byref(self.net), x.ctypes.data)
@@ -418,3 +423,11 @@ def chain_objf(g: dict, init, f: dict, nnet: np.ndarray, l2=0.0, oor=0.01, leaky
     L.orc_chain_objf(C.byref(o), C.byref(d), C.byref(n), x.ctypes.data, T, deriv.ctypes.data, C.byref(r))
     res = {k: getattr(r, k) for k, _ in OrcChainResult._fields_}
     return deriv, res
+
+
+def mx_qdq_rows(x: np.ndarray) -> np.ndarray:
+    """OCP MXFP8 quantise-dequantise of each row (blocks of 32), the oracle's rule"""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty_like(x)
+    lib().orc_mx_qdq_rows(x.ctypes.data, y.ctypes.data, x.shape[0], x.shape[1])
+    return y

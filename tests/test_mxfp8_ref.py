@@ -30,3 +30,15 @@ def test_roundtrip_error_bound():
     assert np.all(s >= 1) and np.all(s <= 253)
     z, zs = mx_quantize(np.zeros((1, 32)))
     assert not z.any() and zs[0, 0] == 127
+
+
+def test_oracle_mx_qdq_matches_numpy():
+    """the C oracle's MXFP8 quantise-dequantise (its fp8 network emulation) equals
+    the numpy restatement bit for bit"""
+    import oracle
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((40, 256)) * np.exp(rng.uniform(-10, 10, (40, 1)))).astype(np.float32)
+    x[0, :32] = 0
+    x[1, 5] = 448.0 * 2 ** 7
+    q, s = mx_quantize(x)
+    np.testing.assert_array_equal(oracle.mx_qdq_rows(x), mx_dequantize(q, s).astype(np.float32))
