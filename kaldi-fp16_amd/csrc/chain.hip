@@ -524,7 +524,7 @@ static size_t den_rec_fixed_bytes(int S, int P, int nsl) {
                         nsl + 2) + 64;
 }
 static size_t den_post_lds_bytes(int S, int P, int nslq) {
-    return (size_t)4 * (64 + 2 * (size_t)S + 3 * (size_t)P + (size_t)nslq * 66);
+    return (size_t)4 * (64 + 2 * (size_t)S + 4 * (size_t)P + (size_t)nslq * 66);
 }
 
 // ---------------------------------------------------------------------------
@@ -702,11 +702,9 @@ __device__ __forceinline__ SellLds stage_sell(const SellDev &T, int gi, int G, i
 // rebuild the full alpha'[t+1] in LDS from the exchanged slices. alpha' of every
 // frame goes to HBM for the backward kernel.
 template <typename XT>
-__global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const DenRun r, const DenX X) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
+                                             unsigned char *smem, int seq, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int seq, gi;
-    den_map(X, seq, gi);
     const int G = X.G, nsl = g.f.nsl;
     float *red = reinterpret_cast<float *>(smem);          // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;        // [32]
@@ -816,17 +814,26 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
         r.stats[(size_t)seq * 8 + 1] = r.den_out[seq * 2 + 1];
     }
 }
+template <typename XT>
+__global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const DenRun r, const DenX X) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int seq, gi;
+    den_map(X, seq, gi);
+    den_fwd_body<XT>(g, r, X, smem, seq, gi);
+}
 
 // Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per
 // sequence: beta'[t] over the source rows of this block's slices (exchanged),
 // beta[t] = beta'[t] + leaky*<init, beta'[t]>; beta[t] for t >= 1 goes to HBM for
-// k_den_post.
+// k_den_post. The reference scales beta'[t] by 1/sum(alpha[t]) and starts from
+// 1/total_prob; any positive per-frame factor gives the same posteriors once
+// k_den_post normalises each frame (the den posteriors of a frame sum to one:
+// they are d log p / d x_t), so this pass scales by 1/<init, beta'[t+1]> and
+// starts from ones — it needs nothing from the forward pass and runs beside it.
 template <typename XT>
-__global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const DenRun r, const DenX X) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, const DenX &X,
+                                             unsigned char *smem, int seq, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int seq, gi;
-    den_map(X, seq, gi);
     const int G = X.G, nsl = g.b.nsl;
     float *red = reinterpret_cast<float *>(smem);      // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;    // [32]
@@ -838,21 +845,20 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
     const int T = r.frames[seq];
     const long long row0 = r.row0[seq];
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
     const int rs = nsl * 64;
     float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rs;
     const float leaky = r.leaky;
-    const float total = r.den_out[seq * 2 + 0];
 
     const SellLds B = stage_sell(g.b, gi, G, nk, sbase, X.cache_b);
-    const float inv_tot = total > 0.0f ? 1.0f / total : 0.0f;  // BetaDashLastFrame
+    // BetaDashLastFrame up to the per-frame factor: beta'[T] = 1, <init, 1> = 1
     float part = 0.f;
-    for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s] * inv_tot;
-    float tb = leaky * block_sum<DEN_WAVES>(part, red);
-    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = inv_tot + tb;
+    for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
+    float nrm = block_sum<DEN_WAVES>(part, red);
+    float tb = leaky * nrm;
+    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = 1.0f + tb;
     if (gi == 0)
         for (int c = tid; c < rs; c += DEN_THREADS)
-            __builtin_nontemporal_store(inv_tot + tb, bstore + (size_t)T * rs + c);
+            __builtin_nontemporal_store(1.0f + tb, bstore + (size_t)T * rs + c);
     RowPre<XT> pre;
     if (T > 0) {
         pre.fetch(nnet + (row0 + (long long)(T - 1) * r.stride) * r.ld, P);
@@ -866,9 +872,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
     for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
         const int buf = t & 1;
         float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
-        const float at = asum[t];
-        const bool scale = at > 0.0f;
-        const float inv = scale ? 1.0f / at : 1.0f;
+        const bool scale = nrm > 0.0f;
+        const float inv = scale ? 1.0f / nrm : 1.0f;
         part = 0.f;
         auto term = [&](int dst, int pdf, float tp) { return vb[dst] * tp * xe[pdf]; };
         for (int k = wave; k < nk; k += DEN_WAVES) {  // kernel_den_backward_transitions
@@ -885,7 +890,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
         den_publish(X, blk + X.spg * 64, red, seq);
         if (t > 0) pre.fetch(nnet + (row0 + (long long)(t - 1) * r.stride) * r.ld, P);
         if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
-        tb = leaky * den_gather_psum(X, seq, buf);
+        nrm = den_gather_psum(X, seq, buf);  // <init, beta'[t]>: next frame's factor
+        tb = leaky * nrm;
         float *bt = bstore + (size_t)t * rs;
         den_consume(X, seq, buf, nsl, B.perm, B.initp, [&](int st, float v, float, int owner, int c) {
             const float b = v + tb;
@@ -901,6 +907,24 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_bwd(const DenDev g, const D
         }
         __syncthreads();
     }
+}
+// Forward and backward recursions of every sequence in one launch: blocks of the
+// first half run alpha with exchange XF, the second half beta with XB (the two
+// passes are independent, see den_bwd_body). One launch keeps all 2*nseq*G blocks
+// co-resident, which the bounded exchange polls rely on; the XCD grouping of
+// den_map is kept (G consecutive ids share an XCD).
+template <typename XT>
+__global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const DenRun r, const DenX XF,
+                                                        const DenX XB) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int half = XF.nseq * XF.G, nb = 2 * half, b = blockIdx.x;
+    int w = b;
+    if (nb % 8 == 0 && (nb / 8) % XF.G == 0) w = (b % 8) * (nb / 8) + b / 8;
+    const bool bwd = w >= half;
+    const int inner = bwd ? w - half : w;
+    const int seq = inner >> XF.lgG, gi = inner & (XF.G - 1);
+    if (bwd) den_bwd_body<XT>(g, r, XB, smem, seq, gi);
+    else den_fwd_body<XT>(g, r, XF, smem, seq, gi);
 }
 
 // Posteriors (kernel_den_posteriors, chain_den.cu:253-280) for every (sequence,
@@ -921,7 +945,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     float *xe = vb + S;                                // [P]
     float *xr = xe + P;                                // [P]
     float *numrow = xr + P;                            // [P]
-    int *metaq = reinterpret_cast<int *>(numrow + P);
+    float *gam = numrow + P;                           // [P] unnormalised den posteriors
+    int *metaq = reinterpret_cast<int *>(gam + P);
     const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
     for (int i = tid; i < nslq * 64; i += DEN_THREADS) metaq[i] = g.q.perm[i];
     for (int i = tid; i < nslq; i += DEN_THREADS) {
@@ -937,7 +962,6 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     const int rsf = g.f.nsl * 64, rsb = g.b.nsl * 64;  // slice-ordered rows (k_den_fwd / k_den_bwd)
     const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rsf;
     const float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rsb;
-    const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
 
     int ok = 1;
     float w = 1.0f;
@@ -994,12 +1018,10 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
                 if (p > 0 && p <= P) numrow[p - 1] = nps[q];
             }
         }
-        const float at = asum[t];
-        const bool scale = at > 0.0f;
-        const float inv = scale ? 1.0f / at : 1.0f;
         __syncthreads();
         h16 *orow = (MODE == DEN_PRODUCT) ? r.out_grad + (row0 + (long long)t * r.stride) * r.ldg : nullptr;
         const bool even = (t & 1) == 0;
+        float gpart = 0.f;
         for (int j = wave; j < nslq; j += DEN_WAVES) {
             const int pdf = permq[j * 64 + lane];
             float acc = sell_slice(g.q.arc, lenq[j], offq[j], lane, [&](int src, int dst, float tp) {
@@ -1007,7 +1029,15 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
             });
             if (pdf < 0) continue;
             const float gv = acc * xe[pdf];
-            const float den = scale ? gv * inv : gv;
+            gam[pdf] = gv;
+            gpart += gv;
+        }
+        // the frame's occupation sums to one (alpha and beta carry arbitrary
+        // per-frame factors, see den_bwd_body): normalise in a fixed order
+        const float gsum = block_sum<DEN_WAVES>(gpart, red);
+        const float ginv = gsum > 0.0f ? 1.0f / gsum : 0.0f;
+        for (int pdf = tid; pdf < P; pdf += DEN_THREADS) {
+            const float den = gam[pdf] * ginv;
             if (MODE == DEN_ABI) {
                 r.post_dense[(size_t)t * P + pdf] = den;
             } else {
@@ -1343,16 +1373,18 @@ void launch_den_fwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb
     else
         hipLaunchKernelGGL((k_den_fwd<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
 }
-void launch_den_bwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb, bool fp32_in,
-                    int mode) {
+// both recursions in one launch (k_den_fb); XF / XB from two exchange buffers
+void launch_den_fb(const DenDev &g, const DenRun &r, const DenX &XF, DenXBuf &xf, const DenX &XB,
+                   DenXBuf &xbb, bool fp32_in) {
     hipStream_t st = kf_stream();
-    xb.zero(st);
-    dim3 grid(X.nseq * X.G);
-    size_t lds = X.lds_b;
+    xf.zero(st);
+    xbb.zero(st);
+    dim3 grid(2 * XF.nseq * XF.G);
+    const size_t lds = std::max(XF.lds_f, XB.lds_b);
     if (fp32_in)
-        hipLaunchKernelGGL((k_den_bwd<float>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+        hipLaunchKernelGGL((k_den_fb<float>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
     else
-        hipLaunchKernelGGL((k_den_bwd<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+        hipLaunchKernelGGL((k_den_fb<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
 }
 void launch_den_post(const DenDev &g, const DenRun &r, const DenX &X, bool fp32_in, int mode) {
     hipStream_t st = kf_stream();
@@ -2026,16 +2058,18 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     r.stats = (float *)stats.p;
     r.post_dense = (float *)post.p;
     r.den_out = (float *)dout.p;
-    DenX X{};
-    DenXBuf xbuf;
-    if (!xbuf.make(g, 1, den_pick_G(1), X)) {
+    DenX X{}, XB{};
+    DenXBuf xbuf, xbuf2;
+    const int G = h_post ? den_pick_G(2) : den_pick_G(1);
+    if (!xbuf.make(g, 1, G, X) || (h_post && !xbuf2.make(g, 1, G, XB))) {
         den_set_error("den_forward: hipMalloc failed");
         return -1e30f;
     }
-    launch_den_fwd(g, r, X, xbuf, true);
     if (h_post) {
-        launch_den_bwd(g, r, X, xbuf, true, DEN_ABI);
+        launch_den_fb(g, r, X, xbuf, XB, xbuf2, true);
         launch_den_post(g, r, X, true, DEN_ABI);
+    } else {
+        launch_den_fwd(g, r, X, xbuf, true);
     }
     float st8[8] = {0};
     hipMemcpyAsync(st8, stats.p, 32, hipMemcpyDeviceToHost, st);
@@ -2045,7 +2079,7 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
         den_set_error("den_forward_backward: %s", hipGetErrorString(e));
         return -1e30f;
     }
-    if (xbuf.timed_out(st, 1)) {
+    if (xbuf.timed_out(st, 1) || (h_post && xbuf2.timed_out(st, 1))) {
         den_set_error("den_forward_backward: cross-workgroup exchange timed out");
         return -1e30f;
     }
@@ -2088,6 +2122,7 @@ struct KfNumBatch {
 
 struct KfChain {
     const KfDenGraph *den = nullptr;
+    DenXBuf xbuf2;  // the backward recursion's exchange (k_den_fb)
     int max_seqs = 0, max_frames = 0;
     float *alpha_store = nullptr, *beta_store = nullptr, *asum_store = nullptr, *stats = nullptr;
     float *num_ab = nullptr;      // numerator alpha/beta
@@ -2391,13 +2426,13 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
     const DenDev &dd = c->den->t->dev;
     double bytes = frames * (3.0 * 8.0 * c->den->num_arcs + 8.0 * dd.S + 6.0 * dd.P);
     int pd = kf_prof_start(KF_PROF_CHAIN_DEN, bytes);
-    DenX X{};
-    if (!c->xbuf.make(dd, nseq, den_pick_G(nseq), X)) {
+    DenX X{}, XB{};
+    const int G = den_pick_G(2 * nseq);  // forward and backward blocks share the CUs
+    if (!c->xbuf.make(dd, nseq, G, X) || !c->xbuf2.make(dd, nseq, G, XB)) {
         kfc_set_error("kf_chain_compute: hipMalloc failed");
         return -1;
     }
-    launch_den_fwd(dd, r, X, c->xbuf, false);
-    launch_den_bwd(dd, r, X, c->xbuf, false, DEN_PRODUCT);
+    launch_den_fb(dd, r, X, c->xbuf, XB, c->xbuf2, false);
     hipStreamWaitEvent(st, c->ev_num, 0);  // the numerator is needed from here on
     launch_den_post(dd, r, X, false, DEN_PRODUCT);
     kf_prof_stop(pd);
@@ -2427,7 +2462,7 @@ extern "C" int kf_chain_result(KfChain *c, KfChainResult *out) {
         kfc_set_error("kf_chain_result: stream error");
         return -1;
     }
-    if (n && c->xbuf.cnt && c->xbuf.timed_out(st, n)) {
+    if (n && c->xbuf.cnt && (c->xbuf.timed_out(st, n) || c->xbuf2.timed_out(st, n))) {
         kfc_set_error("kf_chain_result: den cross-workgroup exchange timed out (blocks not resident)");
         return -1;
     }
