@@ -523,8 +523,8 @@ static size_t den_rec_fixed_bytes(int S, int P, int nsl) {
     return (size_t)4 * (64 + (size_t)S + P + (P & 1) + 2 * (size_t)nsl + 128 * (size_t)nsl +
                         nsl + 2) + 64;
 }
-static size_t den_post_lds_bytes(int S, int P, int nslq) {
-    return (size_t)4 * (64 + 2 * (size_t)S + 4 * (size_t)P + (size_t)nslq * 66);
+static size_t den_post_lds_bytes(int S, int P, int nslq, int pair = 1) {
+    return (size_t)4 * (64 + 2 * (size_t)pair * S + (size_t)pair * P + (size_t)nslq * 66);
 }
 
 // ---------------------------------------------------------------------------
@@ -931,22 +931,39 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
 // frame) in parallel — gamma[t] needs only the stored alpha'[t] and beta[t+1] — by
 // pdf rows in arc order (no atomics), and in the product mode the objective
 // assembly of backward.go:224-371 into the fp16 gradient row. The whole pass always
-// runs; a non-finite objective only zeroes what is written.
+// runs; a non-finite objective only zeroes what is written. PAIR frames share one
+// stream of the pdf-ordered arc records (the pass is bound by that L2 stream).
 #define POST_FRAMES 4  // frames per block
-template <typename XT, int MODE>
+template <int PAIR>
+__device__ __forceinline__ void post_slice(const uint2 *arcs, int len, int off, int lane,
+                                           const float *va, const float *vb, int S, float acc[PAIR]) {
+    const uint2 *e = arcs + (size_t)off * 64 + lane;
+#pragma unroll
+    for (int f = 0; f < PAIR; ++f) acc[f] = 0.f;
+    for (int k = 0; k < len; k += 8) {
+        uint2 rr[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int src = rr[i].x & 0xFFFF, dst = rr[i].x >> 16;
+            const float tp = __uint_as_float(rr[i].y);
+#pragma unroll
+            for (int f = 0; f < PAIR; ++f) acc[f] += va[f * S + src] * tp * vb[f * S + dst];
+        }
+    }
+}
+template <typename XT, int MODE, int PAIR>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const DenRun r, int nfb) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int seq = blockIdx.x / nfb, fb = blockIdx.x % nfb;
     const int nslq = g.q.nsl;
     float *red = reinterpret_cast<float *>(smem);      // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;  // [S] alpha'[t]
-    float *vb = va + S;                                // [S] beta[t+1]
-    float *xe = vb + S;                                // [P]
-    float *xr = xe + P;                                // [P]
-    float *numrow = xr + P;                            // [P]
-    float *gam = numrow + P;                           // [P] unnormalised den posteriors
-    int *metaq = reinterpret_cast<int *>(gam + P);
+    float *va = reinterpret_cast<float *>(smem) + 64;  // [PAIR][S] alpha'[t]
+    float *vb = va + PAIR * S;                         // [PAIR][S] beta[t+1]
+    float *gam = vb + PAIR * S;                        // [PAIR][P] den, then the gradient
+    int *metaq = reinterpret_cast<int *>(gam + PAIR * P);
     const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
     for (int i = tid; i < nslq * 64; i += DEN_THREADS) metaq[i] = g.q.perm[i];
     for (int i = tid; i < nslq; i += DEN_THREADS) {
@@ -959,7 +976,7 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     if (t0 >= t1) return;
     const long long row0 = r.row0[seq];
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    const int rsf = g.f.nsl * 64, rsb = g.b.nsl * 64;  // slice-ordered rows (k_den_fwd / k_den_bwd)
+    const int rsf = g.f.nsl * 64, rsb = g.b.nsl * 64;  // slice-ordered rows (k_den_fb)
     const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rsf;
     const float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rsb;
 
@@ -985,83 +1002,95 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
             st8[7] = ok ? 1.0f : 0.0f;
         }
     }
-    for (int p = tid; p < P; p += DEN_THREADS) numrow[p] = 0.0f;
     const float l2s = r.opts.supervision_weight * r.opts.l2_regularize;
     const float oscale = 2.0f * r.opts.out_of_range_regularize;
     const bool do_oor = MODE == DEN_PRODUCT && r.opts.out_of_range_regularize > 0.0f;
     const bool do_l2 = MODE == DEN_PRODUCT && r.opts.l2_regularize > 0.0f;
     float oor = 0.f, sq = 0.f;
-    __syncthreads();
-    for (int t = t0; t < t1; ++t) {
-        // stage alpha'[t], beta[t+1], the output row and the numerator posteriors
-        const float *ar = astore + (size_t)t * rsf, *br = bstore + (size_t)(t + 1) * rsb;
-        for (int c = tid; c < rsf; c += DEN_THREADS) {
-            const int st = g.f.perm[c];
-            const float v = __builtin_nontemporal_load(ar + c);
-            if (st >= 0) va[st] = v;
-        }
-        for (int c = tid; c < rsb; c += DEN_THREADS) {
-            const int st = g.b.perm[c];
-            const float v = __builtin_nontemporal_load(br + c);
-            if (st >= 0) vb[st] = v;
-        }
-        const XT *xrow = nnet + (row0 + (long long)t * r.stride) * r.ld;
-        for (int p = tid; p < P; p += DEN_THREADS) {
-            const float x = (float)xrow[p];
-            xr[p] = x;
-            xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, x)));
-        }
-        if (MODE == DEN_PRODUCT) {  // the numerator's pdf set is the same every frame
-            const float *nps = nf->post_sparse + (size_t)t * NG;
-            for (int q = tid; q < NG; q += DEN_THREADS) {
-                int p = nf->grp_pdf[q];
-                if (p > 0 && p <= P) numrow[p - 1] = nps[q];
+    for (int t = t0; t < t1; t += PAIR) {
+        const int nf2 = min(PAIR, t1 - t);
+        // stage alpha'[t+f], beta[t+f+1] (a missing second frame computes zeros)
+#pragma unroll
+        for (int f = 0; f < PAIR; ++f) {
+            const bool live = f < nf2;
+            const float *ar = astore + (size_t)(t + f) * rsf, *br = bstore + (size_t)(t + f + 1) * rsb;
+            for (int c = tid; c < rsf; c += DEN_THREADS) {
+                const int st = g.f.perm[c];
+                const float v = live ? __builtin_nontemporal_load(ar + c) : 0.f;
+                if (st >= 0) va[f * S + st] = v;
+            }
+            for (int c = tid; c < rsb; c += DEN_THREADS) {
+                const int st = g.b.perm[c];
+                const float v = live ? __builtin_nontemporal_load(br + c) : 0.f;
+                if (st >= 0) vb[f * S + st] = v;
             }
         }
         __syncthreads();
-        h16 *orow = (MODE == DEN_PRODUCT) ? r.out_grad + (row0 + (long long)t * r.stride) * r.ldg : nullptr;
-        const bool even = (t & 1) == 0;
-        float gpart = 0.f;
+        float gpart[PAIR];
+#pragma unroll
+        for (int f = 0; f < PAIR; ++f) gpart[f] = 0.f;
         for (int j = wave; j < nslq; j += DEN_WAVES) {
             const int pdf = permq[j * 64 + lane];
-            float acc = sell_slice(g.q.arc, lenq[j], offq[j], lane, [&](int src, int dst, float tp) {
-                return va[src] * tp * vb[dst];
-            });
+            float acc[PAIR];
+            post_slice<PAIR>(g.q.arc, lenq[j], offq[j], lane, va, vb, S, acc);
             if (pdf < 0) continue;
-            const float gv = acc * xe[pdf];
-            gam[pdf] = gv;
-            gpart += gv;
-        }
-        // the frame's occupation sums to one (alpha and beta carry arbitrary
-        // per-frame factors, see den_bwd_body): normalise in a fixed order
-        const float gsum = block_sum<DEN_WAVES>(gpart, red);
-        const float ginv = gsum > 0.0f ? 1.0f / gsum : 0.0f;
-        for (int pdf = tid; pdf < P; pdf += DEN_THREADS) {
-            const float den = gam[pdf] * ginv;
-            if (MODE == DEN_ABI) {
-                r.post_dense[(size_t)t * P + pdf] = den;
-            } else {
-                const float x = xr[pdf];
-                float d = 0.0f;
-                if (do_oor && even) {  // chain_backward.cu:27-67
-                    if (x < -30.0f) {
-                        d += (-30.0f - x) * oscale;
-                        oor += 1.0f;
-                    } else if (x > 30.0f) {
-                        d += (30.0f - x) * oscale;
-                        oor += 1.0f;
-                    }
-                }
-                d += w * numrow[pdf];
-                d -= w * den;
-                if (do_l2) {
-                    d -= l2s * x;
-                    sq += x * x;
-                }
-                orow[pdf] = ok ? (h16)(-d) : (h16)0.0f;  // loss gradient = -deriv
+#pragma unroll
+            for (int f = 0; f < PAIR; ++f) {
+                if (f >= nf2) break;
+                const float x = (float)nnet[(row0 + (long long)(t + f) * r.stride) * r.ld + pdf];
+                const float gv = acc[f] * expf(fmaxf(-30.0f, fminf(30.0f, x)));  // kernel_apply_exp
+                gam[f * P + pdf] = gv;
+                gpart[f] += gv;
             }
         }
-        __syncthreads();
+#pragma unroll
+        for (int f = 0; f < PAIR; ++f) {
+            if (f >= nf2) break;
+            const int tf = t + f;
+            // the frame's occupation sums to one (alpha and beta carry arbitrary
+            // per-frame factors, see den_bwd_body): normalise in a fixed order
+            const float gsum = block_sum<DEN_WAVES>(gpart[f], red);
+            const float ginv = gsum > 0.0f ? 1.0f / gsum : 0.0f;
+            float *gm = gam + f * P;
+            if (MODE == DEN_ABI) {
+                for (int pdf = tid; pdf < P; pdf += DEN_THREADS)
+                    r.post_dense[(size_t)tf * P + pdf] = gm[pdf] * ginv;
+            } else {
+                // d = (oor) + w*num - w*den - l2: -w*den first, the numerator's sparse
+                // posteriors (its pdf set) added in place, then the dense pass
+                for (int pdf = tid; pdf < P; pdf += DEN_THREADS) gm[pdf] = -(w * (gm[pdf] * ginv));
+                __syncthreads();
+                const float *nps = nf->post_sparse + (size_t)tf * NG;
+                for (int q = tid; q < NG; q += DEN_THREADS) {
+                    const int p = nf->grp_pdf[q];
+                    if (p > 0 && p <= P) gm[p - 1] = w * nps[q] + gm[p - 1];
+                }
+                __syncthreads();
+                const XT *xrow = nnet + (row0 + (long long)tf * r.stride) * r.ld;
+                h16 *orow = r.out_grad + (row0 + (long long)tf * r.stride) * r.ldg;
+                const bool even = (tf & 1) == 0;
+                for (int pdf = tid; pdf < P; pdf += DEN_THREADS) {
+                    const float x = (float)xrow[pdf];
+                    float d = 0.0f;
+                    if (do_oor && even) {  // chain_backward.cu:27-67
+                        if (x < -30.0f) {
+                            d += (-30.0f - x) * oscale;
+                            oor += 1.0f;
+                        } else if (x > 30.0f) {
+                            d += (30.0f - x) * oscale;
+                            oor += 1.0f;
+                        }
+                    }
+                    d += gm[pdf];
+                    if (do_l2) {
+                        d -= l2s * x;
+                        sq += x * x;
+                    }
+                    orow[pdf] = ok ? (h16)(-d) : (h16)0.0f;  // loss gradient = -deriv
+                }
+            }
+            __syncthreads();
+        }
     }
     if (MODE == DEN_PRODUCT) {
         float o = block_sum<DEN_WAVES>(oor, red);
@@ -1390,13 +1419,22 @@ void launch_den_post(const DenDev &g, const DenRun &r, const DenX &X, bool fp32_
     hipStream_t st = kf_stream();
     const int nfb = (r.max_frames + POST_FRAMES - 1) / POST_FRAMES;
     dim3 pgrid(X.nseq * nfb);
-    size_t plds = den_post_lds_bytes(g.S, g.P, g.q.nsl);
-    if (mode == DEN_PRODUCT)
-        hipLaunchKernelGGL((k_den_post<h16, DEN_PRODUCT>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb);
-    else if (fp32_in)
-        hipLaunchKernelGGL((k_den_post<float, DEN_ABI>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb);
-    else
-        hipLaunchKernelGGL((k_den_post<h16, DEN_ABI>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb);
+    // frame pairs share the arc stream when both frames' alpha/beta fit in LDS
+    const bool pair = den_post_lds_bytes(g.S, g.P, g.q.nsl, 2) <= DEN_LDS_TOTAL;
+    size_t plds = den_post_lds_bytes(g.S, g.P, g.q.nsl, pair ? 2 : 1);
+#define KF_POST(XT_, MODE_, PAIR_) \
+    hipLaunchKernelGGL((k_den_post<XT_, MODE_, PAIR_>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb)
+    if (mode == DEN_PRODUCT) {
+        if (pair) KF_POST(h16, DEN_PRODUCT, 2);
+        else KF_POST(h16, DEN_PRODUCT, 1);
+    } else if (fp32_in) {
+        if (pair) KF_POST(float, DEN_ABI, 2);
+        else KF_POST(float, DEN_ABI, 1);
+    } else {
+        if (pair) KF_POST(h16, DEN_ABI, 2);
+        else KF_POST(h16, DEN_ABI, 1);
+    }
+#undef KF_POST
 }
 
 // ---- numerator FST host preparation (reverse CSR + pdf groups) -------------
