@@ -1013,11 +1013,14 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
     // 8-wave 256-row tiles halve the staged bytes per MFMA flop against the 4-wave
     // 128-row ones; KF_GEMM_BIG=0 selects the 4-wave family for A/B.
     static const int big = gemm_big();
+    static const int b128 = getenv("KF_GEMM_B128") ? atoi(getenv("KF_GEMM_B128")) : 0;
     int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : (big && N >= 256 ? 3 : 0));
+    if (tile == 0 && b128 && N <= 128) tile = 4;
     if (E.out8 && tile == 1) tile = 0;  // out8 needs 32-column blocks inside one wave's tile
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
         if (tile == 3) return launch<256, 256, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
+        if (tile == 4) return launch<256, 128, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 1) return launch<128, 160, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 2) return launch<256, 64, 4, 1, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);  \
         return launch<128, 128, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);               \
@@ -1049,7 +1052,7 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     static const int wbig = getenv("KF_GEMM_WBIG") ? atoi(getenv("KF_GEMM_WBIG")) : 1;
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
     if (BNc == 64) BMc = 256;
-    if (wbig && BNc == 128) BMc = 256, BNc = 256;
+    if (wbig && BNc == 128) BMc = 256, BNc = N > 128 ? 256 : 128;
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
     int splits = (512 + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
@@ -1075,6 +1078,8 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     do {                                                                                         \
         if (BMc == 256 && BNc == 256)                                                            \
             rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 256 && BNc == 128)                                                       \
+            rc = launch<256, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 160)                                                                     \
             rc = launch<128, 160, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 64)                                                                      \

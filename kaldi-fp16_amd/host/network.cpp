@@ -1116,12 +1116,45 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         set_err("conv " + L.name + ": input gradient of a 1-filter conv not supported");
                         return -1;
                     }
-                    KfOperand A2 = op_col2im(nl, dz, T);
-                    KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
-                    E.ldo2 = L.fin;  // dz of the input conv layer viewed as [(t,h) x fin]
-                    if (E.out) E.ldo = L.fin;
-                    if (!ck(kf_gemm_fused(T * L.hin, L.fin, noff * L.fout, &A2, &B2, &E), "conv dgrad"))
-                        return -1;
+                    if (L.hsub > 1 && L.hin % L.hsub == 0 && !E.out) {
+                        // strided conv: input row h' = hsub*j + pi only receives the taps
+                        // with (pi - dh) % hsub == 0, so one GEMM per residue pi skips the
+                        // (hsub-1)/hsub of the K range the plain col2im reads as zeros
+                        for (int pi = 0; pi < L.hsub; ++pi) {
+                            KfOperand A2 = op_col2im(nl, dz, T);
+                            KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
+                            int np = 0;
+                            for (int o = 0; o < noff; ++o) {
+                                const int r = pi - nl.dh[o];
+                                if (((r % L.hsub) + L.hsub) % L.hsub) continue;
+                                A2.dt[np] = -nl.dt[o];
+                                A2.dh[np] = r / L.hsub;  // exact: r is a multiple of hsub
+                                B2.dt[np] = o * L.fin;
+                                ++np;
+                            }
+                            if (!np) continue;
+                            A2.nparts = B2.nparts = np;
+                            A2.ncols = B2.ncols = np * L.fout;
+                            A2.hout = L.hin / L.hsub;
+                            A2.hmul = 1;
+                            A2.hdiv = 1;
+                            A2.nrows = T * A2.hout;
+                            KfEpilogue Ep = E;  // rows hsub*m + pi of the [(t,h) x fin] gradient
+                            Ep.out2 = (char *)E.out2 + (size_t)pi * L.fin * 2;
+                            Ep.ldo2 = (long long)L.hsub * L.fin;
+                            if (E.mask_in) Ep.mask_in = E.mask_in + (size_t)pi * L.fin / 8;
+                            if (!ck(kf_gemm_fused(T * A2.hout, L.fin, np * L.fout, &A2, &B2, &Ep),
+                                    "conv dgrad (strided)"))
+                                return -1;
+                        }
+                    } else {
+                        KfOperand A2 = op_col2im(nl, dz, T);
+                        KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
+                        E.ldo2 = L.fin;  // dz of the input conv layer viewed as [(t,h) x fin]
+                        if (E.out) E.ldo = L.fin;
+                        if (!ck(kf_gemm_fused(T * L.hin, L.fin, noff * L.fout, &A2, &B2, &E), "conv dgrad"))
+                            return -1;
+                    }
                 }
                 break;
             }
