@@ -1053,6 +1053,18 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
     if (BNc == 64) BMc = 256;
     if (wbig && BNc == 128) BMc = 256, BNc = N > 128 ? 256 : 128;
+    // tile rows: the candidate wasting the fewest padded rows of M (ties: the larger)
+    static const int wfit = getenv("KF_GEMM_WFIT") ? atoi(getenv("KF_GEMM_WFIT")) : 1;
+    if (wfit && BMc == 256 && BNc != 160) {
+        const int cands[3] = {256, BNc == 256 ? 320 : 256, 192};
+        int best = 256;
+        long long bw = (long long)(M + 255) / 256 * 256;
+        for (int c : cands) {
+            const long long w = (long long)(M + c - 1) / c * c;
+            if (w < bw) bw = w, best = c;
+        }
+        BMc = best;
+    }
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
     int splits = (512 + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
@@ -1076,7 +1088,15 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     int rc;
 #define KF_WG(AM_, BM_)                                                                          \
     do {                                                                                         \
-        if (BMc == 256 && BNc == 256)                                                            \
+        if (BMc == 320 && BNc == 256)                                                            \
+            rc = launch<320, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 192 && BNc == 256)                                                       \
+            rc = launch<192, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 192 && BNc == 128)                                                       \
+            rc = launch<192, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 192 && BNc == 64)                                                        \
+            rc = launch<192, 64, 4, 1, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 256 && BNc == 256)                                                       \
             rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BMc == 256 && BNc == 128)                                                       \
             rc = launch<256, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
