@@ -519,8 +519,8 @@ struct StatePre {  // alpha' row prefetch (S <= DEN_MAXS * DEN_THREADS)
 // fwd / bwd: fixed part (va or vb, xe, len/off/coff); the rest of the 160 KiB LDS
 // holds resident arc records
 #define DEN_LDS_TOTAL (160 * 1024)
-static size_t den_rec_fixed_bytes(int S, int P, int nsl) {
-    return (size_t)4 * (64 + (size_t)S + P + (P & 1) + 2 * (size_t)nsl + 128 * (size_t)nsl +
+static size_t den_rec_fixed_bytes(int S, int P, int nsl, int ns = 1) {
+    return (size_t)4 * (64 + (size_t)ns * (S + P + (P & 1)) + 2 * (size_t)nsl + 128 * (size_t)nsl +
                         nsl + 2) + 64;
 }
 static size_t den_post_lds_bytes(int S, int P, int nslq, int pair = 1) {
@@ -547,9 +547,10 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 }
 
 struct DenX {
-    float *buf;     // [nseq][2][G][blk]; blk = spg*64 + 64 (tail: lane 0 = partial sum)
+    float *buf;     // [nseq][2][G][blk]; blk = ns*spg*64 + 64 (tail: lane s = partial sum of s)
     unsigned *cnt;  // [nseq] arrivals, then [1] timeout word (zeroed before each launch)
-    int G, lgG, spg, blk, nseq;
+    int G, lgG, spg, blk, nseq;  // nseq: exchange units (groups of ns sequences)
+    int ns, nseqs;               // sequences per unit, sequences in all
     unsigned cache_f, cache_b;  // LDS bytes for resident arc records (fwd / bwd kernels)
     unsigned lds_f, lds_b;      // dynamic LDS of the fwd / bwd kernels
 };
@@ -565,18 +566,20 @@ __device__ __forceinline__ void den_map(const DenX &X, int &seq, int &gi) {
 }
 
 // publish: the payload's sc1 stores are drained by every wave; wave 0 stores the
-// tail {psum} and one lane adds the arrival
-__device__ __forceinline__ void den_publish(const DenX &X, float *tail, const float *red, int seq) {
+// tail {psum of each of the NS sequences} and one lane adds the arrival
+template <int NS>
+__device__ __forceinline__ void den_publish(const DenX &X, float *tail, const float *red, int unit) {
     const int tid = threadIdx.x, lane = tid & 63;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid < 64) {
         float ps = 0.f;
+        const int s = lane < NS ? lane : 0;
 #pragma unroll
-        for (int w2 = 0; w2 < DEN_WAVES; ++w2) ps += red[w2];
-        st_sc1(tail + lane, lane == 0 ? ps : 0.0f);
+        for (int w2 = 0; w2 < DEN_WAVES; ++w2) ps += red[s * DEN_WAVES + w2];
+        st_sc1(tail + lane, lane < NS ? ps : 0.0f);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[seq], 1u, RLX_AGENT);
+        if (lane == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[unit], 1u, RLX_AGENT);
     }
 }
 // wait for `target` arrivals (one lane polls); false on timeout, uniform
@@ -603,33 +606,44 @@ __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     return *lds_flag != 0;
 }
-// the G partial sums of buffer `buf` in block order (every lane: same value)
-__device__ __forceinline__ float den_gather_psum(const DenX &X, int seq, int buf) {
+// the G partial sums of sequence s in buffer `buf`, in block order (every lane: same value)
+__device__ __forceinline__ float den_gather_psum(const DenX &X, int unit, int buf, int s) {
     const int lane = threadIdx.x & 63;
     float v = 0.0f;
-    if (lane < X.G) v = ld_sc1(X.buf + (((size_t)seq * 2 + buf) * X.G + lane) * X.blk + X.spg * 64);
-    float s = 0.0f;
-    for (int g2 = 0; g2 < X.G; ++g2) s += __shfl(v, g2, 64);
-    return s;
+    if (lane < X.G)
+        v = ld_sc1(X.buf + (((size_t)unit * 2 + buf) * X.G + lane) * X.blk + X.ns * X.spg * 64 + s);
+    float sum = 0.0f;
+    for (int g2 = 0; g2 < X.G; ++g2) sum += __shfl(v, g2, 64);
+    return sum;
 }
-// all exchanged slices of buffer `buf`, scattered to their states: f(state, value)
-template <class F>
-__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, int nsl,
+// all exchanged slices of buffer `buf` for the NS sequences, scattered to their
+// states: f(s, state, value, initp, owner, slot); all loads in flight at once
+template <int NS, class F>
+__device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, int nsl,
                                             const int *perm, const float *initp, F f) {
-    const int tid = threadIdx.x, n = nsl * 64;
-    const float *xb = X.buf + ((size_t)seq * 2 + buf) * X.G * X.blk;
-    float v[DEN_MAXS];
+    int tid = threadIdx.x;
+    // opaque to the optimiser: the per-slot addresses below are rebuilt every frame
+    // instead of being hoisted out of the frame loop as 64-bit values (16 of them
+    // for NS = 2 spill at the 128-VGPR budget of a 1024-thread block)
+    asm volatile("" : "+v"(tid));
+    const int n = nsl * 64;
+    const float *xb = X.buf + ((size_t)unit * 2 + buf) * X.G * X.blk;
 #pragma unroll
-    for (int m = 0; m < DEN_MAXS; ++m) {  // all loads in flight at once, unconditionally
-        const int c = min(tid + m * DEN_THREADS, n - 1), j = c >> 6;
-        v[m] = ld_sc1(xb + (size_t)(j & (X.G - 1)) * X.blk + (j >> X.lgG) * 64 + (c & 63));
-    }
+    for (int q = 0; q < NS; ++q) {  // one sequence at a time: DEN_MAXS values live
+        float v[DEN_MAXS];
 #pragma unroll
-    for (int m = 0; m < DEN_MAXS; ++m) {
-        const int c = tid + m * DEN_THREADS;
-        if (c < n) {
-            const int st = perm[c];
-            if (st >= 0) f(st, v[m], initp[c], (c >> 6) & (X.G - 1), c);
+        for (int m = 0; m < DEN_MAXS; ++m) {  // unconditional loads (index clamped)
+            const int c = min(tid + m * DEN_THREADS, n - 1), j = c >> 6;
+            v[m] = ld_sc1(xb + (size_t)(j & (X.G - 1)) * X.blk + (size_t)q * X.spg * 64 +
+                          (j >> X.lgG) * 64 + (c & 63));
+        }
+#pragma unroll
+        for (int m = 0; m < DEN_MAXS; ++m) {
+            const int c = tid + m * DEN_THREADS;
+            if (c < n) {
+                const int st = perm[c];
+                if (st >= 0) f(q, st, v[m], initp[c], (c >> 6) & (X.G - 1), c);
+            }
         }
     }
 }
@@ -650,6 +664,25 @@ __device__ __forceinline__ float sell_slice(const uint2 *arcs, int len, int off,
             acc += term(rr[i].x & 0xFFFF, rr[i].x >> 16, __uint_as_float(rr[i].y));
     }
     return acc;
+}
+
+// the same pass for NS sequences sharing the records: acc[q] += term(q, f1, f2, tp)
+template <int NS, class Term>
+__device__ __forceinline__ void sell_slice_ns(const uint2 *arcs, int len, int off, int lane,
+                                              float (&acc)[NS], Term term) {
+    const uint2 *e = arcs + (size_t)off * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) acc[q] = 0.f;
+    for (int k = 0; k < len; k += 8) {  // 8 records in flight per lane (len is a multiple of 8)
+        uint2 rr[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int q = 0; q < NS; ++q)
+                acc[q] += term(q, rr[i].x & 0xFFFF, rr[i].x >> 16, __uint_as_float(rr[i].y));
+    }
 }
 
 // Per-block SELL state in LDS: len/off of every slice, and the arc records of this
@@ -697,121 +730,170 @@ __device__ __forceinline__ SellLds stage_sell(const SellDev &T, int gi, int G, i
     return L;
 }
 
-// Forward pass (chain_den.cu:583-620), G blocks per sequence: block gi computes
-// alpha[t+1] for the destination rows of slices gi, gi+G, ... and all blocks
-// rebuild the full alpha'[t+1] in LDS from the exchanged slices. alpha' of every
-// frame goes to HBM for the backward kernel.
-template <typename XT>
+// Forward pass (chain_den.cu:583-620), G blocks per exchange unit of NS sequences:
+// block gi computes alpha[t+1] for the destination rows of slices gi, gi+G, ... of
+// every sequence of its unit (the NS sequences share each arc record read), and all
+// blocks rebuild the full alpha'[t+1] in LDS from the exchanged slices. alpha' of
+// every frame goes to HBM for the posterior kernel. Ragged units: a sequence past
+// its last frame stops updating (its alpha'[T] stays in LDS for the total).
+template <typename XT, int NS>
 __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
-                                             unsigned char *smem, int seq, int gi) {
+                                             unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int G = X.G, nsl = g.f.nsl;
+    const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);          // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;        // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;      // [S] alpha'[t]
-    float *xe = va + S;                                    // [P] exp(clamp(x))
-    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + P + (P & 1));
+    float *va = reinterpret_cast<float *>(smem) + 64;      // [NS][S] alpha'[t]
+    float *xe = va + NS * S;                               // [NS][PP] exp(clamp(x))
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
     const int nk = (nsl - gi + G - 1) / G;                 // slices owned by this block
 
-    const int T = r.frames[seq];
-    const long long row0 = r.row0[seq];
+    int Ts[NS];
+    long long r0[NS];
+    int Tmax = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const int sq = unit * NS + q;
+        Ts[q] = sq < X.nseqs ? r.frames[sq] : 0;
+        r0[q] = sq < X.nseqs ? r.row0[sq] : 0;
+        Tmax = max(Tmax, Ts[q]);
+    }
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const int rs = nsl * 64;  // stored rows are in slice order: contiguous, whole lines
-    float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rs;
-    float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
     const float leaky = r.leaky;
+    auto astore = [&](int q) { return r.alpha_store + (size_t)(unit * NS + q) * (r.max_frames + 1) * rs; };
+    auto asum = [&](int q) { return r.asum_store + (size_t)(unit * NS + q) * (r.max_frames + 1); };
 
     const SellLds F = stage_sell(g.f, gi, G, nk, sbase, X.cache_f);
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
-    float as = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
-    for (int s = tid; s < S; s += DEN_THREADS) va[s] = g.init[s] + as * leaky * g.init[s];
-    if (gi == 0)
-        for (int c = tid; c < rs; c += DEN_THREADS)
-            __builtin_nontemporal_store(F.initp[c] + as * leaky * F.initp[c], astore + c);
-    if (gi == 0 && tid == 0) {
-        asum[0] = as;
-        r.stats[(size_t)seq * 8 + 3] = 0.0f;  // accumulated by k_den_bwd
-        r.stats[(size_t)seq * 8 + 6] = 0.0f;
-    }
-    RowPre<XT> pre;
-    if (T > 0) {
-        pre.fetch(nnet + row0 * r.ld, P);
+    const float as0 = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
+    float as[NS];
 #pragma unroll
-        for (int i = 0; i < DEN_MAXPT; ++i) {
-            int p = tid + i * DEN_THREADS;
-            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));  // kernel_apply_exp
+    for (int q = 0; q < NS; ++q) {
+        as[q] = as0;
+        for (int s = tid; s < S; s += DEN_THREADS) va[q * S + s] = g.init[s] + as0 * leaky * g.init[s];
+        if (gi == 0 && unit * NS + q < X.nseqs) {
+            float *a0 = astore(q);
+            for (int c = tid; c < rs; c += DEN_THREADS)
+                __builtin_nontemporal_store(F.initp[c] + as0 * leaky * F.initp[c], a0 + c);
+            if (tid == 0) {
+                asum(q)[0] = as0;
+                r.stats[(size_t)(unit * NS + q) * 8 + 3] = 0.0f;  // accumulated by k_den_post
+                r.stats[(size_t)(unit * NS + q) * 8 + 6] = 0.0f;
+            }
         }
     }
-    __syncthreads();
-    const bool tr = r.trace && seq == 0 && gi == 0 && tid == 0;
-#define DEN_TP(i) \
-    if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
-    for (int t = 0; t < T; ++t) {
-        DEN_TP(0);
-        const int buf = (t + 1) & 1;
-        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
-        const bool scale = as > 0.0f;
-        const float inv = scale ? 1.0f / as : 1.0f;
-        part = 0.f;
-        auto term = [&](int src, int pdf, float tp) { return va[src] * tp * xe[pdf]; };
-        for (int k = wave; k < nk; k += DEN_WAVES) {
-            const int j = gi + G * k;
-            const int st = F.perm[j * 64 + lane];
-            const float acc = (k < F.kc) ? sell_slice(F.cache, F.len[j], F.coff[k], lane, term)
-                                         : sell_slice(g.f.arc, F.len[j], F.off[j], lane, term);
-            float v = (st >= 0) ? (scale ? acc * inv : acc) : 0.0f;
-            st_sc1(blk + k * 64 + lane, v);
-            part += v;
-        }
-        DEN_TP(1);
-        part = wave_sum(part);
-        if (lane == 0) red[wave] = part;
-        den_publish(X, blk + X.spg * 64, red, seq);
-        DEN_TP(2);
-        if (t + 1 < T) pre.fetch(nnet + (row0 + (long long)(t + 1) * r.stride) * r.ld, P);
-        DEN_TP(3);
-        if (!den_wait(X, seq, (unsigned)(G * (t + 1)), flag)) return;
-        DEN_TP(4);
-        const float as1 = den_gather_psum(X, seq, buf);
-        DEN_TP(5);
-        float *an = astore + (size_t)(t + 1) * rs;
-        den_consume(X, seq, buf, nsl, F.perm, F.initp, [&](int st, float v, float ip, int owner, int c) {
-            float a = v + as1 * leaky * ip;
-            va[st] = a;
-            if (owner == gi) __builtin_nontemporal_store(a, an + c);  // keep L2 for the arcs
-        });
-        DEN_TP(6);
-        if (t + 1 < T) {
+    RowPre<XT> pre[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+        if (Ts[q] > 0) {
+            pre[q].fetch(nnet + r0[q] * r.ld, P);
 #pragma unroll
             for (int i = 0; i < DEN_MAXPT; ++i) {
                 int p = tid + i * DEN_THREADS;
-                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+                if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));  // kernel_apply_exp
             }
         }
-        if (gi == 0 && tid == 0) asum[t + 1] = as1;
-        as = as1;
+    __syncthreads();
+    const bool tr = r.trace && unit == 0 && gi == 0 && tid == 0;
+#define DEN_TP(i) \
+    if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
+    for (int t = 0; t < Tmax; ++t) {
+        DEN_TP(0);
+        const int buf = (t + 1) & 1;
+        float *blk = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
+        float inv[NS], pq[NS];
+        bool live[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            live[q] = t < Ts[q];
+            inv[q] = as[q] > 0.0f ? 1.0f / as[q] : 1.0f;
+            pq[q] = 0.f;
+        }
+        auto term = [&](int q, int src, int pdf, float tp) { return va[q * S + src] * tp * xe[q * PP + pdf]; };
+        for (int k = wave; k < nk; k += DEN_WAVES) {
+            const int j = gi + G * k;
+            const int st = F.perm[j * 64 + lane];
+            float acc[NS];
+            if (k < F.kc) sell_slice_ns<NS>(F.cache, F.len[j], F.coff[k], lane, acc, term);
+            else sell_slice_ns<NS>(g.f.arc, F.len[j], F.off[j], lane, acc, term);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                const float v = (st >= 0 && live[q]) ? acc[q] * inv[q] : 0.0f;
+                st_sc1(blk + (size_t)q * X.spg * 64 + k * 64 + lane, v);
+                pq[q] += v;
+            }
+        }
+        DEN_TP(1);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const float w = wave_sum(pq[q]);
+            if (lane == 0) red[q * DEN_WAVES + wave] = w;
+        }
+        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, red, unit);
+        DEN_TP(2);
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+            if (t + 1 < Ts[q]) pre[q].fetch(nnet + (r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
+        DEN_TP(3);
+        if (!den_wait(X, unit, (unsigned)(G * (t + 1)), flag)) return;
+        DEN_TP(4);
+        float as1[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) as1[q] = den_gather_psum(X, unit, buf, q);
+        DEN_TP(5);
+        den_consume<NS>(X, unit, buf, nsl, F.perm, F.initp,
+                        [&](int q, int st, float v, float ip, int owner, int c) {
+                            if (!live[q]) return;
+                            const float a = v + as1[q] * leaky * ip;
+                            va[q * S + st] = a;
+                            if (owner == gi)  // keep L2 for the arcs
+                                __builtin_nontemporal_store(a, astore(q) + (size_t)(t + 1) * rs + c);
+                        });
+        DEN_TP(6);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (t + 1 < Ts[q]) {
+#pragma unroll
+                for (int i = 0; i < DEN_MAXPT; ++i) {
+                    int p = tid + i * DEN_THREADS;
+                    if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));
+                }
+            }
+            if (live[q]) {
+                if (gi == 0 && tid == 0) asum(q)[t + 1] = as1[q];
+                as[q] = as1[q];
+            }
+        }
         __syncthreads();
         DEN_TP(7);
     }
 #undef DEN_TP
     if (gi != 0) return;
     // total_prob = sum(alpha'[T]); log_correction = sum_{t<T} log(alpha_sum[t])
-    part = 0.f;
-    for (int s = tid; s < S; s += DEN_THREADS) part += va[s];
-    const float total = block_sum<DEN_WAVES>(part, red);
-    double lc = 0.0;
-    for (int t = tid; t < T; t += DEN_THREADS) {
-        float a = asum[t];
-        if (a > 0.0f) lc += log((double)a);
-    }
-    double *redd = reinterpret_cast<double *>(smem) + 8;  // red[16..31]
-    __syncthreads();
-    lc = block_sum_d<DEN_WAVES>(lc, redd);
-    if (tid == 0) {
-        r.den_out[seq * 2 + 0] = total;
-        r.den_out[seq * 2 + 1] = (float)(log((double)total) + lc);
-        r.stats[(size_t)seq * 8 + 1] = r.den_out[seq * 2 + 1];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const int sq = unit * NS + q;
+        if (sq >= X.nseqs) break;
+        part = 0.f;
+        for (int s = tid; s < S; s += DEN_THREADS) part += va[q * S + s];
+        const float total = block_sum<DEN_WAVES>(part, red);
+        double lc = 0.0;
+        for (int t = tid; t < Ts[q]; t += DEN_THREADS) {
+            float a = asum(q)[t];
+            if (a > 0.0f) lc += log((double)a);
+        }
+        double *redd = reinterpret_cast<double *>(smem) + 8;  // red[16..31]
+        __syncthreads();
+        lc = block_sum_d<DEN_WAVES>(lc, redd);
+        if (tid == 0) {
+            r.den_out[sq * 2 + 0] = total;
+            r.den_out[sq * 2 + 1] = (float)(log((double)total) + lc);
+            r.stats[(size_t)sq * 8 + 1] = r.den_out[sq * 2 + 1];
+        }
+        __syncthreads();
     }
 }
 template <typename XT>
@@ -819,101 +901,142 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int seq, gi;
     den_map(X, seq, gi);
-    den_fwd_body<XT>(g, r, X, smem, seq, gi);
+    den_fwd_body<XT, 1>(g, r, X, smem, seq, gi);
 }
 
 // Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per
-// sequence: beta'[t] over the source rows of this block's slices (exchanged),
+// unit: beta'[t] over the source rows of this block's slices (exchanged),
 // beta[t] = beta'[t] + leaky*<init, beta'[t]>; beta[t] for t >= 1 goes to HBM for
 // k_den_post. The reference scales beta'[t] by 1/sum(alpha[t]) and starts from
 // 1/total_prob; any positive per-frame factor gives the same posteriors once
 // k_den_post normalises each frame (the den posteriors of a frame sum to one:
 // they are d log p / d x_t), so this pass scales by 1/<init, beta'[t+1]> and
 // starts from ones — it needs nothing from the forward pass and runs beside it.
-template <typename XT>
+// Ragged units run from the longest sequence's last frame; a shorter sequence
+// joins at its own last frame.
+template <typename XT, int NS>
 __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, const DenX &X,
-                                             unsigned char *smem, int seq, int gi) {
+                                             unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int G = X.G, nsl = g.b.nsl;
+    const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);      // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;    // [32]
-    float *vb = reinterpret_cast<float *>(smem) + 64;  // [S] beta[t+1]
-    float *xe = vb + S;                                // [P] exp(clamp(x))
-    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + P + (P & 1));
+    float *vb = reinterpret_cast<float *>(smem) + 64;  // [NS][S] beta[t+1]
+    float *xe = vb + NS * S;                           // [NS][PP] exp(clamp(x))
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
     const int nk = (nsl - gi + G - 1) / G;
 
-    const int T = r.frames[seq];
-    const long long row0 = r.row0[seq];
+    int Ts[NS];
+    long long r0[NS];
+    int Tmax = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const int sq = unit * NS + q;
+        Ts[q] = sq < X.nseqs ? r.frames[sq] : 0;
+        r0[q] = sq < X.nseqs ? r.row0[sq] : 0;
+        Tmax = max(Tmax, Ts[q]);
+    }
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const int rs = nsl * 64;
-    float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rs;
+    auto bstore = [&](int q) { return r.beta_store + (size_t)(unit * NS + q) * (r.max_frames + 1) * rs; };
     const float leaky = r.leaky;
 
     const SellLds B = stage_sell(g.b, gi, G, nk, sbase, X.cache_b);
-    // BetaDashLastFrame up to the per-frame factor: beta'[T] = 1, <init, 1> = 1
+    // BetaDashLastFrame up to the per-frame factor: beta'[T] = 1, <init, 1> = sum(init)
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
-    float nrm = block_sum<DEN_WAVES>(part, red);
-    float tb = leaky * nrm;
-    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = 1.0f + tb;
-    if (gi == 0)
-        for (int c = tid; c < rs; c += DEN_THREADS)
-            __builtin_nontemporal_store(1.0f + tb, bstore + (size_t)T * rs + c);
-    RowPre<XT> pre;
-    if (T > 0) {
-        pre.fetch(nnet + (row0 + (long long)(T - 1) * r.stride) * r.ld, P);
+    const float n0 = block_sum<DEN_WAVES>(part, red);
+    float nrm[NS];
+    RowPre<XT> pre[NS];
 #pragma unroll
-        for (int i = 0; i < DEN_MAXPT; ++i) {
-            int p = tid + i * DEN_THREADS;
-            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+    for (int q = 0; q < NS; ++q) {
+        nrm[q] = n0;
+        for (int s = tid; s < S; s += DEN_THREADS) vb[q * S + s] = 1.0f + leaky * n0;
+        if (gi == 0 && unit * NS + q < X.nseqs) {
+            float *bT = bstore(q) + (size_t)Ts[q] * rs;
+            for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(1.0f + leaky * n0, bT + c);
         }
-    }
-    __syncthreads();
-    for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
-        const int buf = t & 1;
-        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
-        const bool scale = nrm > 0.0f;
-        const float inv = scale ? 1.0f / nrm : 1.0f;
-        part = 0.f;
-        auto term = [&](int dst, int pdf, float tp) { return vb[dst] * tp * xe[pdf]; };
-        for (int k = wave; k < nk; k += DEN_WAVES) {  // kernel_den_backward_transitions
-            const int j = gi + G * k;
-            const int st = B.perm[j * 64 + lane];
-            const float acc = (k < B.kc) ? sell_slice(B.cache, B.len[j], B.coff[k], lane, term)
-                                         : sell_slice(g.b.arc, B.len[j], B.off[j], lane, term);
-            float bd = (st >= 0) ? (scale ? acc * inv : acc) : 0.0f;
-            st_sc1(blk + k * 64 + lane, bd);
-            part += B.initp[j * 64 + lane] * bd;
-        }
-        part = wave_sum(part);
-        if (lane == 0) red[wave] = part;
-        den_publish(X, blk + X.spg * 64, red, seq);
-        if (t > 0) pre.fetch(nnet + (row0 + (long long)(t - 1) * r.stride) * r.ld, P);
-        if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
-        nrm = den_gather_psum(X, seq, buf);  // <init, beta'[t]>: next frame's factor
-        tb = leaky * nrm;
-        float *bt = bstore + (size_t)t * rs;
-        den_consume(X, seq, buf, nsl, B.perm, B.initp, [&](int st, float v, float, int owner, int c) {
-            const float b = v + tb;
-            vb[st] = b;
-            if (t > 0 && owner == gi) __builtin_nontemporal_store(b, bt + c);
-        });
-        if (t > 0) {
+        if (Ts[q] > 0) {
+            pre[q].fetch(nnet + (r0[q] + (long long)(Ts[q] - 1) * r.stride) * r.ld, P);
 #pragma unroll
             for (int i = 0; i < DEN_MAXPT; ++i) {
                 int p = tid + i * DEN_THREADS;
-                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+                if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = Tmax - 1, it = 0; t >= 0; --t, ++it) {
+        const int buf = t & 1;
+        float *blk = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
+        float inv[NS], pq[NS];
+        bool live[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            live[q] = t < Ts[q];
+            inv[q] = nrm[q] > 0.0f ? 1.0f / nrm[q] : 1.0f;
+            pq[q] = 0.f;
+        }
+        auto term = [&](int q, int dst, int pdf, float tp) { return vb[q * S + dst] * tp * xe[q * PP + pdf]; };
+        for (int k = wave; k < nk; k += DEN_WAVES) {  // kernel_den_backward_transitions
+            const int j = gi + G * k;
+            const int st = B.perm[j * 64 + lane];
+            float acc[NS];
+            if (k < B.kc) sell_slice_ns<NS>(B.cache, B.len[j], B.coff[k], lane, acc, term);
+            else sell_slice_ns<NS>(g.b.arc, B.len[j], B.off[j], lane, acc, term);
+            const float ipj = B.initp[j * 64 + lane];
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                const float bd = (st >= 0 && live[q]) ? acc[q] * inv[q] : 0.0f;
+                st_sc1(blk + (size_t)q * X.spg * 64 + k * 64 + lane, bd);
+                pq[q] += ipj * bd;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const float w = wave_sum(pq[q]);
+            if (lane == 0) red[q * DEN_WAVES + wave] = w;
+        }
+        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, red, unit);
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+            if (live[q] && t > 0) pre[q].fetch(nnet + (r0[q] + (long long)(t - 1) * r.stride) * r.ld, P);
+        if (!den_wait(X, unit, (unsigned)(G * (it + 1)), flag)) return;
+        float tb[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (live[q]) nrm[q] = den_gather_psum(X, unit, buf, q);  // <init, beta'[t]>: next factor
+            tb[q] = leaky * nrm[q];
+        }
+        den_consume<NS>(X, unit, buf, nsl, B.perm, B.initp,
+                        [&](int q, int st, float v, float, int owner, int c) {
+                            if (!live[q]) return;
+                            const float b = v + tb[q];
+                            vb[q * S + st] = b;
+                            if (t > 0 && owner == gi)
+                                __builtin_nontemporal_store(b, bstore(q) + (size_t)t * rs + c);
+                        });
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (live[q] && t > 0) {
+#pragma unroll
+                for (int i = 0; i < DEN_MAXPT; ++i) {
+                    int p = tid + i * DEN_THREADS;
+                    if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));
+                }
             }
         }
         __syncthreads();
     }
 }
+
 // Forward and backward recursions of every sequence in one launch: blocks of the
 // first half run alpha with exchange XF, the second half beta with XB (the two
 // passes are independent, see den_bwd_body). One launch keeps all 2*nseq*G blocks
 // co-resident, which the bounded exchange polls rely on; the XCD grouping of
 // den_map is kept (G consecutive ids share an XCD).
-template <typename XT>
+template <typename XT, int NS>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const DenRun r, const DenX XF,
                                                         const DenX XB) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -922,9 +1045,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
     if (nb % 8 == 0 && (nb / 8) % XF.G == 0) w = (b % 8) * (nb / 8) + b / 8;
     const bool bwd = w >= half;
     const int inner = bwd ? w - half : w;
-    const int seq = inner >> XF.lgG, gi = inner & (XF.G - 1);
-    if (bwd) den_bwd_body<XT>(g, r, XB, smem, seq, gi);
-    else den_fwd_body<XT>(g, r, XF, smem, seq, gi);
+    const int unit = inner >> XF.lgG, gi = inner & (XF.G - 1);
+    if (bwd) den_bwd_body<XT, NS>(g, r, XB, smem, unit, gi);
+    else den_fwd_body<XT, NS>(g, r, XF, smem, unit, gi);
 }
 
 // Posteriors (kernel_den_posteriors, chain_den.cu:253-280) for every (sequence,
@@ -1344,14 +1467,17 @@ struct DenXBuf {
         if (buf) hipFree(buf);
         if (cnt) hipFree(cnt);
     }
-    bool make(const DenDev &g, int nseq, int G, DenX &X) {
+    // nseq sequences in units of ns (ns = 1 or 2 sequences per block)
+    bool make(const DenDev &g, int nseq, int G, DenX &X, int ns = 1) {
         X.G = G;
-        X.nseq = nseq;
+        X.ns = ns;
+        X.nseqs = nseq;
+        X.nseq = (nseq + ns - 1) / ns;
         X.lgG = G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
         X.spg = (g.f.nsl + G - 1) / G;
-        X.blk = X.spg * 64 + 64;
-        const size_t fixed_f = den_rec_fixed_bytes(g.S, g.P, g.f.nsl);
-        const size_t fixed_b = den_rec_fixed_bytes(g.S, g.P, g.b.nsl);
+        X.blk = ns * X.spg * 64 + 64;
+        const size_t fixed_f = den_rec_fixed_bytes(g.S, g.P, g.f.nsl, ns);
+        const size_t fixed_b = den_rec_fixed_bytes(g.S, g.P, g.b.nsl, ns);
         // resident arc records are opt-in (KF_DEN_CACHE=1): measured on MI355X they do not
         // shorten the recursion (it is bound by the LDS gathers, not the L2 stream) and the
         // full-LDS request keeps the numerator kernel off those CUs
@@ -1363,8 +1489,8 @@ struct DenXBuf {
             }
         X.lds_f = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_f + X.cache_f);
         X.lds_b = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_b + X.cache_b);
-        size_t nb = (size_t)nseq * 2 * G * X.blk * 4;
-        size_t nc = (((size_t)nseq + 1) * 4 + 15) / 16 * 16;
+        size_t nb = (size_t)X.nseq * 2 * G * X.blk * 4;
+        size_t nc = (((size_t)X.nseq + 1) * 4 + 15) / 16 * 16;
         if (nb > buf_cap) {
             if (buf) hipFree(buf);
             buf = nullptr;
@@ -1381,12 +1507,14 @@ struct DenXBuf {
         }
         X.buf = buf;
         X.cnt = cnt;
+        units = X.nseq;
         return true;
     }
     void zero(hipStream_t st) { hipMemsetAsync(cnt, 0, cnt_cap, st); }
-    bool timed_out(hipStream_t st, int nseq) {
+    int units = 0;  // of the last make(): the timeout word follows the unit counters
+    bool timed_out(hipStream_t st, int /*nseq*/) {
         unsigned v = 0;
-        hipMemcpyAsync(&v, cnt + nseq, 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&v, cnt + units, 4, hipMemcpyDeviceToHost, st);
         hipStreamSynchronize(st);
         return v != 0;
     }
@@ -1410,15 +1538,20 @@ void launch_den_fb(const DenDev &g, const DenRun &r, const DenX &XF, DenXBuf &xf
     xbb.zero(st);
     dim3 grid(2 * XF.nseq * XF.G);
     const size_t lds = std::max(XF.lds_f, XB.lds_b);
-    if (fp32_in)
-        hipLaunchKernelGGL((k_den_fb<float>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
-    else
-        hipLaunchKernelGGL((k_den_fb<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
+#define KF_FB(XT_, NS_) hipLaunchKernelGGL((k_den_fb<XT_, NS_>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB)
+    if (XF.ns == 2) {
+        if (fp32_in) KF_FB(float, 2);
+        else KF_FB(h16, 2);
+    } else {
+        if (fp32_in) KF_FB(float, 1);
+        else KF_FB(h16, 1);
+    }
+#undef KF_FB
 }
 void launch_den_post(const DenDev &g, const DenRun &r, const DenX &X, bool fp32_in, int mode) {
     hipStream_t st = kf_stream();
     const int nfb = (r.max_frames + POST_FRAMES - 1) / POST_FRAMES;
-    dim3 pgrid(X.nseq * nfb);
+    dim3 pgrid(X.nseqs * nfb);
     // frame pairs share the arc stream when both frames' alpha/beta fit in LDS
     const bool pair = den_post_lds_bytes(g.S, g.P, g.q.nsl, 2) <= DEN_LDS_TOTAL;
     size_t plds = den_post_lds_bytes(g.S, g.P, g.q.nsl, pair ? 2 : 1);
@@ -2465,8 +2598,19 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
     double bytes = frames * (3.0 * 8.0 * c->den->num_arcs + 8.0 * dd.S + 6.0 * dd.P);
     int pd = kf_prof_start(KF_PROF_CHAIN_DEN, bytes);
     DenX X{}, XB{};
-    const int G = den_pick_G(2 * nseq);  // forward and backward blocks share the CUs
-    if (!c->xbuf.make(dd, nseq, G, X) || !c->xbuf2.make(dd, nseq, G, XB)) {
+    // forward and backward blocks share the CUs. KF_DEN_NS=2 puts two sequences in a
+    // block (G = 4), sharing every arc record read; measured on MI355X it is slower
+    // (11.6 vs 9.3 ms for 64 sequences: the G = 4 exchange and doubled LDS gathers cost
+    // more than the halved record stream), so one sequence per block is the default
+    int ns = 1, G = den_pick_G(2 * nseq);
+    {
+        static const int want = getenv("KF_DEN_NS") ? atoi(getenv("KF_DEN_NS")) : 1;
+        const int units = (nseq + 1) / 2;
+        if (want == 2 && nseq >= 2 && den_pick_G(2 * units) == 4 &&
+            den_rec_fixed_bytes(dd.S, dd.P, dd.f.nsl, 2) <= DEN_LDS_TOTAL)
+            ns = 2, G = 4;
+    }
+    if (!c->xbuf.make(dd, nseq, G, X, ns) || !c->xbuf2.make(dd, nseq, G, XB, ns)) {
         kfc_set_error("kf_chain_compute: hipMalloc failed");
         return -1;
     }
