@@ -169,8 +169,12 @@ __device__ __forceinline__ unsigned op_boff(const OpD &d, int t, int h, int kk, 
 
 template <bool KC, int TR, int MODE, int NW>
 struct Stager {
-    static constexpr int NC = TR / (8 * NW);  // 1 KiB pieces (= chunks) per thread
-    static_assert(NC * 8 * NW == TR, "tile rows must split evenly over the waves");
+    // 1 KiB pieces (= chunks) per thread; when TR / 8 pieces do not split evenly over
+    // the waves (160-row tiles on 8 waves) the last wave issues fewer (wave-uniform skip)
+    static constexpr int NP = TR / 8;
+    static constexpr int NC = (NP + NW - 1) / NW;
+    static constexpr bool EVEN = NC * NW == NP;
+    static_assert(NP * 8 == TR, "tile rows must be a multiple of 8");
     unsigned o0[NC];                    // KC: part-0 row byte offset; MN: fixed byte offset base
     unsigned o1[MODE == OP_P2 && KC ? NC : 1];  // KC/P2: part-1 row byte offset
     int th[MODE == OP_GEN ? NC : 1];    // GEN: KC packed (t<<8)|h ; MN packed part info
@@ -302,8 +306,9 @@ struct Stager {
                     }
                 }
             }
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, (__attribute__((address_space(3))) void *)(dst + q * 1024), 16, voff, 0, 0, 0);
+            if (EVEN || q < NP)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void *)(dst + q * 1024), 16, voff, 0, 0, 0);
         });
     }
 };
@@ -489,6 +494,119 @@ __device__ __forceinline__ int mx_exponent(float amax) {
     return min(max(ex - 8, -126), 126);
 }
 
+// ---------------------------------------------------------------------------
+// fused epilogue of a BM x BN tile held as 16x16 accumulators. Per-column
+// parameters go to LDS once per workgroup; then every wave stages its
+// accumulators through its own LDS region 32 rows at a time and each lane owns 8
+// consecutive columns of a row (16-byte global I/O). `smem` must hold
+// 4*BN + 32*(BN/WN + 4)*WM*WN floats; every LDS-DMA into it must have landed.
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN / WN / 16], char *smem,
+                                               const KfEpilogue &E, int M, int N, int m0, int n0,
+                                               int tid, int lane, int wave) {
+    constexpr int NW = WM * WN, NTH = 64 * NW;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    const int wm = wave / WN, wn = wave % WN;
+    wait_vmcnt<0>();
+    __syncthreads();
+    float *prm = reinterpret_cast<float *>(smem);
+    for (int c = tid; c < BN; c += NTH) {
+        const int n = n0 + c;
+        const bool in = n < N;
+        prm[c] = (E.bias && in) ? (float)((const h16 *)E.bias)[n] : 0.f;
+        prm[BN + c] = (E.scale && in) ? E.scale[n] : 0.f;
+        prm[2 * BN + c] = (E.scale && in) ? E.shift[n] : 0.f;
+        prm[3 * BN + c] = (E.scale2 && in) ? E.scale2[n] : 1.f;
+    }
+    __syncthreads();
+    const EpiCols P{prm, prm + BN, prm + 2 * BN, prm + 3 * BN};
+    constexpr int LDT = WTN + 4;
+    float *st = prm + 4 * BN + wave * 32 * LDT;
+    constexpr int CG = WTN / 8;
+    constexpr int ITEMS = 32 * CG / 64;
+    static_assert(ITEMS * 64 == 32 * CG, "items per lane");
+    static_assert(TM % 2 == 0, "epilogue stages 32 rows");
+    // row operands (residual, old C, input mask) of 32-row chunk ic + 1 are in
+    // flight while chunk ic is processed (two register slots)
+    half8 rres[2][ITEMS], cold[2][ITEMS];
+    unsigned mb[2][ITEMS];
+    auto prefetch = [&](auto ICc) {
+        constexpr int icp = decltype(ICc)::value, sl = icp & 1;
+        static_for<ITEMS>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+            const int m = m0 + wm * WTM + icp * 32 + r, n = n0 + wn * WTN + 8 * cg;
+            const bool ok = m < M && n < N;
+            rres[sl][k] = half8{};
+            cold[sl][k] = half8{};
+            mb[sl][k] = 0xFFu;
+            if (ok && E.resid) rres[sl][k] = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
+            if (ok && E.beta != 0.f) cold[sl][k] = load_h8((const h16 *)E.out + (long long)m * E.ldo + n);
+            if (ok && E.mask_in) mb[sl][k] = E.mask_in[((long long)m * E.ldo2 + n) >> 3];
+        });
+    };
+    prefetch(std::integral_constant<int, 0>{});
+    static_for<TM / 2>([&](auto IC) {
+        constexpr int ic = decltype(IC)::value, sl = ic & 1;
+        if constexpr (ic + 1 < TM / 2) prefetch(std::integral_constant<int, ic + 1>{});
+        static_for<2>([&](auto I2) {
+            static_for<TN>([&](auto J) {
+                const int c = J * 16 + (lane & 15);
+                static_for<4>([&](auto EI) {
+                    const int r = I2 * 16 + 4 * (lane >> 4) + EI;
+                    st[r * LDT + c] = acc[2 * ic + I2][J][decltype(EI)::value];
+                });
+            });
+        });
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        static_for<ITEMS>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+            const int nl = wn * WTN + 8 * cg;
+            const int m = m0 + wm * WTM + ic * 32 + r, n = n0 + nl;
+            const bool live = m < M && n < N;
+            float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (live) {
+                float4v x0 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg);
+                float4v x1 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = x0[e];
+                    v[e + 4] = x1[e];
+                }
+                epilogue8(E, P, m, n, nl, v, cold[sl][k], rres[sl][k], mb[sl][k]);
+            }
+            if constexpr (CG % 4 == 0) {
+                // MXFP8 copy: the 4 lanes l..l+3 (l % 4 == 0) hold one 32-column block
+                if (E.out8) {
+                    float amax = 0.f;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+                    amax = fmaxf(amax, __shfl_xor(amax, 1));
+                    amax = fmaxf(amax, __shfl_xor(amax, 2));
+                    const int ex = mx_exponent(amax);
+                    const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
+                    float q[8];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) q[e] = v[e] * inv;
+                    const uint2 pk = pack_e4m3x8(q);
+                    if (live) {
+                        *reinterpret_cast<uint2 *>((uint8_t *)E.out8 + (long long)m * E.ldo8 + n) = pk;
+                        if ((lane & 3) == 0) E.scale8[(long long)m * (E.ldo8 >> 5) + (n >> 5)] = (uint8_t)(ex + 127);
+                    }
+                }
+            }
+        });
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    });
+}
+
 template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE,
           int F8 = 0>
 __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int K, OpD A, OpD B,
@@ -508,6 +626,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     using SA = Stager<AKC, BM, AM, NW>;
     using SB = Stager<BKC, BN, BMODE, NW>;
     constexpr int LPT = SA::NC + SB::NC + (F8 ? SCS::SPW : 0);  // LDS-DMA per thread per stage
+    static_assert((SA::EVEN && SB::EVEN) || ST == 2, "uneven stagers need the vmcnt(0) ring");
     static_assert(ST >= 2 && ST <= 4, "stages");
     static_assert(4 * BN * 4 + (32 * (WTN + 4) * 4) * NW <= SmemSize<BM, BN, ST, SCB>::bytes,
                   "epilogue staging");
@@ -645,100 +764,155 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
         if (do_bsum && tid < BN && n0 + tid < N)
             G.bias_slab[(long long)blockIdx.y * N + n0 + tid] = bsum;
     } else {
-        // Per-column parameters go to LDS once per workgroup; then every wave
-        // stages its accumulators through its own LDS region 32 rows at a time and
-        // each lane owns 8 consecutive columns of a row (16-byte global I/O).
-        wait_vmcnt<0>();
-        __syncthreads();
-        float *prm = reinterpret_cast<float *>(smem);
-        for (int c = tid; c < BN; c += NTH) {
-            const int n = n0 + c;
-            const bool in = n < N;
-            prm[c] = (E.bias && in) ? (float)((const h16 *)E.bias)[n] : 0.f;
-            prm[BN + c] = (E.scale && in) ? E.scale[n] : 0.f;
-            prm[2 * BN + c] = (E.scale && in) ? E.shift[n] : 0.f;
-            prm[3 * BN + c] = (E.scale2 && in) ? E.scale2[n] : 1.f;
+        fused_epilogue<BM, BN, WM, WN>(acc, smem, E, M, N, m0, n0, tid, lane, wave);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Convolution with the input halo resident in LDS (forward, and the input gradient
+// as a transposed convolution). The im2col GEMM above stages every tap's A rows
+// through LDS separately, so a 3x3 conv moves each source element ~9x from L2;
+// here a tile's source frames x heights x 64 channels land ONCE per channel chunk
+// (one LDS-DMA sweep, zero rows for the time and height padding) and every tap's
+// A fragment is read from that image at a per-tap row offset. The reduction runs
+// chunk-major, tap-minor: K-step (c, p) = 64 channels of chunk c under tap p, so
+// B (weights) still streams one 64-row slab per step through a 2-stage ring, and
+// the halo of chunk c + 1 is issued in ntaps slices alongside, into the other of
+// two halo buffers.
+//
+// Halo image: row R = f * hpos + pos holds source frame tbase + f and padded
+// height shp = idx * hmul + par, where pos = par * hpe + idx (heights de-interleaved
+// by parity when hmul = 2, so consecutive output heights read consecutive rows for
+// every tap); 128 bytes per row, 16-byte chunks XOR-swizzled like kc_off.
+// Output row m = (t, h) under tap p reads halo row
+//     (t - tbase) * hpos + h + ctap[p]
+// with ctap[p] = (dt_p - dtmin) * hpos + ((dh_p + pad) % hmul) * hpe + (dh_p + pad) / hmul.
+// ---------------------------------------------------------------------------
+struct HaloArgs {
+    const h16 *x;           // source [T x ...] rows of ld elements, heights of pw channels
+    long long ld;
+    int T, hout, hmul, hsrc, pw, pad, hpe, hpos, nf, dtmin;
+    int ntaps, nch;         // taps, 64-channel chunks per tap
+    int rows;               // halo rows per chunk image (nf * hpos)
+    int npieces;            // 1 KiB LDS-DMA pieces per image (ceil(rows / 8))
+    int slice;              // pieces issued per step (ceil(npieces / ntaps))
+    int halo_bytes;         // per image, 1 KiB multiple
+    int nbuf;               // halo images (2 when nch > 1)
+    int ctap[KF_MAX_PARTS];
+    int bshift[KF_MAX_PARTS];  // BROW: row shift of tap p's weight block (op_wrows)
+};
+
+// BROW: B is op_wrows' shifted weight rows (input gradient); the kernel then stages
+// it as a plain 64-column operand whose base moves per step (scalar), instead of
+// re-deriving every chunk's part offsets as the general stager would each step.
+template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW>
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N, OpD B, KfEpilogue E,
+                                                                    HaloArgs H, int n_mtiles,
+                                                                    int n_ntiles) {
+    constexpr int NW = WM * WN;
+    constexpr int WTM = BM / WM, WTN = BN / WN;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int B_STAGE = BN * BK * 2;
+    using SB = Stager<BKC, BN, BMODE, NW>;
+    extern __shared__ __attribute__((aligned(16))) char dsm[];
+    char *bring = dsm + H.nbuf * H.halo_bytes;  // 2 B stages after the halo images
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+
+    // XCD-aware tile order (as gemm_kernel): the N tiles of one M tile share an XCD
+    const int ntiles = n_mtiles * n_ntiles;
+    int tile = blockIdx.x;
+    if (ntiles >= 8) {
+        const int q = ntiles / 8, rmd = ntiles % 8, xcd = tile % 8, loc = tile / 8;
+        tile = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + loc;
+    }
+    const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tbase = m0 / H.hout + H.dtmin;
+
+    SB sb;
+    sb.init(B, n0, wave, lane);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(H.x), rb = make_rsrc(B.base);
+    const int K = H.ntaps * H.pw;
+
+    // halo pieces [q0, q1) of chunk c into image `img`, wave-strided
+    auto halo_issue = [&](int c, int img, int q0, int q1) {
+        char *dst = dsm + img * H.halo_bytes;
+        for (int q = q0 + wave; q < q1; q += NW) {
+            const int R = 8 * q + (lane >> 3);
+            unsigned voff = BAD;
+            if (R < H.rows) {
+                const int f = R / H.hpos, pos = R - f * H.hpos;
+                const int par = pos / H.hpe, idx = pos - par * H.hpe;
+                const int sh = idx * H.hmul + par - H.pad, t = tbase + f;
+                if ((unsigned)t < (unsigned)H.T && (unsigned)sh < (unsigned)H.hsrc) {
+                    const int kc = (lane & 7) ^ ((R >> 1) & 7);
+                    voff = (unsigned)(((long long)t * H.ld + (long long)sh * H.pw + c * BK + kc * 8) * 2);
+                }
+            }
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rx, (__attribute__((address_space(3))) void *)(dst + q * 1024), 16, voff, 0, 0, 0);
         }
-        __syncthreads();
-        const EpiCols P{prm, prm + BN, prm + 2 * BN, prm + 3 * BN};
-        constexpr int LDT = WTN + 4;
-        float *st = prm + 4 * BN + wave * 32 * LDT;
-        constexpr int CG = WTN / 8;
-        constexpr int ITEMS = 32 * CG / 64;
-        static_assert(ITEMS * 64 == 32 * CG, "items per lane");
-        static_assert(TM % 2 == 0, "epilogue stages 32 rows");
-        static_for<TM / 2>([&](auto IC) {
-            constexpr int ic = decltype(IC)::value;
-            static_for<2>([&](auto I2) {
+    };
+
+    // per-lane halo row of each 16-row group's row for tap 0 offset 0
+    int rb0[TM];
+    static_for<TM>([&](auto I) {
+        const int r = wm * WTM + I * 16 + (lane & 15);
+        const int m = min(m0 + r, M - 1);
+        const int t = m / H.hout, h = m - t * H.hout;
+        rb0[I] = (t - tbase + H.dtmin) * H.hpos + h;
+    });
+
+    float4v acc[TM][TN];
+    static_for<TM>([&](auto I) {
+        static_for<TN>([&](auto J) { acc[I][J] = float4v{0.f, 0.f, 0.f, 0.f}; });
+    });
+
+    const int steps = H.nch * H.ntaps;
+    auto issue_b = [&](int st1, char *dst) {
+        const int c1 = st1 / H.ntaps, p1 = st1 - c1 * H.ntaps;
+        if constexpr (BROW) {
+            const h16 *bb = B.base + (long long)H.bshift[p1] * B.ld + c1 * BK;
+            sb.issue(B, make_rsrc(bb), 0, BK, dst, wave, lane);
+        } else {
+            sb.issue(B, rb, p1 * H.pw + c1 * BK, K, dst, wave, lane);
+        }
+    };
+    halo_issue(0, 0, 0, H.npieces);
+    issue_b(0, bring);
+    for (int st = 0; st < steps; ++st) {
+        const int c = st / H.ntaps, p = st - c * H.ntaps;
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (st + 1 < steps) issue_b(st + 1, bring + ((st + 1) & 1) * B_STAGE);
+        if (c + 1 < H.nch) {
+            const int q0 = p * H.slice;
+            halo_issue(c + 1, (c + 1) & 1, q0, min(H.npieces, q0 + H.slice));
+        }
+        const char *ta = dsm + (H.nbuf > 1 ? (c & 1) : 0) * H.halo_bytes;
+        const char *tb = bring + (st & 1) * B_STAGE;
+        const int ct = __builtin_amdgcn_readfirstlane(H.ctap[p]);
+        static_for<BK / 32>([&](auto S) {
+            constexpr int s = decltype(S)::value;
+            half8 fa[TM], fb[TN];
+            static_for<TM>([&](auto I) {
+                const int R = rb0[I] + ct;
+                fa[I] = *reinterpret_cast<const half8 *>(ta + kc_off(R, s * 4 + (lane >> 4)));
+            });
+            static_for<TN>([&](auto J) { fb[J] = load_frag<BKC, BN>(tb, wn * WTN + J * 16, s, lane); });
+            static_for<TM>([&](auto I) {
                 static_for<TN>([&](auto J) {
-                    const int c = J * 16 + (lane & 15);
-                    static_for<4>([&](auto EI) {
-                        const int r = I2 * 16 + 4 * (lane >> 4) + EI;
-                        st[r * LDT + c] = acc[2 * ic + I2][J][decltype(EI)::value];
-                    });
+                    acc[I][J] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[I], fb[J], acc[I][J], 0, 0, 0);
                 });
             });
-            // prefetch the row operands of every item before any store
-            half8 rres[ITEMS], cold[ITEMS];
-            unsigned mb[ITEMS];
-            static_for<ITEMS>([&](auto K) {
-                constexpr int k = decltype(K)::value;
-                const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
-                const int m = m0 + wm * WTM + ic * 32 + r, n = n0 + wn * WTN + 8 * cg;
-                const bool ok = m < M && n < N;
-                rres[k] = half8{};
-                cold[k] = half8{};
-                mb[k] = 0xFFu;
-                if (ok && E.resid) rres[k] = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
-                if (ok && E.beta != 0.f) cold[k] = load_h8((const h16 *)E.out + (long long)m * E.ldo + n);
-                if (ok && E.mask_in) mb[k] = E.mask_in[((long long)m * E.ldo2 + n) >> 3];
-            });
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            static_for<ITEMS>([&](auto K) {
-                constexpr int k = decltype(K)::value;
-                const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
-                const int nl = wn * WTN + 8 * cg;
-                const int m = m0 + wm * WTM + ic * 32 + r, n = n0 + nl;
-                const bool live = m < M && n < N;
-                float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-                if (live) {
-                    float4v x0 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg);
-                    float4v x1 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg + 4);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        v[e] = x0[e];
-                        v[e + 4] = x1[e];
-                    }
-                    epilogue8(E, P, m, n, nl, v, cold[k], rres[k], mb[k]);
-                }
-                if constexpr (CG % 4 == 0) {
-                    // MXFP8 copy: the 4 lanes l..l+3 (l % 4 == 0) hold one 32-column block
-                    if (E.out8) {
-                        float amax = 0.f;
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
-                        amax = fmaxf(amax, __shfl_xor(amax, 1));
-                        amax = fmaxf(amax, __shfl_xor(amax, 2));
-                        const int ex = mx_exponent(amax);
-                        const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
-                        float q[8];
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) q[e] = v[e] * inv;
-                        const uint2 pk = pack_e4m3x8(q);
-                        if (live) {
-                            *reinterpret_cast<uint2 *>((uint8_t *)E.out8 + (long long)m * E.ldo8 + n) = pk;
-                            if ((lane & 3) == 0) E.scale8[(long long)m * (E.ldo8 >> 5) + (n >> 5)] = (uint8_t)(ex + 127);
-                        }
-                    }
-                }
-            });
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         });
+        __builtin_amdgcn_sched_barrier(0);
     }
+    fused_epilogue<BM, BN, WM, WN>(acc, dsm, E, M, N, m0, n0, tid, lane, wave);
 }
 
 // split-K reduction: dst[m][n] (+)= sum_s slab[s][m][n]
@@ -755,6 +929,24 @@ __global__ void k_slab_reduce(const float *slab, int splits, int M, int N, float
     }
 }
 
+// bias column sums over the splits: 4 waves split the slabs of 64 columns, fixed-order
+// combine (the one-thread-per-column form was latency bound: 27 us for 86 splits)
+__global__ __launch_bounds__(256) void k_slab_reduce_cols(const float *slab, int splits, int N,
+                                                          float *dst, int accumulate) {
+    __shared__ float part[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    float s = 0.f;
+    if (c < N)
+        for (int k = g; k < splits; k += 4) s += slab[(long long)k * N + c];
+    part[g][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (g == 0 && c < N) {
+        const int l = threadIdx.x & 63;
+        const float t = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+        dst[c] = accumulate ? dst[c] + t : t;
+    }
+}
+
 __global__ void k_rows_sum(h16 *edge, const h16 *src, long long ld, int r0, int r1, int cols) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= cols) return;
@@ -767,6 +959,7 @@ __global__ void k_rows_sum(h16 *edge, const h16 *src, long long ld, int r0, int 
 // optional per-launch HIP-event timing (kf_prof_*), used by bench.py to price
 // the dominant kernel class over the timed region on the stream it runs on
 // ---------------------------------------------------------------------------
+#include <algorithm>
 #include <vector>
 namespace {
 struct ProfRec {
@@ -958,6 +1151,122 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
     return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// conv_halo_kernel dispatch: A must be a conv im2col / col2im operand (k-contiguous,
+// 64-channel parts, zero time padding, no edge rows, hdiv 1, hmul 1 or 2). Returns
+// 1 when launched, 0 when not applicable (the caller runs the im2col GEMM), -1 on error.
+// KF_CONV_HALO=0 disables it (A/B).
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW>
+static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const HaloArgs &H, size_t lds) {
+    const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
+    ProfRec rec{};
+    if (g_prof) {
+        rec.a = prof_event();
+        rec.b = prof_event();
+        rec.cls = KF_PROF_FUSED;
+        rec.flops = 2.0 * M * N * (double)H.ntaps * H.pw;
+        hipEventRecord(rec.a, kf_stream());
+    }
+    conv_halo_kernel<BM, BN, WM, WN, BKC, BMODE, BROW>
+        <<<dim3(mt * nt), 64 * WM * WN, lds, kf_stream()>>>(M, N, B, E, H, mt, nt);
+    if (g_prof) {
+        hipEventRecord(rec.b, kf_stream());
+        g_prof_recs.push_back(rec);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        kf_set_error("conv halo launch (M=%d N=%d): %s", M, N, hipGetErrorString(e));
+        return -1;
+    }
+    return 1;
+}
+
+static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm, bool bkc,
+                         const KfEpilogue &E) {
+    static const int on = getenv("KF_CONV_HALO") ? atoi(getenv("KF_CONV_HALO")) : 1;
+    if (!on || op_mode(a) != OP_GEN || !a.p64 || a.edges || a.tclamp || a.hshift ||
+        a.hmul < 1 || a.hmul > 2 || a.hout < 2 || a.ncols != K || a.nparts * a.pw != K)
+        return 0;
+    if (bkc ? bm != OP_GEN : bm != OP_SIMPLE) return 0;
+    // shifted weight rows (op_wrows): every tap's block lies inside the matrix
+    bool brow = bkc && b.hout == 1 && b.hmul == 0 && !b.hshift && !b.edges && !b.tclamp &&
+                b.nparts == a.nparts && b.pw == a.pw;
+    for (int p = 0; brow && p < b.nparts; ++p) brow = b.dt[p] >= 0 && b.dt[p] + b.nrows <= b.T;
+    if (bkc && !brow) return 0;
+    OpD bp = b;
+    if (brow) {  // one 64-column chunk of a plain [nrows x ld] matrix, rebased per step
+        bp.simple = 1;
+        bp.nparts = 1;
+        bp.ncols = BK;
+        bp.pw = BK;
+        bp.T = b.nrows;
+        for (int p = 0; p < KF_MAX_PARTS; ++p) bp.dt[p] = bp.dh[p] = 0;
+    }
+    int dtmin = 1 << 20, dtmax = -(1 << 20), dhmin = 1 << 20, dhmax = -(1 << 20);
+    for (int p = 0; p < a.nparts; ++p) {
+        dtmin = std::min(dtmin, a.dt[p]);
+        dtmax = std::max(dtmax, a.dt[p]);
+        dhmin = std::min(dhmin, a.dh[p]);
+        dhmax = std::max(dhmax, a.dh[p]);
+    }
+    HaloArgs H;
+    memset(&H, 0, sizeof H);
+    H.x = a.base;
+    H.ld = a.ld;
+    H.T = a.T;
+    H.hout = a.hout;
+    H.hmul = a.hmul;
+    H.hsrc = a.hsrc;
+    H.pw = a.pw;
+    H.pad = std::max(0, -dhmin);
+    const int maxshp = (a.hout - 1) * a.hmul + dhmax + H.pad;
+    const int HP = std::max(a.hsrc + H.pad, maxshp + 1);
+    H.hpe = (HP + a.hmul - 1) / a.hmul;
+    H.hpos = H.hpe * a.hmul;
+    H.dtmin = dtmin;
+    H.ntaps = a.nparts;
+    H.nch = a.pw / BK;
+    H.nbuf = H.nch > 1 ? 2 : 1;
+    for (int p = 0; p < a.nparts; ++p) {
+        const int x = a.dh[p] + H.pad;
+        H.ctap[p] = (a.dt[p] - dtmin) * H.hpos + (x % a.hmul) * H.hpe + x / a.hmul;
+        H.bshift[p] = brow ? b.dt[p] : 0;
+    }
+    // 32-bit source offsets: the largest byte offset the halo can form
+    if (((long long)a.T * a.ld + (long long)a.hsrc * a.pw) * 2 >= (1LL << 32) - 64) return 0;
+    const int BN_ = N <= 64 ? 64 : N <= 128 ? 128 : 256;
+    // 256-row tiles only: where the two halo images do not fit beside a 256-column B ring
+    // (cnn5's stride-2 forward) the 128-row halo tile measured slower than im2col
+    for (int BM_ : {256}) {
+        H.nf = (BM_ - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
+        H.rows = H.nf * H.hpos;
+        H.npieces = (H.rows + 7) / 8;
+        H.slice = (H.npieces + H.ntaps - 1) / H.ntaps;
+        H.halo_bytes = H.npieces * 1024;
+        const int nw = BN_ == 64 ? 4 : 8, wtn = BN_ == 64 ? 64 : BN_ == 128 ? 64 : 64;
+        const size_t epi = 16 * BN_ + 32 * (wtn + 4) * 4 * nw;
+        const size_t lds = std::max((size_t)H.nbuf * H.halo_bytes + 2 * BN_ * BK * 2, epi);
+        if (lds > 160 * 1024) continue;
+#define KF_HALO(BKC_, BMODE_, BROW_)                                                                     \
+        do {                                                                                      \
+            if (BN_ == 64)                                                                        \
+                return BM_ == 256 ? launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds)  \
+                                  : launch_halo<128, 64, 4, 1, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds); \
+            if (BN_ == 128)                                                                       \
+                return BM_ == 256 ? launch_halo<256, 128, 4, 2, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds) \
+                                  : launch_halo<128, 128, 4, 2, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds); \
+            return BM_ == 256 ? launch_halo<256, 256, 2, 4, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds)     \
+                              : launch_halo<128, 256, 2, 4, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds);    \
+        } while (0)
+        if (bkc) KF_HALO(true, OP_SIMPLE, true);
+        KF_HALO(false, OP_SIMPLE, false);
+#undef KF_HALO
+    }
+    return 0;
+}
+
 static int gemm_big() {
     const char *e = getenv("KF_GEMM_BIG");
     return e ? atoi(e) : 1;
@@ -1010,18 +1319,25 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
             return launch<128, 128, 2, 2, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
         return launch<128, 128, 2, 2, true, true, false, 2, OP_P2, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
     }
+    if (!E.out8) {
+        const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);
+        if (hr != 0) return hr < 0 ? -1 : 0;
+    }
     // 8-wave 256-row tiles halve the staged bytes per MFMA flop against the 4-wave
     // 128-row ones; KF_GEMM_BIG=0 selects the 4-wave family for A/B.
     static const int big = gemm_big();
     static const int b128 = getenv("KF_GEMM_B128") ? atoi(getenv("KF_GEMM_B128")) : 0;
+    static const int b160 = getenv("KF_GEMM_B160") ? atoi(getenv("KF_GEMM_B160")) : 1;
     int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : (big && N >= 256 ? 3 : 0));
     if (tile == 0 && b128 && N <= 128) tile = 4;
     if (E.out8 && tile == 1) tile = 0;  // out8 needs 32-column blocks inside one wave's tile
+    if (tile == 1 && b160) tile = 5;    // 8-wave 384x160: 1.5x the flops per staged byte
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
         if (tile == 3) return launch<256, 256, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 4) return launch<256, 128, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 1) return launch<128, 160, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
+        if (tile == 5) return launch<384, 160, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 2) return launch<256, 64, 4, 1, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);  \
         return launch<128, 128, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);               \
     } while (0)
@@ -1050,7 +1366,9 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     }
     if (!mn_gen_ok(a, "A") || !mn_gen_ok(b, "B")) return -1;
     static const int wbig = getenv("KF_GEMM_WBIG") ? atoi(getenv("KF_GEMM_WBIG")) : 1;
+    static const int w160 = getenv("KF_GEMM_W160") ? atoi(getenv("KF_GEMM_W160")) : 1;
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
+    if (BNc == 160 && w160) BMc = 384;
     if (BNc == 64) BMc = 256;
     if (wbig && BNc == 128) BMc = 256, BNc = N > 128 ? 256 : 128;
     // tile rows: the candidate wasting the fewest padded rows of M (ties: the larger)
@@ -1066,7 +1384,10 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         BMc = best;
     }
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
-    int splits = (512 + tiles - 1) / tiles;
+    // workgroups per launch: every split writes an M x N fp32 slab that the reduce
+    // reads back, so the target trades CU fill against slab traffic
+    static const int wg_target = getenv("KF_WG_TARGET") ? atoi(getenv("KF_WG_TARGET")) : 512;
+    int splits = (wg_target + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
     if (splits > maxsplit) splits = maxsplit;
     if (splits < 1) splits = 1;
@@ -1100,6 +1421,8 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
             rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BMc == 256 && BNc == 128)                                                       \
             rc = launch<256, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 384 && BNc == 160)                                                       \
+            rc = launch<384, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 160)                                                                     \
             rc = launch<128, 160, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 64)                                                                      \
@@ -1116,8 +1439,8 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     k_slab_reduce<<<kf_blocks((long long)M * N, 256, 4096), 256, 0, kf_stream()>>>(
         G.slab, splits, M, N, dW, ldw, accumulate);
     if (bias_grad)
-        k_slab_reduce<<<kf_blocks(N, 256, 64), 256, 0, kf_stream()>>>(G.bias_slab, splits, 1, N,
-                                                                      bias_grad, N, accumulate);
+        k_slab_reduce_cols<<<(N + 63) / 64, 256, 0, kf_stream()>>>(G.bias_slab, splits, N,
+                                                                   bias_grad, accumulate);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         kf_set_error("wgrad reduce: %s", hipGetErrorString(e));

@@ -1,13 +1,21 @@
 """Print one training step's kernel sequence from a rocprofv3 kernel trace.
 
-usage: python scripts/step_trace.py <run_kernel_trace.csv> [step_index_from_end]
+usage: python scripts/step_trace.py <run_kernel_trace.csv | run_results.db> [step_index_from_end]
 Steps are delimited by k_sgd_flat (the last kernel of a step).
 """
 import csv
 import re
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+if sys.argv[1].endswith(".db"):  # rocprofv3's default rocpd (SQLite) output
+    import sqlite3
+    cur = sqlite3.connect(sys.argv[1]).execute(
+        "select start, end, name, queue_id, grid_x, grid_y, workgroup_x, vgpr_count, accum_vgpr_count from kernels")
+    keys = ["Start_Timestamp", "End_Timestamp", "Kernel_Name", "Queue_Id", "Grid_Size_X", "Grid_Size_Y",
+            "Workgroup_Size_X", "VGPR_Count", "Accum_VGPR_Count"]
+    rows = [dict(zip(keys, map(str, r))) for r in cur]
+else:
+    rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "k_sgd_flat" in r["Kernel_Name"]]
 back = int(sys.argv[2]) if len(sys.argv) > 2 else 1
