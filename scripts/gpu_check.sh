@@ -16,10 +16,10 @@ step() {  # step <name> <timeout> <cmd...>
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-    step pytest_gpu 900 python -m pytest tests -m "gpu and not slow" -x -q
+    step pytest_gpu 900 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = slow ]; then
-    step pytest_gpu_slow 900 python -m pytest tests -m "gpu and slow" -x -q
+    step pytest_gpu_slow 900 python -u -m pytest tests -m "gpu and slow" -x -q --timeout 300 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 3}
