@@ -156,6 +156,23 @@ int kf_sgd_flat(float *w32, void *w16, const float *g, float *v, float lr, float
 int kf_f32_to_f16_flat(const float *src, void *dst, long long n);
 const char *kf_layers_last_error(void);
 
+/* Kaldi compressed-matrix expansion (egs input, kf_egs.h). One descriptor per stored
+ * matrix; payload_off = byte offset of its payload in the device blob (2-byte aligned,
+ * 4 for FM); rows land at out rows [out_row, out_row + rows). cols <= 256. */
+enum { KF_CM_ONEBYTE_COLHDR = 1, KF_CM_TWOBYTE = 2, KF_CM_ONEBYTE = 3, KF_CM_FLOAT = 4 };
+typedef struct {
+    int format, rows, cols, out_row;
+    float min_value, range;
+    long long payload_off;
+} KfCmDesc;
+int kf_cm_expand(const KfCmDesc *dev_desc, int nmat, int max_rows, int max_cols,
+                 const void *dev_blob, void *dev_out, int ldo);
+/* Same from host arrays: every descriptor is bounds-checked against blob_bytes, then
+ * descriptors + blob travel in one pinned, stream-ordered H2D copy (kf_get_stream())
+ * ahead of the launch. The host arrays may be freed on return. */
+int kf_cm_expand_host(const KfCmDesc *desc, int nmat, int max_rows, int max_cols,
+                      const void *blob, size_t blob_bytes, void *dev_out, int ldo);
+
 /* optional HIP-event timing of every GEMM launch on the current stream
  * (class 0 = kf_gemm_fused, 1 = kf_gemm_wgrad); collect sums since reset */
 void kf_prof_enable(int on);

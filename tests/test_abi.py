@@ -18,6 +18,7 @@ HEADERS = {
     "cnn_fp16.h": "libkaldi_fp16.so",
     "kaldi_bridge.h": "libkaldi_fp16_cgo.so",
     "kf_nnet.h": "libkaldi_fp16_nnet.so",
+    "kf_egs.h": "libkaldi_fp16_egs.so",
 }
 
 
