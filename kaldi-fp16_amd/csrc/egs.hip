@@ -7,8 +7,10 @@
 // Here the stored bytes (CM: 1 B/value + 8 B/column) go to HBM as one packed blob
 // and this kernel does the rest in one launch for the whole minibatch.
 //
-// Arithmetic is the reference's, op for op, with no contraction (the __f*_rn
-// intrinsics cannot fuse): Go on amd64 evaluates each float32 operation separately.
+// Arithmetic is the reference's, op for op, with no contraction: Go on amd64 evaluates
+// each float32 operation separately. HIP's __f*_rn are plain operators that the
+// default -ffp-contract=fast would fuse into FMAs, so contraction is switched off for
+// this file (pragma below) — found by the bit-exact GPU test.
 //   uint16ToFloat  matrix.go:11-14   min + (range * f32(1/65535)) * f32(v)
 //   charToFloat    matrix.go:17-27   three pieces; the last divides in float64
 //   CM2            matrix.go:106-130 min + f32(v) * (range / 65535)
@@ -23,24 +25,32 @@
 #include "kf_common.h"
 #include "../../include/kf_ops.h"
 
+#pragma clang fp contract(off)
+
 namespace {
 
 constexpr int kRows = 64;      // rows per workgroup
 constexpr int kMaxCols = 256;  // LDS tile bound (Kaldi features: 40; ivectors: 100)
 
+// Own single-rounding helpers: the operators below carry no 'contract' flag under the
+// pragma above (HIP's __fmul_rn / __fadd_rn live in a header compiled with contraction).
+__device__ __forceinline__ float mul_rn(float a, float b) { return a * b; }
+__device__ __forceinline__ float add_rn(float a, float b) { return a + b; }
+__device__ __forceinline__ float sub_rn(float a, float b) { return a - b; }
+
 __device__ __forceinline__ float u16_to_float(float mn, float rg, unsigned v) {
     const float inv65535 = 1.52590218966964e-05f;
-    return __fadd_rn(mn, __fmul_rn(__fmul_rn(rg, inv65535), (float)v));
+    return add_rn(mn, mul_rn(mul_rn(rg, inv65535), (float)v));
 }
 
 __device__ __forceinline__ float char_to_float(float p0, float p25, float p75, float p100,
                                                unsigned v) {
     if (v <= 64u)
-        return __fadd_rn(p0, __fmul_rn(__fmul_rn(__fsub_rn(p25, p0), (float)v), 1.0f / 64.0f));
+        return add_rn(p0, mul_rn(mul_rn(sub_rn(p25, p0), (float)v), 1.0f / 64.0f));
     if (v <= 192u)
-        return __fadd_rn(p25, __fmul_rn(__fmul_rn(__fsub_rn(p75, p25), (float)(v - 64u)),
+        return add_rn(p25, mul_rn(mul_rn(sub_rn(p75, p25), (float)(v - 64u)),
                                         1.0f / 128.0f));
-    const float prod = __fmul_rn(__fsub_rn(p100, p75), (float)(v - 192u));
+    const float prod = mul_rn(sub_rn(p100, p75), (float)(v - 192u));
     return (float)__dadd_rn((double)p75, __ddiv_rn((double)prod, 63.0));
 }
 
@@ -87,12 +97,12 @@ __global__ void __launch_bounds__(256) k_cm_expand(const KfCmDesc *__restrict__ 
         const uint16_t *v = reinterpret_cast<const uint16_t *>(p);
         for (int i = threadIdx.x; i < nr * cols; i += 256)
             o[(long long)(i / cols) * ldo + i % cols] =
-                (h16)__fadd_rn(d.min_value, __fmul_rn((float)v[base + i], inc));
+                (h16)add_rn(d.min_value, mul_rn((float)v[base + i], inc));
     } else if (d.format == KF_CM_ONEBYTE) {
         const float inc = __fdiv_rn(d.range, 255.0f);
         for (int i = threadIdx.x; i < nr * cols; i += 256)
             o[(long long)(i / cols) * ldo + i % cols] =
-                (h16)__fadd_rn(d.min_value, __fmul_rn((float)p[base + i], inc));
+                (h16)add_rn(d.min_value, mul_rn((float)p[base + i], inc));
     } else {  // KF_CM_FLOAT
         const float *v = reinterpret_cast<const float *>(p);
         for (int i = threadIdx.x; i < nr * cols; i += 256)
