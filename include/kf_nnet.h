@@ -58,6 +58,9 @@ int nnet_get_params(const KfNet *net, float *host_flat); /* fp32 master */
 int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean, const float *var,
                 const float *gamma, const float *beta, float eps, float target_rms);
 
+/* replace an idct-layer's matrix: host fp32 [dim x dim], y = x . m (weight_loader.go:88-97) */
+int nnet_set_idct(KfNet *net, const char *layer, const float *m, int rows, int cols);
+
 /* forward on T frames of fp16 features already in device memory */
 int nnet_forward(KfNet *net, const void *features_dev, int T);
 /* device pointer of a layer's output activation (fp16 [rows x cols]) */

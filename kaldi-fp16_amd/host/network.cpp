@@ -548,6 +548,31 @@ extern "C" int nnet_get_params(const KfNet *net, float *host) {
     return 0;
 }
 
+// Replaces an idct-layer's fixed matrix (LoadWeights / allocWeightsFromKaldi, LayerIDCT:
+// weight_loader.go:88-97, :760-770): host fp32 [dim x dim] in the y = x . M orientation,
+// stored fp16 by truncation like every weight (tensor.go:158-173).
+extern "C" int nnet_set_idct(KfNet *net, const char *layer, const float *m, int rows, int cols) {
+    for (auto &nl : net->layers) {
+        if (nl.L.name != layer) continue;
+        if (nl.L.type != LayerType::IDCT || !nl.idct) break;
+        const int d = nl.L.out_dim;
+        if (rows != d || cols != d || !m) {
+            set_err("set_idct: " + nl.L.name + " needs a " + std::to_string(d) + "x" + std::to_string(d) +
+                    " matrix, got " + std::to_string(rows) + "x" + std::to_string(cols));
+            return -1;
+        }
+        std::vector<uint16_t> h((size_t)d * d);
+        for (size_t i = 0; i < h.size(); ++i) h[i] = f32_to_f16_trunc(m[i]);
+        if (bridge_transfer_fp16(nl.idct, h.data(), h.size())) {
+            set_err("set_idct: upload failed");
+            return -1;
+        }
+        return 0;
+    }
+    set_err(std::string("set_idct: no idct layer ") + (layer ? layer : "(null)"));
+    return -1;
+}
+
 extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean,
                            const float *var, const float *gamma, const float *beta, float eps,
                            float target_rms) {

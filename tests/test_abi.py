@@ -19,6 +19,7 @@ HEADERS = {
     "kaldi_bridge.h": "libkaldi_fp16_cgo.so",
     "kf_nnet.h": "libkaldi_fp16_nnet.so",
     "kf_egs.h": "libkaldi_fp16_egs.so",
+    "kf_model.h": "libkaldi_fp16_nnet.so",
 }
 
 
