@@ -268,8 +268,56 @@ int ops_softmax(void *data, int rows, int cols) {
     k_softmax<<<rows, 256, 0, kf_stream()>>>((h16 *)data, cols, 0);
     return ops_check("softmax kernel");
 }
+// Row-wise log-softmax with the row held in registers: one wave per row, 16-byte loads,
+// max / sum by wave shuffles, one read and one write of the row (k_softmax re-reads it
+// three times). The reference's LogSoftmax (ops.cu:120-166) takes the row max with an
+// integer atomicMax on float bits, which is wrong for all-negative rows; this one is not.
+constexpr int kLsmMaxChunks = 8;  // cols <= 64 lanes * 8 chunks * 8 = 4096
+__global__ __launch_bounds__(256) void k_log_softmax_rows(h16 *data, int rows, int cols) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;  // whole wave
+    half8 *r = reinterpret_cast<half8 *>(data + (long long)row * cols);
+    const int nch = cols >> 3;
+    half8 v[kLsmMaxChunks];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kLsmMaxChunks; ++k) {
+        const int c = lane + 64 * k;
+        v[k] = c < nch ? r[c] : half8{};
+        if (c < nch)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) mx = fmaxf(mx, (float)v[k][e]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < kLsmMaxChunks; ++k)
+        if (lane + 64 * k < nch)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += expf((float)v[k][e] - mx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float lse = mx + logf(s);
+#pragma unroll
+    for (int k = 0; k < kLsmMaxChunks; ++k) {
+        const int c = lane + 64 * k;
+        if (c < nch) {
+            half8 w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) w[e] = (h16)((float)v[k][e] - lse);
+            r[c] = w;
+        }
+    }
+}
+
 int ops_log_softmax(void *data, int rows, int cols) {
     if (rows <= 0 || cols <= 0) return 0;
+    if (cols % 8 == 0 && cols <= 64 * 8 * kLsmMaxChunks && aligned16(data)) {
+        k_log_softmax_rows<<<(rows + 3) / 4, 256, 0, kf_stream()>>>((h16 *)data, rows, cols);
+        return ops_check("log_softmax kernel");
+    }
     k_softmax<<<rows, 256, 0, kf_stream()>>>((h16 *)data, cols, 1);
     return ops_check("log_softmax kernel");
 }

@@ -153,6 +153,11 @@ KfEpilogue epi0() {
 struct KfNet {
     std::vector<Layer> all;
     std::vector<NetLayer> layers;
+    // Model.ChainOutput (model.go:271-281): the output layer named "output", else the first
+    // output layer; backward is seeded there. Trainable layers off its input path (the xent
+    // branch) get no gradient (network_backward.go:110-115): their ranges are zeroed.
+    int chain_out = -1;
+    std::vector<std::pair<long long, long long>> offpath;  // (float offset, count) in grad
     int feat_dim = 0, max_T = 0, T = 0;
     const void *features = nullptr;
     long long nparams = 0;
@@ -402,6 +407,21 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
     if (net->layers.empty()) {
         set_err("no layers");
         return nullptr;
+    }
+    for (size_t i = 0; i < net->layers.size() && net->chain_out < 0; ++i)
+        if (net->layers[i].L.type == LayerType::Output && net->layers[i].L.name == "output") net->chain_out = (int)i;
+    for (size_t i = 0; i < net->layers.size() && net->chain_out < 0; ++i)
+        if (net->layers[i].L.type == LayerType::Output) net->chain_out = (int)i;
+    if (net->chain_out < 0) net->chain_out = (int)net->layers.size() - 1;
+    {
+        std::vector<char> on(net->layers.size(), 0);
+        for (int cur = net->chain_out; cur >= 0; cur = net->layers[cur].input) on[cur] = 1;
+        for (size_t i = 0; i < net->layers.size(); ++i) {
+            if (on[i]) continue;
+            const NetLayer &nl = net->layers[i];
+            for (int pi : {nl.pW, nl.pb, nl.pW2, nl.pb2})
+                if (pi >= 0) net->offpath.emplace_back(net->params[pi].off, (long long)net->params[pi].rows * net->params[pi].cols);
+        }
     }
     // which layers need an input gradient (a trainable layer lies below them)
     for (size_t i = 0; i < net->layers.size(); ++i) {
@@ -1004,7 +1024,9 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     const void *dz = out_grad;  // gradient w.r.t. pre-activation of the current layer
     const void *gcur = out_grad;  // stored gradient w.r.t. the current layer's output
     int flip = 0, done = 0;
-    for (int li = n - 1; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
+    for (const auto &r : net->offpath) bridge_gpu_memset(net->grad + r.first, 0, (size_t)r.second * 4);
+    (void)n;
+    for (int li = net->chain_out; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
         NetLayer &nl = net->layers[li];
         const Layer &L = nl.L;
         const int din = L.in_dim, dout = L.out_dim;

@@ -67,6 +67,7 @@ _sig(core, "kf_get_stream", _vp)
 _sig(core, "ops_gemm", _i, _vp, _i, _i, _i, _f, _vp, _i, _vp, _i, _f, _vp, _i)
 _sig(core, "ops_cublas_create", _vp)
 _sig(core, "ops_cublas_destroy", None, _vp)
+_sig(core, "ops_log_softmax", _i, _vp, _i, _i)
 
 # ---------------------------------------------------------------- nnet_*
 _sig(nnet, "nnet_create", _vp, C.c_char_p, _i)

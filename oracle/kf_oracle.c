@@ -484,6 +484,20 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 orc_matmul(T, dout, din, x8 ? x8 : x, x8 ? wq : L->W, y);
                 bias_relu_bn(y, T, dout, L->b, NULL, NULL, mode, 0, NULL);
                 if (mode) orc_round_f16(y, (long long)T * dout);
+                if (L->log_softmax) {
+                    /* LogSoftmax of the stored fp16 affine output (forward.go:991-997), in
+                     * double; the reference's integer-atomicMax row max (ops.cu:120-166)
+                     * is wrong for all-negative rows and is not restated */
+                    for (int t = 0; t < T; ++t) {
+                        float *row = y + (size_t)t * dout;
+                        double mx = -INFINITY, s = 0.0;
+                        for (int d = 0; d < dout; ++d) mx = row[d] > mx ? row[d] : mx;
+                        for (int d = 0; d < dout; ++d) s += exp((double)row[d] - mx);
+                        const double lse = mx + log(s);
+                        for (int d = 0; d < dout; ++d) row[d] = (float)((double)row[d] - lse);
+                    }
+                    if (mode) orc_round_f16(y, (long long)T * dout);
+                }
                 break;
             default:
                 free(y);
@@ -510,15 +524,20 @@ static float *colsum(const float *g, int rows, int D) {
  * and this restatement rounds at exactly those tensors in F mode.
  */
 int orc_net_backward(OrcNet *net, const float *features, const float *out_grad) {
+    return orc_net_backward_top(net, features, out_grad, net->nlayers - 1);
+}
+
+int orc_net_backward_top(OrcNet *net, const float *features, const float *out_grad, int top_li) {
     const int T = net->T, mode = net->round_mode;
     const int n = net->nlayers;
+    if (top_li < 0 || top_li >= n) return -1;
     float **v = (float **)xalloc(sizeof(float *) * n);
     {
-        const OrcLayer *top = &net->layers[n - 1];
-        v[n - 1] = (float *)xalloc(sizeof(float) * (size_t)T * top->out_dim);
-        memcpy(v[n - 1], out_grad, sizeof(float) * (size_t)T * top->out_dim);
+        const OrcLayer *top = &net->layers[top_li];
+        v[top_li] = (float *)xalloc(sizeof(float) * (size_t)T * top->out_dim);
+        memcpy(v[top_li], out_grad, sizeof(float) * (size_t)T * top->out_dim);
     }
-    for (int li = n - 1; li >= 0; --li) {
+    for (int li = top_li; li >= 0; --li) {
         const OrcLayer *L = &net->layers[li];
         if (!v[li]) continue;
         const int din = L->in_dim, dout = L->out_dim;

@@ -69,6 +69,7 @@ typedef struct {
     const float *b2;  /* tdnnf AffineBias */
     OrcBN bn;         /* conv / tdnnf / batchnorm-component / prefinal BN1 */
     OrcBN bn2;        /* prefinal BN2 (small dim); mean==NULL -> none */
+    int log_softmax;  /* output-layer include-log-softmax=true (forward.go:991-997) */
 } OrcLayer;
 
 typedef struct {
@@ -103,6 +104,9 @@ void orc_mx_qdq_rows(const float *x, float *y, long long rows, int cols);
 int orc_net_forward(OrcNet *net, const float *features);
 /* out_grad [T x out_dim(last)], already fp16-representable */
 int orc_net_backward(OrcNet *net, const float *features, const float *out_grad);
+/* the same seeded at layer `top` (Model.ChainOutput, network_backward.go:102-115):
+ * layers off its input path get no gradient */
+int orc_net_backward_top(OrcNet *net, const float *features, const float *out_grad, int top);
 void orc_net_free(OrcNet *net);
 
 /* v = mom*v + g; w32 -= lr*v (backward_wrappers.cu:129-142) */

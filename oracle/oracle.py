@@ -48,6 +48,7 @@ def lib(native: bool = False):
         _lib.orc_matmul.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib.orc_net_forward.argtypes = [C.c_void_p, C.c_void_p]
         _lib.orc_net_backward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        _lib.orc_net_backward_top.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         _lib.orc_net_free.argtypes = [C.c_void_p]
         _lib.orc_sgd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_longlong]
         _lib.orc_mx_qdq_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_int]
@@ -71,7 +72,8 @@ class OrcLayer(C.Structure):
                 ("fout", C.c_int), ("noff", C.c_int), ("toff", C.c_int * 9), ("hoff", C.c_int * 9),
                 ("bn_dim", C.c_int), ("stride", C.c_int), ("bypass", C.c_float),
                 ("small_dim", C.c_int), ("big_dim", C.c_int),
-                ("W", _fp), ("b", _fp), ("W2", _fp), ("b2", _fp), ("bn", OrcBN), ("bn2", OrcBN)]
+                ("W", _fp), ("b", _fp), ("W2", _fp), ("b2", _fp), ("bn", OrcBN), ("bn2", OrcBN),
+                ("log_softmax", C.c_int)]
 
 
 class OrcNet(C.Structure):
@@ -198,6 +200,8 @@ class OracleNet:
             elif kind == "output-layer":
                 o.type = ORC["OUTPUT"]
                 o.W, o.b = self._p(params[L["name"] + ".W"]), self._p(params[L["name"] + ".Bias"])
+                # layers.go:345: include-log-softmax defaults to true
+                o.log_softmax = int(L["kv"].get("include-log-softmax", "true").lower() in ("true", "1", "t"))
             index[L["name"]] = i
         self.arr = arr
         self.index = index
@@ -256,9 +260,17 @@ class OracleNet:
         p = self.net.mask[i]
         return None if not p else np.ctypeslib.as_array(p, shape=(self.net.T * width,)).copy()
 
+    def chain_output(self) -> int:
+        """Model.ChainOutput (model.go:271-281): the output layer named "output", else the first."""
+        outs = [i for i, L in enumerate(self.L) if L["kind"] == "output-layer"]
+        for i in outs:
+            if self.L[i]["name"] == "output":
+                return i
+        return outs[0] if outs else len(self.L) - 1
+
     def backward(self, out_grad: np.ndarray):
         g = np.ascontiguousarray(out_grad, dtype=np.float32)
-        rc = lib().orc_net_backward(C.byref(self.net), self.x.ctypes.data, g.ctypes.data)
+        rc = lib().orc_net_backward_top(C.byref(self.net), self.x.ctypes.data, g.ctypes.data, self.chain_output())
         assert rc == 0
 
     def grads(self) -> dict:
@@ -267,8 +279,8 @@ class OracleNet:
         T = self.net.T
 
         def get(ptrs, i, n):
-            p = ptrs[i]
-            return None if not p else np.ctypeslib.as_array(p, shape=(n,)).copy()
+            p = ptrs[i]  # no gradient reached the layer (off the chain-output path): zeros
+            return np.zeros(n, np.float32) if not p else np.ctypeslib.as_array(p, shape=(n,)).copy()
 
         for i, L in enumerate(self.L):
             k, n = L["kind"], L["name"]
