@@ -1356,9 +1356,18 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
     if (tile == 0 && b128 && N <= 128) tile = 4;
     if (E.out8 && tile == 1) tile = 0;  // out8 needs 32-column blocks inside one wave's tile
     if (tile == 1 && b160) tile = 5;    // 8-wave 384x160: 1.5x the flops per staged byte
+    // Wide fused GEMMs spend much of a tile in the epilogue's HBM traffic (the TDNN-F
+    // affine forward and linear input gradient, K = 320, write 2-3 full-width fp16
+    // tensors). 192x128 tiles stage 80 KB of LDS, so two workgroups share a CU and one's
+    // epilogue overlaps the other's MFMA loop: 293 -> 266 us and 244 -> 228 us per
+    // launch against 256x256, step 47.2 -> 46.2 ms. KF_GEMM_T6=0 restores 256x256,
+    // 1 limits 192x128 to K <= 640.
+    static const int t6 = getenv("KF_GEMM_T6") ? atoi(getenv("KF_GEMM_T6")) : 2;
+    if (t6 && tile == 3 && (K <= 640 || t6 == 2) && !E.out8) tile = 6;
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
         if (tile == 3) return launch<256, 256, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
+        if (tile == 6) return launch<192, 128, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 4) return launch<256, 128, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 1) return launch<128, 160, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 5) return launch<384, 160, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
