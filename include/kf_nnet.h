@@ -60,6 +60,8 @@ int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean, con
 
 /* replace an idct-layer's matrix: host fp32 [dim x dim], y = x . m (weight_loader.go:88-97) */
 int nnet_set_idct(KfNet *net, const char *layer, const float *m, int rows, int cols);
+/* attention layer key scale (> 0); default 1/sqrt(key-dim) or the xconfig key-scale */
+int nnet_set_key_scale(KfNet *net, const char *layer, float key_scale);
 
 /* forward on T frames of fp16 features already in device memory */
 int nnet_forward(KfNet *net, const void *features_dev, int T);

@@ -173,6 +173,24 @@ int kf_cm_expand(const KfCmDesc *dev_desc, int nmat, int max_rows, int max_cols,
 int kf_cm_expand_host(const KfCmDesc *desc, int nmat, int max_rows, int max_cols,
                       const void *blob, size_t blob_bytes, void *dev_out, int ldo);
 
+/* Restricted self-attention of attention-relu-batchnorm layers (csrc/attention.hip;
+ * forward.go:795-909 runs it on the CPU). proj: fp16 [T x ldp] affine output, per head
+ * [key kd | value vd | query key kd | query context ctx]; frame t attends to rows
+ * t + (o - num_left) * stride, o < context, zero outside [0, T). */
+typedef struct {
+    const void *proj;
+    long long ldp;
+    int T, num_heads, key_dim, value_dim, context, num_left, stride;
+    float key_scale;
+} KfAttention;
+/* out: fp16 [T x ldo], width num_heads * (value_dim + context); y = bn(relu(att));
+ * mask (may be NULL): ReLU bits, row-major over width (width % 8 == 0). */
+int kf_attention_forward(const KfAttention *a, void *out, long long ldo, uint8_t *mask, const float *scale,
+                         const float *shift);
+/* dz: fp16 gradient at the attention output (pre-ReLU) [T x ldz]; dproj: fp16, same
+ * layout and ld as proj (every element written); scratch: fp32 [2 x T x heads x context]. */
+int kf_attention_backward(const KfAttention *a, const void *dz, long long ldz, void *dproj, float *scratch);
+
 /* optional HIP-event timing of every GEMM launch on the current stream
  * (class 0 = kf_gemm_fused, 1 = kf_gemm_wgrad); collect sums since reset */
 void kf_prof_enable(int on);

@@ -56,6 +56,9 @@ struct NetLayer {
     uint8_t *mask = nullptr;  // relu bits
     void *aux = nullptr;      // tdnnf bottleneck / prefinal big
     void *idct = nullptr;     // fp16 [D x D]
+    void *dproj = nullptr;    // attention: fp16 [maxT x affine] gradient of aux (the affine output)
+    float *att_scratch = nullptr;  // attention: fp32 [2 x maxT x heads x context]
+    float key_scale = 0.f;
     bool bypass = false;
     bool needs_dx = false;
     // MXFP8 forward (nnet_set_fp8): output / aux copies written by the producing
@@ -64,6 +67,22 @@ struct NetLayer {
 };
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+KfAttention att_args(const NetLayer &nl, int T) {
+    const Layer &L = nl.L;
+    KfAttention a;
+    a.proj = nl.aux;
+    a.T = T;
+    a.num_heads = L.num_heads;
+    a.key_dim = L.key_dim;
+    a.value_dim = L.value_dim;
+    a.context = 1 + L.num_left + L.num_right;
+    a.ldp = (long long)L.num_heads * (2 * L.key_dim + L.value_dim + a.context);
+    a.num_left = L.num_left;
+    a.stride = L.att_stride;
+    a.key_scale = nl.key_scale;
+    return a;
+}
 
 KfOperand op_base(const void *p, long long ld, int rows, int cols, int kcontig) {
     KfOperand d;
@@ -283,8 +302,15 @@ void identity_bn(std::vector<float> *h, int dim) {  // identityBN, forward.go:11
 
 bool is_trainable(LayerType t) {
     return t == LayerType::ConvReluBN || t == LayerType::TDNNF || t == LayerType::Linear ||
-           t == LayerType::Prefinal || t == LayerType::Output;
+           t == LayerType::Prefinal || t == LayerType::Output || t == LayerType::Attention;
 }
+
+// affine width of an attention layer: heads x (key + value + query key + query context)
+int att_affine(const Layer &L) {
+    const int ctx = 1 + L.num_left + L.num_right;
+    return L.num_heads * (2 * L.key_dim + L.value_dim + ctx);
+}
+
 
 }  // namespace
 
@@ -394,6 +420,20 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
                 nl.pW = add_param(net.get(), n + ".W", din, dout);
                 nl.pb = add_param(net.get(), n + ".Bias", 1, dout);
                 break;
+            case LayerType::Attention: {
+                const int ctx = 1 + L.num_left + L.num_right, A = att_affine(L);
+                if (L.num_heads <= 0 || L.key_dim <= 0 || L.value_dim < 0 || L.att_stride <= 0 || ctx > 64 ||
+                    L.num_heads * ctx > 1024 || A % 8 || dout % 8 || din % 8) {
+                    set_err("attention layer " + n + ": needs heads > 0, key-dim > 0, context <= 64, "
+                            "heads*context <= 1024 and affine / output / input dims multiples of 8");
+                    return nullptr;
+                }
+                nl.pW = add_param(net.get(), n + ".W", din, A);
+                nl.pb = add_param(net.get(), n + ".Bias", 1, A);
+                nl.key_scale = L.key_scale > 0 ? (float)L.key_scale : (float)(1.0 / sqrt((double)L.key_dim));
+                identity_bn(nl.hbn, dout);
+                break;
+            }
             case LayerType::SpecAugment:
             case LayerType::CombineFeatureMaps:
                 break;
@@ -461,7 +501,18 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             }
         }
         int mwidth = 0;
-        if (L.type == LayerType::ConvReluBN || L.type == LayerType::TDNNF) mwidth = dout;
+        if (L.type == LayerType::ConvReluBN || L.type == LayerType::TDNNF || L.type == LayerType::Attention)
+            mwidth = dout;
+        if (L.type == LayerType::Attention) {
+            const int A = att_affine(L), ctx = 1 + L.num_left + L.num_right;
+            nl.aux = net->dalloc((size_t)T * A * 2);
+            nl.dproj = net->dalloc((size_t)T * A * 2);
+            nl.att_scratch = (float *)net->dalloc((size_t)2 * T * L.num_heads * ctx * 4);
+            if (!nl.aux || !nl.dproj || !nl.att_scratch) {
+                set_err("alloc attention buffers");
+                return nullptr;
+            }
+        }
         if (L.type == LayerType::Prefinal) mwidth = L.big_dim;
         if (mwidth) nl.mask = (uint8_t *)net->dalloc(align_up(T * mwidth / 8 + 16, 256));
         if (L.type == LayerType::TDNNF) nl.aux = net->dalloc(T * L.bottleneck * 2);
@@ -485,7 +536,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
         if (L.type == LayerType::ConvReluBN &&
             !upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, L.fout, dout, nl.bn_scale, nl.bn_shift))
             return nullptr;
-        if (L.type == LayerType::TDNNF &&
+        if ((L.type == LayerType::TDNNF || L.type == LayerType::Attention) &&
             !upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, dout, dout, nl.bn_scale, nl.bn_shift))
             return nullptr;
         if (L.type == LayerType::Prefinal &&
@@ -593,6 +644,17 @@ extern "C" int nnet_set_idct(KfNet *net, const char *layer, const float *m, int 
     return -1;
 }
 
+// AttentionSpec.KeyScale from a loaded model (weight_loader.go:266-271)
+extern "C" int nnet_set_key_scale(KfNet *net, const char *layer, float key_scale) {
+    for (auto &nl : net->layers)
+        if (nl.L.name == layer && nl.L.type == LayerType::Attention && key_scale > 0) {
+            nl.key_scale = key_scale;
+            return 0;
+        }
+    set_err(std::string("set_key_scale: no attention layer ") + (layer ? layer : "(null)"));
+    return -1;
+}
+
 extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean,
                            const float *var, const float *gamma, const float *beta, float eps,
                            float target_rms) {
@@ -613,7 +675,8 @@ extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float
                 width = L.out_dim;
             } else if (L.type == LayerType::Prefinal) {
                 dim = width = L.big_dim;
-            } else if (L.type == LayerType::TDNNF || L.type == LayerType::Batchnorm) {
+            } else if (L.type == LayerType::TDNNF || L.type == LayerType::Batchnorm ||
+                       L.type == LayerType::Attention) {
                 dim = width = L.out_dim;
             } else {
                 break;
@@ -885,6 +948,22 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
                 if (!ck(kf_gemm_fused(T, dout, x8 ? nl.w8.ld : din, &A, &B, &E), "linear")) return -1;
                 break;
             }
+            case LayerType::Attention: {
+                // affine on the GPU (forward.go:813-826), then the per-head attention with
+                // ReLU + BatchNorm fused (the reference's CPU loop, :850-908)
+                const int A = att_affine(L);
+                KfOperand Aop = op_base(x, din, T, din, 1);
+                KfOperand B = op_base(wptr(net, nl.pW), A, din, A, 0);
+                KfEpilogue E = epi0();
+                E.out = nl.aux;
+                E.ldo = A;
+                E.bias = wptr(net, nl.pb);
+                if (!ck(kf_gemm_fused(T, A, din, &Aop, &B, &E), "attention affine")) return -1;
+                KfAttention att = att_args(nl, T);
+                if (!ck(kf_attention_forward(&att, nl.act, dout, nl.mask, nl.bn_scale, nl.bn_shift), "attention"))
+                    return -1;
+                break;
+            }
             case LayerType::Prefinal: {
                 const int big = L.big_dim, small = L.small_dim;
                 const Mx *x8 = in8(net, nl);
@@ -974,6 +1053,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
             }
             return true;
         case LayerType::ConvReluBN:
+        case LayerType::Attention:
             E.scale2 = pl.bn_scale;
             E.mask_in = pl.mask;
             return true;
@@ -1052,6 +1132,26 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     KfOperand A2 = op_base(dz, dout, T, dout, 1);
                     KfOperand B2 = op_base(wptr(net, nl.pW), dout, din, dout, 1);
                     if (!ck(kf_gemm_fused(T, din, dout, &A2, &B2, &E), "dgrad")) return -1;
+                }
+                break;
+            }
+            case LayerType::Attention: {
+                // dz = gradient at the attention output (pre-ReLU, from dx_epilogue);
+                // exact attention backward into d(affine output), then the affine's
+                // weight / bias / input gradients
+                const int A = att_affine(L);
+                KfAttention att = att_args(nl, T);
+                if (!ck(kf_attention_backward(&att, dz, dout, nl.dproj, nl.att_scratch), "attention backward"))
+                    return -1;
+                KfOperand Aw = op_base(x, din, T, din, 0);
+                KfOperand Bw = op_base(nl.dproj, A, T, A, 0);
+                if (!ck(kf_gemm_wgrad(din, A, T, &Aw, &Bw, gptr(net, nl.pW), A, gptr(net, nl.pb), 0),
+                        "attention wgrad"))
+                    return -1;
+                if (want_dx) {
+                    KfOperand A2 = op_base(nl.dproj, A, T, A, 1);
+                    KfOperand B2 = op_base(wptr(net, nl.pW), A, din, A, 1);
+                    if (!ck(kf_gemm_fused(T, din, A, &A2, &B2, &E), "attention dgrad")) return -1;
                 }
                 break;
             }

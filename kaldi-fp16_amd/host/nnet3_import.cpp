@@ -420,6 +420,7 @@ struct Loader {
         int d;
     };
     std::vector<Idct> idcts;
+    std::vector<std::pair<std::string, float>> kscales;
     KfLoadStats st{0, 0, 0};
 
     const Comp *need(const std::string &n) {
@@ -626,6 +627,21 @@ extern "C" int nnet_load_kaldi(KfNet *net, const KfNnet3Model *m, int mode, KfLo
                 ok = ok && L.vector(n + ".Bias", c->bias, (n + ".affine bias").c_str());
                 break;
             }
+            case NNET_ATTENTION: {
+                if (mode == KF_LOAD_REPLACE) {  // LoadWeights: "attention loading not implemented"
+                    L.st.layers_skipped++;
+                    continue;
+                }
+                // allocWeightsFromKaldi (:221-275): affine, batchnorm, key scale
+                const Comp *aff = L.need(n + ".affine");
+                ok = aff && L.matrix(n + ".W", *aff, (n + ".affine").c_str());
+                ok = ok && L.vector(n + ".Bias", aff->bias, (n + ".affine bias").c_str());
+                const Comp *b = ok ? L.need(n + ".batchnorm") : nullptr;
+                ok = ok && b && L.bn(n, 0, *b, dout, false, (n + ".batchnorm").c_str());
+                const Comp *at = m->get(n + ".attention");
+                if (ok && at && at->kscale > 0) L.kscales.emplace_back(n, at->kscale);
+                break;
+            }
             default:
                 L.st.layers_skipped++;
                 continue;
@@ -647,6 +663,11 @@ extern "C" int nnet_load_kaldi(KfNet *net, const KfNnet3Model *m, int mode, KfLo
     for (auto &i : L.idcts)
         if (nnet_set_idct(net, i.layer.c_str(), i.m.data(), i.d, i.d) != 0) {
             set_err("nnet_set_idct: %s", nnet_last_error() ? nnet_last_error() : "failed");
+            return -1;
+        }
+    for (auto &k : L.kscales)
+        if (nnet_set_key_scale(net, k.first.c_str(), k.second) != 0) {
+            set_err("nnet_set_key_scale: %s", nnet_last_error() ? nnet_last_error() : "failed");
             return -1;
         }
     if (stats) *stats = L.st;

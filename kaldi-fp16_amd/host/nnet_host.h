@@ -56,6 +56,9 @@ struct Layer {  // layers.go:12-120 (specs flattened)
     int small_dim = 0, big_dim = 0;
     // output
     bool include_log_softmax = true;
+    // attention-relu-batchnorm (layers.go:298-321, AttentionSpec :92-104)
+    int num_heads = 1, key_dim = 0, value_dim = 0, num_left = 0, num_right = 0, att_stride = 1;
+    double key_scale = 0;  // 0 -> 1/sqrt(key_dim) (weight_loader.go:266-271)
 };
 
 bool ParseXConfig(const std::string &text, std::vector<LayerConfig> &out, std::string &err);

@@ -273,6 +273,13 @@ bool ResolveLayers(const std::vector<LayerConfig> &cfgs, std::vector<Layer> &lay
                 int nh = cfg.get_int("num-heads", 1), vd = cfg.get_int("value-dim", 0);
                 int ctx = 1 + cfg.get_int("num-left-inputs", 0) + cfg.get_int("num-right-inputs", 0);
                 L.out_dim = nh * (vd + ctx);
+                L.num_heads = nh;
+                L.value_dim = vd;
+                L.key_dim = cfg.get_int("key-dim", 0);
+                L.num_left = cfg.get_int("num-left-inputs", 0);
+                L.num_right = cfg.get_int("num-right-inputs", 0);
+                L.att_stride = cfg.get_int("time-stride", 1);
+                L.key_scale = cfg.get_float("key-scale", 0.0);
                 break;
             }
             case LayerType::Prefinal: {

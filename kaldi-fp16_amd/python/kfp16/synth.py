@@ -64,7 +64,7 @@ def bn_specs(net_layers, conv_fout: dict, prefinal_dims: dict):
             specs.append((name, 0, dout))
         elif ty == 6:          # conv-relu-batchnorm: per filter
             specs.append((name, 0, conv_fout[name]))
-        elif ty == 7:          # tdnnf
+        elif ty in (7, 8):     # tdnnf, attention-relu-batchnorm
             specs.append((name, 0, dout))
         elif ty == 9:          # prefinal: big then small
             big, small = prefinal_dims[name]

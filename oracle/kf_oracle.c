@@ -306,13 +306,94 @@ static void bias_relu_bn(float *z, int rows, int D, const float *bias, const Orc
     }
 }
 
+/* ---- restricted attention (forward.go:795-909) -------------------------------
+ * proj [T x heads*A] per head [key kd | value vd | query key kd | query ctx]; frame t
+ * attends to rows t + (o - nleft)*stride, zero outside [0, T) (the reference pads). The
+ * per-head loop is the reference's, float32 with the exp in float64. */
+static void att_weights(const OrcLayer *L, const float *proj, int T, int t, int h, float *w) {
+    const int A = 2 * L->kd + L->vd + L->ctx, ld = L->heads * A;
+    const float *q = proj + (size_t)t * ld + (size_t)h * A + L->kd + L->vd;
+    float mx = -1e30f, s = 0.f;
+    for (int o = 0; o < L->ctx; ++o) {
+        const int r = t + (o - L->nleft) * L->astride;
+        float dot = 0.f;
+        if (r >= 0 && r < T) {
+            const float *k = proj + (size_t)r * ld + (size_t)h * A;
+            for (int d = 0; d < L->kd; ++d) dot += q[d] * k[d];
+        }
+        w[o] = q[L->kd + o] + L->key_scale * dot;
+        if (w[o] > mx) mx = w[o];
+    }
+    for (int o = 0; o < L->ctx; ++o) {
+        w[o] = (float)exp((double)(w[o] - mx));
+        s += w[o];
+    }
+    for (int o = 0; o < L->ctx; ++o) w[o] /= s;
+}
+
+static void att_forward(const OrcLayer *L, const float *proj, int T, float *out) {
+    const int A = 2 * L->kd + L->vd + L->ctx, ld = L->heads * A, od = L->vd + L->ctx;
+    float w[64];
+    for (int t = 0; t < T; ++t)
+        for (int h = 0; h < L->heads; ++h) {
+            att_weights(L, proj, T, t, h, w);
+            float *y = out + (size_t)t * L->heads * od + (size_t)h * od;
+            for (int d = 0; d < L->vd; ++d) y[d] = 0.f;
+            for (int o = 0; o < L->ctx; ++o) {
+                const int r = t + (o - L->nleft) * L->astride;
+                if (r >= 0 && r < T) {
+                    const float *v = proj + (size_t)r * ld + (size_t)h * A + L->kd;
+                    for (int d = 0; d < L->vd; ++d) y[d] += w[o] * v[d];
+                }
+                y[L->vd + o] = w[o];
+            }
+        }
+}
+
+/* exact gradient of att_forward: dz [T x heads*od] -> dproj [T x heads*A] */
+static void att_backward(const OrcLayer *L, const float *proj, int T, const float *dz, float *dproj) {
+    const int A = 2 * L->kd + L->vd + L->ctx, ld = L->heads * A, od = L->vd + L->ctx;
+    float w[64], dw[64], db[64];
+    memset(dproj, 0, sizeof(float) * (size_t)T * ld);
+    for (int t = 0; t < T; ++t)
+        for (int h = 0; h < L->heads; ++h) {
+            att_weights(L, proj, T, t, h, w);
+            const float *g = dz + (size_t)t * L->heads * od + (size_t)h * od;
+            const float *qk = proj + (size_t)t * ld + (size_t)h * A + L->kd + L->vd;
+            float sw = 0.f;
+            for (int o = 0; o < L->ctx; ++o) {
+                const int r = t + (o - L->nleft) * L->astride;
+                dw[o] = g[L->vd + o];
+                if (r >= 0 && r < T) {
+                    const float *v = proj + (size_t)r * ld + (size_t)h * A + L->kd;
+                    for (int d = 0; d < L->vd; ++d) dw[o] += g[d] * v[d];
+                }
+                sw += w[o] * dw[o];
+            }
+            float *dq = dproj + (size_t)t * ld + (size_t)h * A + L->kd + L->vd;
+            for (int o = 0; o < L->ctx; ++o) {
+                db[o] = w[o] * (dw[o] - sw);
+                dq[L->kd + o] += db[o];
+                const int r = t + (o - L->nleft) * L->astride;
+                if (r < 0 || r >= T) continue;
+                const float *k = proj + (size_t)r * ld + (size_t)h * A;
+                float *dk = dproj + (size_t)r * ld + (size_t)h * A;
+                for (int d = 0; d < L->kd; ++d) {
+                    dq[d] += L->key_scale * db[o] * k[d];
+                    dk[d] += L->key_scale * db[o] * qk[d];
+                }
+                for (int d = 0; d < L->vd; ++d) dk[L->kd + d] += w[o] * g[d];
+            }
+        }
+}
+
 static int layer_needs_dx(const OrcNet *net, int li) {
     /* does any trainable layer lie below li on its input chain? */
     int cur = net->layers[li].input;
     while (cur >= 0) {
         int ty = net->layers[cur].type;
         if (ty == ORC_CONV || ty == ORC_TDNNF || ty == ORC_LINEAR || ty == ORC_PREFINAL ||
-            ty == ORC_OUTPUT)
+            ty == ORC_OUTPUT || ty == ORC_ATTENTION)
             return 1;
         cur = net->layers[cur].input;
     }
@@ -479,6 +560,19 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 net->aux[li] = bg;
                 break;
             }
+            case ORC_ATTENTION: {
+                const int A = L->heads * (2 * L->kd + L->vd + L->ctx);
+                float *proj = (float *)xalloc(sizeof(float) * (size_t)T * A);
+                orc_matmul(T, A, din, x, L->W, proj);
+                bias_relu_bn(proj, T, A, L->b, NULL, NULL, mode, 0, NULL);
+                if (mode) orc_round_f16(proj, (long long)T * A);  /* the stored fp16 affine output */
+                att_forward(L, proj, T, y);
+                net->mask[li] = (uint8_t *)xalloc((size_t)T * dout);
+                bias_relu_bn(y, T, dout, NULL, &L->bn, net->mask[li], mode, 1, FM(li));
+                if (mode) orc_round_f16(y, (long long)T * dout);
+                net->aux[li] = proj;
+                break;
+            }
             case ORC_OUTPUT:
                 if (x8) wq = mx_cols_new(L->W, din, dout);
                 orc_matmul(T, dout, din, x8 ? x8 : x, x8 ? wq : L->W, y);
@@ -561,6 +655,26 @@ int orc_net_backward_top(OrcNet *net, const float *features, const float *out_gr
                     dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
                     matmul_nt(T, din, dout, dz, L->W, dx); /* W [din x dout] viewed as B^T */
                 }
+                break;
+            }
+            case ORC_ATTENTION: {
+                const int A = L->heads * (2 * L->kd + L->vd + L->ctx);
+                float *dz = (float *)xalloc(sizeof(float) * (size_t)T * dout);
+                for (long long i = 0; i < (long long)T * dout; ++i)
+                    dz[i] = net->mask[li][i] ? g[i] * bn_scale(&L->bn, (int)(i % dout)) : 0.f;
+                if (mode) orc_round_f16(dz, (long long)T * dout);
+                float *dp = (float *)xalloc(sizeof(float) * (size_t)T * A);
+                att_backward(L, net->aux[li], T, dz, dp);
+                free(dz);
+                if (mode) orc_round_f16(dp, (long long)T * A);  /* stored fp16 on the GPU */
+                net->gW[li] = (float *)xalloc(sizeof(float) * (size_t)din * A);
+                matmul_tn(din, A, T, x, dp, net->gW[li]);
+                net->gb[li] = colsum(dp, T, A);
+                if (need_dx) {
+                    dx = (float *)xalloc(sizeof(float) * (size_t)T * din);
+                    matmul_nt(T, din, A, dp, L->W, dx);
+                }
+                free(dp);
                 break;
             }
             case ORC_CONV: {

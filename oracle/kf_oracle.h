@@ -42,6 +42,7 @@ enum {
     ORC_LINEAR = 5,
     ORC_PREFINAL = 6,
     ORC_OUTPUT = 7,
+    ORC_ATTENTION = 8,
 };
 enum { ORC_ROUND_NONE = 0, ORC_ROUND_FUSED = 1, ORC_ROUND_REF = 2 };
 
@@ -70,6 +71,9 @@ typedef struct {
     OrcBN bn;         /* conv / tdnnf / batchnorm-component / prefinal BN1 */
     OrcBN bn2;        /* prefinal BN2 (small dim); mean==NULL -> none */
     int log_softmax;  /* output-layer include-log-softmax=true (forward.go:991-997) */
+    /* attention-relu-batchnorm (forward.go:795-909): W [din x heads*(2kd+vd+ctx)], b */
+    int heads, kd, vd, ctx, nleft, astride;
+    float key_scale;
 } OrcLayer;
 
 typedef struct {

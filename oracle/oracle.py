@@ -55,7 +55,7 @@ def lib(native: bool = False):
     return _lib
 
 
-ORC = dict(IDCT=1, BATCHNORM=2, CONV=3, TDNNF=4, LINEAR=5, PREFINAL=6, OUTPUT=7)
+ORC = dict(IDCT=1, BATCHNORM=2, CONV=3, TDNNF=4, LINEAR=5, PREFINAL=6, OUTPUT=7, ATTENTION=8)
 ROUND_NONE, ROUND_FUSED, ROUND_REF = 0, 1, 2
 
 _fp = C.POINTER(C.c_float)
@@ -73,7 +73,8 @@ class OrcLayer(C.Structure):
                 ("bn_dim", C.c_int), ("stride", C.c_int), ("bypass", C.c_float),
                 ("small_dim", C.c_int), ("big_dim", C.c_int),
                 ("W", _fp), ("b", _fp), ("W2", _fp), ("b2", _fp), ("bn", OrcBN), ("bn2", OrcBN),
-                ("log_softmax", C.c_int)]
+                ("log_softmax", C.c_int), ("heads", C.c_int), ("kd", C.c_int), ("vd", C.c_int),
+                ("ctx", C.c_int), ("nleft", C.c_int), ("astride", C.c_int), ("key_scale", C.c_float)]
 
 
 class OrcNet(C.Structure):
@@ -123,6 +124,12 @@ def parse_xconfig(text: str):
             L.update(small_dim=int(kv["small-dim"]), big_dim=int(kv["big-dim"]), out_dim=int(kv["small-dim"]))
         elif kind == "output-layer":
             L["out_dim"] = int(kv["dim"])
+        elif kind == "attention-relu-batchnorm-layer":   # layers.go:298-321
+            nl_, nr_ = int(kv.get("num-left-inputs", 0)), int(kv.get("num-right-inputs", 0))
+            L.update(heads=int(kv.get("num-heads", 1)), kd=int(kv.get("key-dim", 0)), vd=int(kv.get("value-dim", 0)),
+                     nleft=nl_, ctx=1 + nl_ + nr_, astride=int(kv.get("time-stride", 1)))
+            L["key_scale"] = float(kv.get("key-scale", 0)) or 1.0 / np.sqrt(L["kd"])
+            L["out_dim"] = L["heads"] * (L["vd"] + L["ctx"])
         else:
             raise ValueError(f"oracle: unsupported layer kind {kind}")
         dims[name] = L["out_dim"]
@@ -197,6 +204,12 @@ class OracleNet:
                 o.bn = self._bn(bns.get((n, 0)), L["big_dim"])
                 if (n, 1) in bns:
                     o.bn2 = self._bn(bns[(n, 1)], L["small_dim"])
+            elif kind == "attention-relu-batchnorm-layer":
+                o.type = ORC["ATTENTION"]
+                o.heads, o.kd, o.vd, o.ctx, o.nleft, o.astride = L["heads"], L["kd"], L["vd"], L["ctx"], L["nleft"], L["astride"]
+                o.key_scale = np.float32(L["key_scale"])
+                o.W, o.b = self._p(params[L["name"] + ".W"]), self._p(params[L["name"] + ".Bias"])
+                o.bn = self._bn(bns.get((L["name"], 0)), L["out_dim"])
             elif kind == "output-layer":
                 o.type = ORC["OUTPUT"]
                 o.W, o.b = self._p(params[L["name"] + ".W"]), self._p(params[L["name"] + ".Bias"])
@@ -301,6 +314,10 @@ class OracleNet:
                 out[n + ".BigW"] = get(self.net.gW, i, din * big).reshape(din, big)
                 out[n + ".BigBias"] = get(self.net.gb, i, big).reshape(1, -1)
                 out[n + ".SmallW"] = get(self.net.gW2, i, big * small).reshape(big, small)
+            elif k == "attention-relu-batchnorm-layer":
+                A = L["heads"] * (2 * L["kd"] + L["vd"] + L["ctx"])
+                out[n + ".W"] = get(self.net.gW, i, L["in_dim"] * A).reshape(L["in_dim"], A)
+                out[n + ".Bias"] = get(self.net.gb, i, A).reshape(1, -1)
             elif k == "output-layer":
                 out[n + ".W"] = get(self.net.gW, i, L["in_dim"] * L["out_dim"]).reshape(L["in_dim"], L["out_dim"])
                 out[n + ".Bias"] = get(self.net.gb, i, L["out_dim"]).reshape(1, -1)

@@ -1,0 +1,71 @@
+"""attention-relu-batchnorm layer on the MI355X against the oracle.
+
+Forward: the affine on the fused GEMM, then k_att_fwd (restricted attention + ReLU +
+BatchNorm) — the reference's CPU loop (forward.go:795-909), which the oracle restates
+(tests/test_oracle_attention.py pins it). Backward: the exact gradient (k_att_bwd_q /
+k_att_bwd_kv), compared with the oracle's exact backward (pinned there by finite
+differences). Tolerances: SURVEY §8d (activations 2e-3 rel-Frobenius, gradients 5e-3)."""
+import numpy as np
+import pytest
+
+from conftest import rel_fro
+from test_gpu_nnet import _forward_parity, _oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("T", [96, 301])
+def test_attention_network_forward_backward(gpu, T):
+    kf = gpu
+    from kfp16 import synth
+    xcfg = synth.load_xconfig("tiny_att.xconfig")
+    net = kf.Network(xcfg, max_frames=T)
+    params, bns = synth.init_network(net)
+    feats = synth.make_features(T, 40)
+    fbuf = kf.upload_fp16(feats)
+    net.forward(fbuf.ptr, T)
+    on = _oracle(xcfg, params, bns, feats)
+    masks = _forward_parity(net, on, None)
+    on.close()
+    on = _oracle(xcfg, params, bns, feats)
+    on.forward(feats.astype(np.float32), force_masks=masks)
+    og = (np.random.default_rng(7).standard_normal((T, 200)) * 0.05).astype(np.float16)
+    gbuf = kf.upload_fp16(og)
+    net.backward(gbuf.ptr)
+    got = net.read_grads()
+    on.backward(og.astype(np.float32))
+    ref = on.grads()
+    errs = {k: rel_fro(got[k], ref[k]) for k in ref}
+    bad = {k: v for k, v in errs.items() if v > 5e-3}
+    assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
+
+
+def test_attention_import_key_scale(gpu):
+    """NewNetworkFromKaldi for attention (weight_loader.go:221-275): affine, batchnorm and
+    the <KeyScale> of <name>.attention; a different key scale changes the output."""
+    kf = gpu
+    from kfp16 import model, synth
+    import nnet3_writer as NW
+    import nnet3_text as TT
+    xcfg = synth.load_xconfig("tiny_att.xconfig")
+    T = 96
+    a = kf.Network(xcfg, max_frames=T)
+    params, bns = synth.init_network(a)
+    txt = NW.network_text(a.layers, params, bns)
+    m, v, _, _ = bns[("attention3", 0)]
+    txt += TT.write_component("attention3.affine", "NaturalGradientAffineComponent",
+                              params["attention3.W"].T, params["attention3.Bias"].reshape(-1))
+    txt += TT.write_component("attention3.batchnorm", "BatchNormComponent", mean=m, var=v, bn_dim=len(m))
+    b = kf.Network(xcfg, max_frames=T)
+    model.Nnet3Model.from_text(txt).load_into(b)
+    feats = synth.make_features(T, 40)
+    fbuf = kf.upload_fp16(feats)
+    a.forward(fbuf.ptr, T)
+    b.forward(fbuf.ptr, T)
+    assert np.array_equal(a.read_activation("attention3").view(np.uint16),
+                          b.read_activation("attention3").view(np.uint16))
+    c = kf.Network(xcfg, max_frames=T)
+    model.Nnet3Model.from_text(txt + "<ComponentName> attention3.attention <RestrictedAttentionComponent> "
+                               "<NumHeads> 4 <KeyDim> 16 <ValueDim> 32 <KeyScale> 0.9\n").load_into(c)
+    c.forward(fbuf.ptr, T)
+    assert not np.array_equal(a.read_activation("attention3"), c.read_activation("attention3"))
