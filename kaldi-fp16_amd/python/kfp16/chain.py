@@ -206,3 +206,22 @@ class Chain:
             self.close()
         except Exception:
             pass
+
+
+def den_graph_from_fst(path_or_bytes, num_pdfs: int) -> dict:
+    """NewNativeDenominator's transition extraction (denominator.go:68-117): read den.fst
+    (OpenFst vector or compact acceptor, through the egs FST reader kf_egs_parse_fst),
+    drop epsilon arcs, pdf0 = label - 1, tp = float32(exp(-weight)) computed in float64.
+    Returns the dict DenGraph takes; initial probabilities are left to
+    kf_den_graph_create's 100-iteration rule (denominator.go:131-171)."""
+    from . import egs
+    data = path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray)) else open(path_or_bytes, "rb").read()
+    f = egs.parse_fst(bytes(data))
+    if f is None:
+        raise KfError("failed to parse den.fst (unsupported format?)")
+    src = np.repeat(np.arange(f.num_states, dtype=np.int32), np.diff(f.arc_off))
+    keep = f.label - 1 >= 0
+    tp = np.exp(-f.weight.astype(np.float64)).astype(np.float32)
+    return dict(S=int(f.num_states), P=int(num_pdfs), A=int(keep.sum()), src=src[keep].astype(np.int32),
+                dst=f.next_state[keep].astype(np.int32), pdf0=(f.label[keep] - 1).astype(np.int32),
+                tp=tp[keep], start=int(f.start))

@@ -180,7 +180,7 @@ def write_ark(path, examples: list[bytes]):
 
 
 def make_egs(rng, n, *, rows=(150, 203, 224), feat_kind="CM", ivec_kind="CM2", fst_states=(40, 80),
-             key_prefix="utt", fps=None, with_ivec=True, **kw):
+             key_prefix="utt", fps=None, with_ivec=True, num_pdfs=3080, **kw):
     """n random examples: (list of ark bytes, list of per-example metadata)."""
     exs, meta = [], []
     for e in range(n):
@@ -188,7 +188,7 @@ def make_egs(rng, n, *, rows=(150, 203, 224), feat_kind="CM", ivec_kind="CM2", f
         feats = random_matrix(rng, feat_kind, R, 40)
         ivec = random_matrix(rng, ivec_kind, 1, 100) if with_ivec else None
         S = int(rng.integers(fst_states[0], fst_states[1] + 1))
-        states = random_num_fst(rng, S)
+        states = random_num_fst(rng, S, num_pdfs)
         key = f"{key_prefix}-{e:04d}"
         f = fps if fps is not None else max(1, (R - 60) // 3)
         exs.append(example_bytes(key, feats, ivec, fst_states=states, frames_per_seq=f, **kw))
