@@ -54,7 +54,8 @@ int nnet_param_info(const KfNet *net, int idx, char *name, int namelen, int *row
  * (optimize.go:52-70 via ops_fp16_to_fp32) */
 int nnet_set_params(KfNet *net, const float *host_flat);
 int nnet_get_params(const KfNet *net, float *host_flat); /* fp32 master */
-/* which = 0: the layer's (first) BatchNorm, 1: prefinal's second BatchNorm */
+/* which = 0: the layer's (first) BatchNorm, 1: prefinal's second BatchNorm;
+ * target_rms <= 0: the layer's configured target-rms (a batchnorm-component's, else 1) */
 int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean, const float *var,
                 const float *gamma, const float *beta, float eps, float target_rms);
 
@@ -63,6 +64,11 @@ int nnet_set_idct(KfNet *net, const char *layer, const float *m, int rows, int c
 /* attention layer key scale (> 0); default 1/sqrt(key-dim) or the xconfig key-scale */
 int nnet_set_key_scale(KfNet *net, const char *layer, float key_scale);
 
+/* forward with the ivector input (an input layer named "ivector", read through
+ * ReplaceIndex(ivector, t, 0)): ivectors fp16 [B x ivector-dim] on the device, one row per
+ * sequence; seq_row0 host int[B+1] with the frame offsets (0 ... T). */
+int nnet_forward_ivector(KfNet *net, const void *features_dev, int T, const void *ivectors_dev, int B,
+                         const int *seq_row0);
 /* forward on T frames of fp16 features already in device memory */
 int nnet_forward(KfNet *net, const void *features_dev, int T);
 /* device pointer of a layer's output activation (fp16 [rows x cols]) */

@@ -191,6 +191,30 @@ int kf_attention_forward(const KfAttention *a, void *out, long long ldo, uint8_t
  * layout and ld as proj (every element written); scratch: fp32 [2 x T x heads x context]. */
 int kf_attention_backward(const KfAttention *a, const void *dz, long long ldz, void *dproj, float *scratch);
 
+/* ivector input path (csrc/ivector.hip). dev_seq_off: device int[B+1] frame offsets of
+ * the sequences (seq_off[B] = T); NULL in kf_combine_feature_maps = b is frame-level.
+ * combine: out[t][h*(nf1+nf2) + f] = f < nf1 ? a[t][h*nf1 + f] : b[seq(t)][h*nf2 + f-nf1] */
+int kf_combine_feature_maps(const void *a, long long lda, const void *b, long long ldb, const int *dev_seq_off,
+                            int B, void *out, long long ldo, int T, int height, int nf1, int nf2);
+/* db[s][h*nf2 + g] = sum over the frames t of sequence s of dy[t][h*(nf1+nf2) + nf1 + g] */
+int kf_combine_feature_maps_backward(const void *dy, long long ldy, const int *dev_seq_off, int B, void *db,
+                                     long long ldb, int height, int nf1, int nf2);
+/* small num-filters-in convolution as im2col + GEMM: P [T*hout x kp], column tap*fin + c
+ * = x[t + dt[tap]][ho*sub + dh[tap]][c] (zero outside), columns >= ntaps*fin zero */
+int kf_im2col_small(const void *x, long long ldx, int T, int hin, int hout, int sub, int fin, int ntaps,
+                    const int *dt, const int *dh, void *P, int kp);
+/* its transpose, gather form: dx [T x hin*fin] */
+int kf_col2im_small(const void *dP, int T, int hin, int hout, int sub, int fin, int ntaps, const int *dt,
+                    const int *dh, int kp, void *dx, long long ldx);
+/* per-sequence linear-component on R rows, any dims: y = x . W (fp32 accumulation) and
+ * its weight gradient dW = x^T . g (fp32, overwritten, summed in row order) */
+int kf_rows_gemm(const void *x, long long ldx, const void *W, long long ldw, void *y, long long ldy, int R, int K,
+                 int N);
+int kf_rows_wgrad(const void *x, long long ldx, const void *g, long long ldg, float *dW, long long ldd, int R, int M,
+                  int N);
+/* y[r][c] = x[r][c] * scale[c] (fp16 in / out, fp32 scale) */
+int kf_scale_cols(const void *x, long long ldx, const float *scale, void *y, long long ldy, int rows, int cols);
+
 /* optional HIP-event timing of every GEMM launch on the current stream
  * (class 0 = kf_gemm_fused, 1 = kf_gemm_wgrad); collect sums since reset */
 void kf_prof_enable(int on);

@@ -14,6 +14,7 @@
 //     and the data-parallel gradient exchange is one contiguous buffer.
 // Memory comes from the bridge_* ABI, as the Go layer does (internal/gpu/tensor.go).
 #include <cmath>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -59,6 +60,14 @@ struct NetLayer {
     void *dproj = nullptr;    // attention: fp16 [maxT x affine] gradient of aux (the affine output)
     float *att_scratch = nullptr;  // attention: fp32 [2 x maxT x heads x context]
     float key_scale = 0.f;
+    bool per_seq = false;     // runs on the B per-sequence rows (ReplaceIndex(ivector, t, 0) branch)
+    int input2 = -100;        // combine-feature-maps: second Append input (-2 = ivector input)
+    // small num-filters-in conv (fin not 1 and not a multiple of 32): im2col + GEMM
+    int kp = 0;               // padded K (multiple of 64)
+    void *im2col = nullptr;   // fp16 [maxT*hout x kp], also reused for dP in backward
+    void *wpad = nullptr;     // fp16 [kp x fout], rows >= ntaps*fin zero
+    float *gwpad = nullptr;   // fp32 [kp x fout] weight gradient over the padded K
+    void *gdb = nullptr;      // fp16 per-sequence gradient [maxT x dim] (combine backward)
     bool bypass = false;
     bool needs_dx = false;
     // MXFP8 forward (nnet_set_fp8): output / aux copies written by the producing
@@ -179,6 +188,11 @@ struct KfNet {
     std::vector<std::pair<long long, long long>> offpath;  // (float offset, count) in grad
     int feat_dim = 0, max_T = 0, T = 0;
     const void *features = nullptr;
+    // ivector input: one row per sequence, frames -> sequences by
+    // seq_off (device int[B+1]); layers fed from it run on B rows (per_seq)
+    int ivec_dim = 0, B = 0;
+    const void *ivec = nullptr;
+    int *seq_off = nullptr;
     long long nparams = 0;
     std::vector<ParamRef> params;
     float *master = nullptr, *grad = nullptr, *vel = nullptr;
@@ -332,8 +346,17 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
     std::map<std::string, int> index;  // layer name -> index in net->layers (-1 = input)
     for (const Layer &L : net->all) {
         if (L.type == LayerType::Input) {
-            if (net->feat_dim && net->feat_dim != L.out_dim) {
-                set_err("multiple input layers are not supported (ivector Append: SURVEY §8d)");
+            if (L.name == "ivector") {  // per-sequence input (Kaldi's ivector-dim input)
+                if (net->ivec_dim) {
+                    set_err("more than one ivector input");
+                    return nullptr;
+                }
+                net->ivec_dim = L.out_dim;
+                index[L.name] = -2;
+                continue;
+            }
+            if (net->feat_dim) {
+                set_err("more than one frame-level input layer (only 'input' and 'ivector' are supported)");
                 return nullptr;
             }
             net->feat_dim = L.out_dim;
@@ -342,16 +365,50 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
         }
         NetLayer nl;
         nl.L = L;
-        if (L.input.kind == kf::InputRef::Append || L.input_names.size() != 1) {
-            set_err("layer " + L.name + ": Append inputs are not in the fused path yet");
-            return nullptr;
+        auto is_seq = [&](int idx) { return idx == -2 || (idx >= 0 && net->layers[idx].per_seq); };
+        if (L.input.kind == kf::InputRef::Append) {
+            // only combine-feature-maps takes an Append, of a frame-level and a per-sequence
+            // (or frame-level) input (Kaldi's Append(idct-batchnorm, ivector-batchnorm))
+            if (L.type != LayerType::CombineFeatureMaps || L.input_names.size() != 2) {
+                set_err("layer " + L.name + ": Append is supported as the input of combine-feature-maps, of two layers");
+                return nullptr;
+            }
+            auto a = index.find(L.input_names[0]), b = index.find(L.input_names[1]);
+            if (a == index.end() || b == index.end() || is_seq(a->second)) {
+                set_err("layer " + L.name + ": Append inputs not found, or the first one is per-sequence");
+                return nullptr;
+            }
+            nl.input = a->second;
+            nl.input2 = b->second;
+        } else {
+            if (L.input_names.size() != 1) {
+                set_err("layer " + L.name + ": one input expected");
+                return nullptr;
+            }
+            auto it = index.find(L.input_names[0]);
+            if (it == index.end()) {
+                set_err("layer " + L.name + ": input not found");
+                return nullptr;
+            }
+            nl.input = it->second;
+            // ReplaceIndex(x, t, 0) of a per-sequence source, or anything fed by one
+            nl.per_seq = is_seq(nl.input);
+            if (nl.per_seq && L.type != LayerType::Linear && L.type != LayerType::Batchnorm) {
+                set_err("layer " + L.name + ": only linear-component and batchnorm-component run on the "
+                        "per-sequence (ivector) branch");
+                return nullptr;
+            }
         }
-        auto it = index.find(L.input_names[0]);
-        if (it == index.end()) {
-            set_err("layer " + L.name + ": input not found");
-            return nullptr;
+        if (L.type == LayerType::CombineFeatureMaps) {
+            const int da = nl.input < 0 ? net->feat_dim : net->layers[nl.input].L.out_dim;
+            const int db = nl.input2 == -2 ? net->ivec_dim
+                           : nl.input2 >= 0 ? net->layers[nl.input2].L.out_dim : net->feat_dim;
+            if (nl.input2 == -100 || L.height <= 0 || da != L.height * L.nf1 || db != L.height * L.nf2) {
+                set_err("combine-feature-maps " + L.name + ": needs Append(a, b) with dims height*num-filters1 "
+                        "and height*num-filters2");
+                return nullptr;
+            }
         }
-        nl.input = it->second;
         const int din = L.in_dim, dout = L.out_dim;
         const std::string &n = L.name;
         switch (L.type) {
@@ -379,9 +436,8 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
                     set_err("conv layer " + n + ": need 1..9 (time x height) offsets");
                     return nullptr;
                 }
-                if (L.fin != 1 && L.fin % 32) {
-                    set_err("conv layer " + n + ": num-filters-in must be 1 or a multiple of 32");
-                    return nullptr;
+                if (L.fin != 1 && L.fin % 32) {  // small fin: im2col + GEMM (csrc/ivector.hip)
+                    nl.kp = (int)((nl.dt.size() * L.fin + 63) / 64 * 64);
                 }
                 const int K = (int)nl.dt.size() * L.fin;
                 nl.pW = add_param(net.get(), n + ".W", K, L.fout);
@@ -464,11 +520,14 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
         }
     }
     // which layers need an input gradient (a trainable layer lies below them)
-    for (size_t i = 0; i < net->layers.size(); ++i) {
-        bool need = false;
-        for (int cur = net->layers[i].input; cur >= 0; cur = net->layers[cur].input)
-            if (is_trainable(net->layers[cur].L.type)) need = true;
-        net->layers[i].needs_dx = need;
+    {
+        // a trainable layer lies below idx, along inputs and combine-feature-maps' second input
+        std::function<bool(int)> below = [&](int idx) -> bool {
+            if (idx < 0) return false;
+            const NetLayer &q = net->layers[idx];
+            return is_trainable(q.L.type) || below(q.input) || (q.input2 >= 0 && below(q.input2));
+        };
+        for (size_t i = 0; i < net->layers.size(); ++i) net->layers[i].needs_dx = below(net->layers[i].input);
     }
     // flat parameter storage
     const long long P = net->nparams > 0 ? net->nparams : 64;
@@ -510,6 +569,23 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             nl.att_scratch = (float *)net->dalloc((size_t)2 * T * L.num_heads * ctx * 4);
             if (!nl.aux || !nl.dproj || !nl.att_scratch) {
                 set_err("alloc attention buffers");
+                return nullptr;
+            }
+        }
+        if (L.type == LayerType::ConvReluBN && nl.kp) {
+            nl.im2col = net->dalloc((size_t)T * L.hout * nl.kp * 2);
+            nl.wpad = net->dalloc((size_t)nl.kp * L.fout * 2);
+            nl.gwpad = (float *)net->dalloc((size_t)nl.kp * L.fout * 4);
+            if (!nl.im2col || !nl.wpad || !nl.gwpad) {
+                set_err("alloc small-fin conv buffers");
+                return nullptr;
+            }
+            bridge_gpu_memset(nl.wpad, 0, (size_t)nl.kp * L.fout * 2);
+        }
+        if (L.type == LayerType::CombineFeatureMaps && nl.input2 != -100) {
+            nl.gdb = net->dalloc((size_t)T * L.height * L.nf2 * 2);
+            if (!nl.gdb) {
+                set_err("alloc combine gradient");
                 return nullptr;
             }
         }
@@ -663,6 +739,8 @@ extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float
         const Layer &L = nl.L;
         int dim, width;
         std::vector<float> *h;
+        // target_rms <= 0: the layer's configured target-rms (batchnorm-component's, else 1)
+        if (target_rms <= 0) target_rms = (which != 1 && L.type == LayerType::Batchnorm) ? (float)L.target_rms : 1.0f;
         if (which == 1) {
             if (L.type != LayerType::Prefinal) break;
             dim = width = L.small_dim;
@@ -697,6 +775,7 @@ extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float
 }
 
 static const void *act_of(KfNet *net, int idx) {
+    if (idx == -2) return net->ivec;
     if (idx < 0) return net->features;
     NetLayer &nl = net->layers[idx];
     return nl.act_alias ? act_of(net, nl.input) : nl.act;
@@ -846,7 +925,43 @@ extern "C" int nnet_set_fp8(KfNet *net, int on) {
 // ---------------------------------------------------------------------------
 // forward (Network.Forward, forward.go:148-202)
 // ---------------------------------------------------------------------------
+static int forward_impl(KfNet *net, const void *features, int T);
 extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
+    if (net->ivec_dim) {
+        set_err("forward: the network has an ivector input; use nnet_forward_ivector");
+        return -1;
+    }
+    return forward_impl(net, features, T);
+}
+// forward with per-sequence ivectors: ivectors fp16 [B x ivec_dim] on the device,
+// seq_row0 host int[B+1] frame offsets (seq_row0[0] = 0, seq_row0[B] = T)
+extern "C" int nnet_forward_ivector(KfNet *net, const void *features, int T, const void *ivectors, int B,
+                                    const int *seq_row0) {
+    if (!net->ivec_dim || !ivectors || B <= 0 || B > T || !seq_row0 || seq_row0[0] != 0 || seq_row0[B] != T) {
+        set_err("forward_ivector: needs an ivector input layer, B in [1, T] and seq_row0[0] = 0, seq_row0[B] = T");
+        return -1;
+    }
+    for (int s = 0; s < B; ++s)
+        if (seq_row0[s + 1] <= seq_row0[s]) {
+            set_err("forward_ivector: empty or unordered sequence " + std::to_string(s));
+            return -1;
+        }
+    if (!net->seq_off) {
+        net->seq_off = (int *)net->dalloc(((size_t)net->max_T + 1) * 4);
+        if (!net->seq_off) {
+            set_err("alloc seq offsets");
+            return -1;
+        }
+    }
+    if (bridge_transfer_int32(net->seq_off, seq_row0, (size_t)B + 1)) {
+        set_err("upload seq offsets");
+        return -1;
+    }
+    net->ivec = ivectors;
+    net->B = B;
+    return forward_impl(net, features, T);
+}
+static int forward_impl(KfNet *net, const void *features, int T) {
     if (T <= 0 || T > net->max_T) {
         set_err("forward: T=" + std::to_string(T) + " outside (0, max_frames]");
         return -1;
@@ -863,14 +978,24 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
                 if (!ck(kf_small_gemm(x, din, nl.idct, nl.act, dout, T, din, dout), "idct")) return -1;
                 break;
             case LayerType::Batchnorm:
-                if (!ck(kf_bn_apply(x, nl.act, T, dout, nl.bn_scale, nl.bn_shift), "batchnorm")) return -1;
+                if (!ck(kf_bn_apply(x, nl.act, nl.per_seq ? net->B : T, dout, nl.bn_scale, nl.bn_shift),
+                        "batchnorm"))
+                    return -1;
                 break;
             case LayerType::SpecAugment:
                 break;  // pass-through (forward.go:225-231, masking is a TODO there too)
             case LayerType::CombineFeatureMaps:
-                if (!ck(ops_copy(nl.act, x, T * dout), "combine copy") ||
-                    !ck(ops_combine_feature_maps(nl.act, T, dout, L.height, L.nf1, L.nf2), "combine"))
+                if (nl.input2 != -100) {  // Append(a, b): b broadcast per sequence when per_seq
+                    const bool bseq = nl.input2 == -2 || (nl.input2 >= 0 && net->layers[nl.input2].per_seq);
+                    if (!ck(kf_combine_feature_maps(x, L.height * L.nf1, act_of(net, nl.input2), L.height * L.nf2,
+                                                    bseq ? net->seq_off : nullptr, net->B, nl.act, dout, T,
+                                                    L.height, L.nf1, L.nf2),
+                            "combine"))
+                        return -1;
+                } else if (!ck(ops_copy(nl.act, x, T * dout), "combine copy") ||
+                           !ck(ops_combine_feature_maps(nl.act, T, dout, L.height, L.nf1, L.nf2), "combine")) {
                     return -1;
+                }
                 break;
             case LayerType::ConvReluBN: {
                 if (L.fin == 1) {
@@ -883,6 +1008,25 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
                     break;
                 }
                 const int K = (int)nl.dt.size() * L.fin;
+                if (nl.kp) {  // small fin (Kaldi's cnn1 after combine-feature-maps: 6): im2col + GEMM
+                    if (!ck(kf_im2col_small(x, din, T, L.hin, L.hout, L.hsub, L.fin, (int)nl.dt.size(),
+                                            nl.dt.data(), nl.dh.data(), nl.im2col, nl.kp),
+                            "im2col small") ||
+                        !ck(ops_copy(nl.wpad, wptr(net, nl.pW), K * L.fout), "conv weight pad"))
+                        return -1;
+                    KfOperand A = op_base(nl.im2col, nl.kp, T * L.hout, nl.kp, 1);
+                    KfOperand B = op_base(nl.wpad, L.fout, nl.kp, L.fout, 0);
+                    KfEpilogue E = epi0();
+                    E.out = nl.act;
+                    E.ldo = L.fout;
+                    E.bias = wptr(net, nl.pb);
+                    E.relu = 1;
+                    E.mask_out = nl.mask;
+                    E.scale = nl.bn_scale;
+                    E.shift = nl.bn_shift;
+                    if (!ck(kf_gemm_fused(T * L.hout, L.fout, nl.kp, &A, &B, &E), "conv small fin")) return -1;
+                    break;
+                }
                 KfOperand A = op_im2col(nl, x, T, 1);
                 KfOperand B = op_base(wptr(net, nl.pW), L.fout, K, L.fout, 0);
                 KfEpilogue E = epi0();
@@ -938,6 +1082,12 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
                 break;
             }
             case LayerType::Linear: {
+                if (nl.per_seq) {  // ReplaceIndex branch: one row per sequence, any dims (ivector 100)
+                    if (!ck(kf_rows_gemm(x, din, wptr(net, nl.pW), dout, nl.act, dout, net->B, din, dout),
+                            "ivector linear"))
+                        return -1;
+                    break;
+                }
                 const Mx *x8 = in8(net, nl);
                 KfOperand A = x8 ? op_mx(*x8, T, 1, 0, 0) : op_base(x, din, T, din, 1);
                 KfOperand B = x8 ? op_mxw(nl.w8, dout) : op_base(wptr(net, nl.pW), dout, din, dout, 0);
@@ -1061,6 +1211,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
             if (pl.has_bn2) E.scale2 = pl.bn2_scale;
             return true;
         case LayerType::Linear:
+        case LayerType::CombineFeatureMaps:  // raw gradient; its backward splits it (ivector branch)
             return true;
         default:
             set_err("backward: gradient into layer " + L.name + " is not supported");
@@ -1111,7 +1262,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         const Layer &L = nl.L;
         const int din = L.in_dim, dout = L.out_dim;
         const void *x = act_of(net, nl.input);
-        const bool want_dx = nl.needs_dx && nl.input >= 0;
+        bool want_dx = nl.needs_dx && nl.input >= 0;
         void *dz_next = net->dz[flip], *g_next = net->g[flip];
         KfEpilogue E;
         if (want_dx && !dx_epilogue(net, nl.input, dz_next, g_next, E)) return -1;
@@ -1245,6 +1396,35 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
             }
             case LayerType::ConvReluBN: {
                 const int noff = (int)nl.dt.size();
+                if (nl.kp) {  // small fin: the forward's im2col is still in nl.im2col
+                    // wgrad over the padded K (the pad columns are zero), then the first
+                    // ntaps*fin rows into the flat gradient
+                    const int K = noff * L.fin;
+                    KfOperand A = op_base(nl.im2col, nl.kp, T * L.hout, nl.kp, 0);
+                    KfOperand B = op_base(dz, L.fout, T * L.hout, L.fout, 0);
+                    if (!ck(kf_gemm_wgrad(nl.kp, L.fout, T * L.hout, &A, &B, nl.gwpad, L.fout, gptr(net, nl.pb), 0),
+                            "conv small-fin wgrad") ||
+                        !ck(ops_copy(gptr(net, nl.pW), nl.gwpad, 2 * K * L.fout), "conv small-fin wgrad copy"))
+                        return -1;
+                    if (want_dx) {
+                        if (E.out || E.mask_in || E.scale2 || !E.out2) {
+                            set_err("conv " + L.name + ": small-fin input gradient only into combine-feature-maps");
+                            return -1;
+                        }
+                        // dP = dz . Wpad^T into the im2col buffer, then the gather col2im
+                        KfOperand A2 = op_base(dz, L.fout, T * L.hout, L.fout, 1);
+                        KfOperand B2 = op_base(nl.wpad, L.fout, nl.kp, L.fout, 1);
+                        KfEpilogue Ed = epi0();
+                        Ed.out = nl.im2col;
+                        Ed.ldo = nl.kp;
+                        if (!ck(kf_gemm_fused(T * L.hout, nl.kp, L.fout, &A2, &B2, &Ed), "conv small-fin dgrad") ||
+                            !ck(kf_col2im_small(nl.im2col, T, L.hin, L.hout, L.hsub, L.fin, noff, nl.dt.data(),
+                                                nl.dh.data(), nl.kp, E.out2, din),
+                                "col2im small"))
+                            return -1;
+                    }
+                    break;
+                }
                 if (L.fin == 1) {
                     if (!ck(kf_conv_c1_wgrad(T, L.hin, L.hout, L.hsub, L.fout, noff, nl.dt.data(),
                                              nl.dh.data(), x, dz, gptr(net, nl.pW), gptr(net, nl.pb)),
@@ -1305,10 +1485,53 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 }
                 break;
             }
+            case LayerType::CombineFeatureMaps:
+                if (nl.input2 >= 0 && net->layers[nl.input2].needs_dx + is_trainable(net->layers[nl.input2].L.type)) {
+                    // the ivector branch: sum the broadcast columns per sequence, then back
+                    // through its batchnorm-component(s) and linear-component (B rows)
+                    const bool bseq = net->layers[nl.input2].per_seq;
+                    if (!bseq) {
+                        set_err("combine " + L.name + ": gradient into a frame-level second input not supported");
+                        return -1;
+                    }
+                    const int wb = L.height * L.nf2, rowsB = net->B;
+                    if (!ck(kf_combine_feature_maps_backward(dz, dout, net->seq_off, rowsB, nl.gdb, wb, L.height,
+                                                             L.nf1, L.nf2),
+                            "combine backward"))
+                        return -1;
+                    int cur = nl.input2;
+                    while (cur >= 0) {
+                        NetLayer &q = net->layers[cur];
+                        const int qd = q.L.out_dim;
+                        if (q.L.type == LayerType::Batchnorm) {
+                            if (!ck(kf_scale_cols(nl.gdb, qd, q.bn_scale, nl.gdb, qd, rowsB, qd), "ivector bn backward"))
+                                return -1;
+                        } else if (q.L.type == LayerType::Linear) {
+                            if (!ck(kf_rows_wgrad(act_of(net, q.input), q.L.in_dim, nl.gdb, qd, gptr(net, q.pW), qd,
+                                                  rowsB, q.L.in_dim, qd),
+                                    "ivector linear wgrad"))
+                                return -1;
+                            if (q.input >= 0) {
+                                set_err("ivector branch: a linear-component below another one is not supported");
+                                return -1;
+                            }
+                        } else {
+                            set_err("ivector branch: unsupported layer " + q.L.name);
+                            return -1;
+                        }
+                        cur = q.input;
+                    }
+                }
+                if (nl.needs_dx && nl.input >= 0 && net->layers[nl.input].needs_dx +
+                                                        is_trainable(net->layers[nl.input].L.type)) {
+                    set_err("backward through " + L.name + " into a trainable frame-level input is not supported");
+                    return -1;
+                }
+                want_dx = false;
+                break;
             case LayerType::Batchnorm:
             case LayerType::IDCT:
             case LayerType::SpecAugment:
-            case LayerType::CombineFeatureMaps:
                 if (want_dx) {
                     set_err("backward through " + L.name + " into trainable layers is not supported");
                     return -1;

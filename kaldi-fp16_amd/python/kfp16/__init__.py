@@ -82,6 +82,7 @@ _sig(nnet, "nnet_set_params", _i, _vp, _vp)
 _sig(nnet, "nnet_get_params", _i, _vp, _vp)
 _sig(nnet, "nnet_set_bn", _i, _vp, C.c_char_p, _i, _vp, _vp, _vp, _vp, _f, _f)
 _sig(nnet, "nnet_forward", _i, _vp, _vp, _i)
+_sig(nnet, "nnet_forward_ivector", _i, _vp, _vp, _i, _vp, _i, _vp)
 _sig(nnet, "nnet_activation", _vp, _vp, C.c_char_p, C.POINTER(_i), C.POINTER(_i))
 _sig(nnet, "nnet_backward", _i, _vp, _vp)
 _sig(nnet, "nnet_grad_buffer", _vp, _vp)
@@ -240,7 +241,10 @@ class Network:
         check(nnet.nnet_get_params(self.h, flat.ctypes.data), "nnet_get_params")
         return self.unflatten(flat)
 
-    def set_bn(self, layer, which, mean, var, gamma, beta, eps=1e-3, target_rms=1.0):
+    def set_bn(self, layer, which, mean, var, gamma, beta, eps=1e-3, target_rms=None):
+        """target_rms None: the layer's configured target-rms (1 unless a batchnorm-component
+        sets one)."""
+        target_rms = 0.0 if target_rms is None else target_rms
         arrs = [np.ascontiguousarray(a, dtype=np.float32) for a in (mean, var, gamma, beta)]
         check(nnet.nnet_set_bn(self.h, layer.encode(), which, *[a.ctypes.data for a in arrs],
                                float(eps), float(target_rms)), "nnet_set_bn")
@@ -248,6 +252,14 @@ class Network:
     # compute -----------------------------------------------------------
     def forward(self, features_ptr, T: int):
         check(nnet.nnet_forward(self.h, features_ptr, int(T)), "nnet_forward")
+        self.T = int(T)
+
+    def forward_ivector(self, features_ptr, T: int, ivectors_ptr, seq_row0):
+        """Forward with the ivector input: ivectors fp16 [B x dim] on the device, seq_row0
+        int[B+1] frame offsets of the sequences (0 ... T)."""
+        so = np.ascontiguousarray(seq_row0, dtype=np.int32)
+        check(nnet.nnet_forward_ivector(self.h, features_ptr, int(T), ivectors_ptr, len(so) - 1,
+                                        so.ctypes.data), "nnet_forward_ivector")
         self.T = int(T)
 
     def activation(self, layer: str):

@@ -102,7 +102,7 @@ def init_network(net, seed: int = 42):
     conv_fout, prefinal = layer_dims(net)
     bns = make_bn_all(bn_specs(net.layers, conv_fout, prefinal))
     for (name, which), (m, v, g, b) in bns.items():
-        net.set_bn(name, which, m, v, g, b, eps=1e-3, target_rms=1.0)
+        net.set_bn(name, which, m, v, g, b, eps=1e-3)
     return params, bns
 
 

@@ -387,17 +387,19 @@ static void att_backward(const OrcLayer *L, const float *proj, int T, const floa
         }
 }
 
+static int trainable_below(const OrcNet *net, int cur) {
+    if (cur < 0) return 0;
+    const OrcLayer *L = &net->layers[cur];
+    const int ty = L->type;
+    if (ty == ORC_CONV || ty == ORC_TDNNF || ty == ORC_LINEAR || ty == ORC_PREFINAL || ty == ORC_OUTPUT ||
+        ty == ORC_ATTENTION)
+        return 1;
+    return trainable_below(net, L->input) || (ty == ORC_COMBINE && trainable_below(net, L->input2));
+}
+
 static int layer_needs_dx(const OrcNet *net, int li) {
-    /* does any trainable layer lie below li on its input chain? */
-    int cur = net->layers[li].input;
-    while (cur >= 0) {
-        int ty = net->layers[cur].type;
-        if (ty == ORC_CONV || ty == ORC_TDNNF || ty == ORC_LINEAR || ty == ORC_PREFINAL ||
-            ty == ORC_OUTPUT || ty == ORC_ATTENTION)
-            return 1;
-        cur = net->layers[cur].input;
-    }
-    return 0;
+    /* does any trainable layer lie below li (inputs, and combine's second input)? */
+    return trainable_below(net, net->layers[li].input);
 }
 
 /* ---- OCP MXFP8 (e4m3 + E8M0, blocks of 32) quantise-dequantise ---------- */
@@ -475,9 +477,19 @@ int orc_net_forward(OrcNet *net, const float *features) {
     if (!net->act) alloc_net(net);
     for (int li = 0; li < net->nlayers; ++li) {
         const OrcLayer *L = &net->layers[li];
-        const float *x = L->input < 0 ? features : net->act[L->input];
+        const float *x = L->input == -2 ? net->ivec : L->input < 0 ? features : net->act[L->input];
         const int din = L->in_dim, dout = L->out_dim;
         float *y = (float *)xalloc(sizeof(float) * (size_t)T * dout);
+        if (L->per_seq) { /* linear / batchnorm on the B per-sequence rows */
+            const int R = net->B;
+            if (L->type == ORC_LINEAR) orc_matmul(R, dout, din, x, L->W, y);
+            else if (L->type == ORC_BATCHNORM)
+                for (long long i = 0; i < (long long)R * dout; ++i) y[i] = bn_apply(&L->bn, (int)(i % dout), x[i]);
+            else { free(y); return -1; }
+            if (mode) orc_round_f16(y, (long long)R * dout);
+            net->act[li] = y;
+            continue;
+        }
         /* MXFP8 GEMM input of this layer (the producer's copy), or NULL = fp16 GEMM */
         const float *x8 = MX && L->input >= 0 ? net->act8[L->input] : NULL;
         float *wq = NULL, *wq2 = NULL;
@@ -558,6 +570,20 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 MX_OUT(y, T, small);
                 if (mode) orc_round_f16(y, (long long)T * small);
                 net->aux[li] = bg;
+                break;
+            }
+            case ORC_COMBINE: { /* Kaldi combine-feature-maps; b broadcast per sequence */
+                const int n1 = L->nf1, n2 = L->nf2, nf = n1 + n2, H = L->height;
+                const float *b = L->input2 == -2 ? net->ivec : L->input2 < 0 ? features : net->act[L->input2];
+                const int bseq = L->input2 == -2 || (L->input2 >= 0 && net->layers[L->input2].per_seq);
+                for (int t = 0, s = 0; t < T; ++t) {
+                    while (bseq && s + 1 < net->B && net->seq_off[s + 1] <= t) ++s;
+                    const float *br = b + (size_t)(bseq ? s : t) * H * n2;
+                    for (int h = 0; h < H; ++h)
+                        for (int f = 0; f < nf; ++f)
+                            y[(size_t)t * dout + h * nf + f] =
+                                f < n1 ? x[(size_t)t * H * n1 + h * n1 + f] : br[h * n2 + f - n1];
+                }
                 break;
             }
             case ORC_ATTENTION: {
@@ -782,6 +808,34 @@ int orc_net_backward_top(OrcNet *net, const float *features, const float *out_gr
                 }
                 free(dbig);
                 free(ds);
+                break;
+            }
+            case ORC_COMBINE: {
+                /* the ivector branch: the broadcast columns summed per sequence (from the
+                 * stored fp16 gradient), then back through its batchnorm(s) and linear */
+                if (L->input2 < 0 || !net->layers[L->input2].per_seq) break;
+                const int n1 = L->nf1, n2 = L->nf2, nf = n1 + n2, H = L->height, R = net->B;
+                float *db = (float *)xalloc(sizeof(float) * (size_t)R * H * n2);
+                for (int s2 = 0; s2 < R; ++s2)
+                    for (int t = net->seq_off[s2]; t < net->seq_off[s2 + 1]; ++t)
+                        for (int h = 0; h < H; ++h)
+                            for (int q = 0; q < n2; ++q)
+                                db[(size_t)s2 * H * n2 + h * n2 + q] += gr[(size_t)t * dout + h * nf + n1 + q];
+                if (mode) orc_round_f16(db, (long long)R * H * n2);
+                for (int cur = L->input2; cur >= 0; cur = net->layers[cur].input) {
+                    const OrcLayer *Q = &net->layers[cur];
+                    const int qd = Q->out_dim;
+                    if (Q->type == ORC_BATCHNORM) {
+                        for (long long i = 0; i < (long long)R * qd; ++i) db[i] *= bn_scale(&Q->bn, (int)(i % qd));
+                        if (mode) orc_round_f16(db, (long long)R * qd);
+                    } else if (Q->type == ORC_LINEAR) {
+                        const float *xq = Q->input == -2 ? net->ivec : net->act[Q->input];
+                        net->gW[cur] = (float *)xalloc(sizeof(float) * (size_t)Q->in_dim * qd);
+                        matmul_tn(Q->in_dim, qd, R, xq, db, net->gW[cur]);
+                        break; /* its input is the ivector input */
+                    }
+                }
+                free(db);
                 break;
             }
             case ORC_BATCHNORM:

@@ -43,6 +43,7 @@ enum {
     ORC_PREFINAL = 6,
     ORC_OUTPUT = 7,
     ORC_ATTENTION = 8,
+    ORC_COMBINE = 9,  /* combine-feature-maps of Append(input, input2) */
 };
 enum { ORC_ROUND_NONE = 0, ORC_ROUND_FUSED = 1, ORC_ROUND_REF = 2 };
 
@@ -74,6 +75,9 @@ typedef struct {
     /* attention-relu-batchnorm (forward.go:795-909): W [din x heads*(2kd+vd+ctx)], b */
     int heads, kd, vd, ctx, nleft, astride;
     float key_scale;
+    /* ivector path: input -2 = the ivector input; per_seq layers run on the B sequence
+     * rows (ReplaceIndex(ivector, t, 0)); combine: second input, height, filters */
+    int input2, per_seq, height, nf1, nf2;
 } OrcLayer;
 
 typedef struct {
@@ -99,6 +103,10 @@ typedef struct {
      * quantised copies of producer outputs (taken before the fp16 rounding). */
     int mx8;
     float **act8;
+    /* ivector input: [B x ivec_dim] rows, frames of sequence s = [seq_off[s], seq_off[s+1]) */
+    const float *ivec;
+    int B, ivec_dim;
+    const int *seq_off;
 } OrcNet;
 
 /* OCP MXFP8 quantise-dequantise of rows of `cols` (cols % 32 == 0) values:

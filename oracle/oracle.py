@@ -55,7 +55,7 @@ def lib(native: bool = False):
     return _lib
 
 
-ORC = dict(IDCT=1, BATCHNORM=2, CONV=3, TDNNF=4, LINEAR=5, PREFINAL=6, OUTPUT=7, ATTENTION=8)
+ORC = dict(IDCT=1, BATCHNORM=2, CONV=3, TDNNF=4, LINEAR=5, PREFINAL=6, OUTPUT=7, ATTENTION=8, COMBINE=9)
 ROUND_NONE, ROUND_FUSED, ROUND_REF = 0, 1, 2
 
 _fp = C.POINTER(C.c_float)
@@ -74,7 +74,9 @@ class OrcLayer(C.Structure):
                 ("small_dim", C.c_int), ("big_dim", C.c_int),
                 ("W", _fp), ("b", _fp), ("W2", _fp), ("b2", _fp), ("bn", OrcBN), ("bn2", OrcBN),
                 ("log_softmax", C.c_int), ("heads", C.c_int), ("kd", C.c_int), ("vd", C.c_int),
-                ("ctx", C.c_int), ("nleft", C.c_int), ("astride", C.c_int), ("key_scale", C.c_float)]
+                ("ctx", C.c_int), ("nleft", C.c_int), ("astride", C.c_int), ("key_scale", C.c_float),
+                ("input2", C.c_int), ("per_seq", C.c_int), ("height", C.c_int), ("nf1", C.c_int),
+                ("nf2", C.c_int)]
 
 
 class OrcNet(C.Structure):
@@ -84,7 +86,8 @@ class OrcNet(C.Structure):
                 ("aux", C.POINTER(_fp)), ("gW", C.POINTER(_fp)), ("gb", C.POINTER(_fp)),
                 ("gW2", C.POINTER(_fp)), ("gb2", C.POINTER(_fp)), ("gact", C.POINTER(_fp)),
                 ("force_mask", C.POINTER(C.POINTER(C.c_uint8))), ("mx8", C.c_int),
-                ("act8", C.POINTER(_fp))]
+                ("act8", C.POINTER(_fp)), ("ivec", _fp), ("B", C.c_int), ("ivec_dim", C.c_int),
+                ("seq_off", C.POINTER(C.c_int))]
 
 
 def parse_xconfig(text: str):
@@ -94,6 +97,8 @@ def parse_xconfig(text: str):
         line = raw.strip()
         if not line or line.startswith("#"):
             continue
+        import re as _re
+        line = _re.sub(r"\(([^)]*)\)", lambda m: "(" + m.group(1).replace(" ", "") + ")", line)
         toks = line.split()
         kind, kv = toks[0], dict(t.split("=", 1) for t in toks[1:] if "=" in t)
         name = kv.get("name")
@@ -102,8 +107,16 @@ def parse_xconfig(text: str):
             dims[name] = int(kv["dim"])
             prev = name
             continue
-        din = dims[inp]
-        L = dict(kind=kind, name=name, input=inp, in_dim=din, kv=kv)
+        inp2 = None
+        if inp.startswith("Append(") and inp.endswith(")"):       # xconfig.go:304-313
+            parts = inp[7:-1].split(",")
+            inp, inp2 = parts[0], parts[1]
+            din = dims[inp] + dims[inp2]
+        else:
+            if inp.startswith("ReplaceIndex(") and inp.endswith(")"):   # xconfig.go:315-320
+                inp = inp[13:-1].split(",")[0]
+            din = dims[inp]
+        L = dict(kind=kind, name=name, input=inp, input2=inp2, in_dim=din, kv=kv)
         if kind == "idct-layer":
             L["out_dim"] = int(kv.get("dim", din))
         elif kind == "batchnorm-component":
@@ -124,6 +137,9 @@ def parse_xconfig(text: str):
             L.update(small_dim=int(kv["small-dim"]), big_dim=int(kv["big-dim"]), out_dim=int(kv["small-dim"]))
         elif kind == "output-layer":
             L["out_dim"] = int(kv["dim"])
+        elif kind == "combine-feature-maps-layer":       # layers.go:240-251
+            L.update(out_dim=din, height=int(kv["height"]), nf1=int(kv.get("num-filters1", 1)),
+                     nf2=int(kv.get("num-filters2", 1)))
         elif kind == "attention-relu-batchnorm-layer":   # layers.go:298-321
             nl_, nr_ = int(kv.get("num-left-inputs", 0)), int(kv.get("num-right-inputs", 0))
             L.update(heads=int(kv.get("num-heads", 1)), kd=int(kv.get("key-dim", 0)), vd=int(kv.get("value-dim", 0)),
@@ -165,11 +181,19 @@ class OracleNet:
                  mx8=False):
         self.L = parse_xconfig(xconfig)
         self.keep = []
-        index = {}
+        index = {"ivector": -2}
         arr = (OrcLayer * len(self.L))()
+        per_seq = set()
         for i, L in enumerate(self.L):
             o = arr[i]
             o.input = index.get(L["input"], -1)
+            o.input2 = index.get(L["input2"], -1) if L.get("input2") else -100
+            if L.get("input2") is None and (o.input == -2 or o.input in per_seq):
+                o.per_seq = 1
+                per_seq.add(i)
+            if L["kind"] == "combine-feature-maps-layer":
+                o.type = ORC["COMBINE"]
+                o.height, o.nf1, o.nf2 = L["height"], L["nf1"], L["nf2"]
             o.in_dim, o.out_dim = L["in_dim"], L["out_dim"]
             kind = L["kind"]
             if kind == "idct-layer":
@@ -235,8 +259,9 @@ class OracleNet:
         m, v, g, b = spec
         return OrcBN(self._p(m), self._p(v), self._p(g), self._p(b), 1e-3, target_rms)
 
-    def forward(self, features: np.ndarray, force_masks: dict = None):
-        """force_masks: layer name -> uint8 ReLU decisions to replay (see kf_oracle.h)."""
+    def forward(self, features: np.ndarray, force_masks: dict = None, ivectors=None, seq_off=None):
+        """force_masks: layer name -> uint8 ReLU decisions to replay (see kf_oracle.h).
+        ivectors [B x dim] and seq_off int[B+1]: the ivector input (ReplaceIndex rows)."""
         x = np.ascontiguousarray(features, dtype=np.float32)
         fm = None
         if force_masks:
@@ -256,6 +281,13 @@ class OracleNet:
         self.net.feat_dim = x.shape[1]
         self.net.round_mode = self.round_mode
         self.net.mx8 = int(self.mx8)
+        if ivectors is not None:
+            iv = np.ascontiguousarray(ivectors, dtype=np.float32)
+            so = np.ascontiguousarray(seq_off, dtype=np.int32)
+            self.keep += [iv, so]
+            self.net.ivec = iv.ctypes.data_as(_fp)
+            self.net.B, self.net.ivec_dim = iv.shape
+            self.net.seq_off = so.ctypes.data_as(C.POINTER(C.c_int))
         if fm is not None:
             self.net.force_mask = fm
         rc = lib().orc_net_forward(C.byref(self.net), x.ctypes.data)
@@ -263,7 +295,7 @@ class OracleNet:
 
     def act(self, name):
         i = self.index[name]
-        T, d = self.net.T, self.L[i]["out_dim"]
+        T, d = (self.net.B if self.arr[i].per_seq else self.net.T), self.L[i]["out_dim"]
         return np.ctypeslib.as_array(self.net.act[i], shape=(T * d,)).reshape(T, d).copy()
 
     def mask(self, name):
