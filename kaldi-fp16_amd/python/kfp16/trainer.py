@@ -13,9 +13,14 @@ plus, for data parallel, the flat-gradient all-reduce between 3 and 4 (kfp16.dp)
 The numerator FSTs come from the batch's per-sequence CSRs (TrainingBatch.PerSeqCSRs),
 the denominator from a DenGraph the caller builds (NativeDenominator's transitions).
 Everything runs on the GPU; this module only sequences the calls.
+
+A network with Kaldi's ivector input (`input name=ivector`, ReplaceIndex(ivector, t, 0))
+gets the batch's per-eg ivectors, expanded on the GPU next to the features, with one
+sequence per eg (nnet_forward_ivector). The reference drops them at this point.
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass
 
 import numpy as np
@@ -65,6 +70,10 @@ class EgsTrainer:
         if grad_buffer_ptr is not None:
             self.net.bind_grad_buffer(grad_buffer_ptr)
         self.out_ptr = self.net.activation("output")[0]
+        m = re.search(r"^\s*input\s+name=ivector\s+dim=(\d+)", xconfig, re.M)
+        self.ivec_dim = int(m.group(1)) if m else 0
+        self.ivec = DeviceBuffer(max_egs * self.ivec_dim * 2) if self.ivec_dim else None
+        self.max_egs = max_egs
 
     def step(self, batch, allreduce=None):
         """One TrainStep on `batch` (kfp16.egs.TrainingBatch). allreduce: optional callable
@@ -73,10 +82,20 @@ class EgsTrainer:
         T = batch.total_frames
         if T > self.max_frames or batch.feat_dim != 40:
             raise ValueError(f"batch of {T} frames x {batch.feat_dim} does not fit the trainer")
-        batch.features_to_device(self.feat.ptr, 40)
+        if self.ivec_dim:
+            if batch.ivector_dim != self.ivec_dim or batch.batch_size > self.max_egs:
+                raise ValueError(f"batch of {batch.batch_size} egs with {batch.ivector_dim}-dim ivectors does "
+                                 f"not fit the trainer's {self.ivec_dim}-dim ivector input")
+            batch.features_to_device(self.feat.ptr, 40, self.ivec.ptr)
+        else:
+            batch.features_to_device(self.feat.ptr, 40)
         # rows the objective does not write must be zero for this batch
         core.bridge_gpu_memset(self.grad_out.ptr, 0, T * self.P * 2)
-        self.net.forward(self.feat.ptr, T)
+        if self.ivec_dim:
+            seq = np.append(np.asarray(batch.frame_offsets, np.int32), np.int32(T))
+            self.net.forward_ivector(self.feat.ptr, T, self.ivec.ptr, seq)
+        else:
+            self.net.forward(self.feat.ptr, T)
         num = _chain.NumBatch(batch.num_fsts())
         row0, frames = chain_rows(batch.frame_offsets, batch.num_frames, batch.frames_per_seq,
                                   self.cfg.subsampling_factor, self.cfg.left_context)

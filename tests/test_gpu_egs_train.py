@@ -66,3 +66,42 @@ def test_egs_training_improves_objective(gpu, tmp_path):
         objs.append(r.objf / r.frames)
     assert all(np.isfinite(objs)), objs
     assert objs[-1] > objs[0], objs
+
+
+def test_egs_training_with_ivectors(gpu, tmp_path):
+    """Kaldi's ivector front end fed from the egs' own ivectors (one per eg): the step's
+    objective equals the direct path fed with the host-decompressed features and
+    ivectors, and training improves it."""
+    kf = gpu
+    from kfp16 import chain, synth
+    batch, den, trainer = _setup(kf, tmp_path)
+    assert batch.ivector_dim == 100
+    xcfg = synth.load_xconfig("tiny_ivec.xconfig")
+    tr = trainer.EgsTrainer(xcfg, den, max_egs=8, max_frames=1200,
+                            config=trainer.TrainConfig(learning_rate=0.0, momentum=0.0))
+    synth.init_network(tr.net)
+    tr.step(batch)
+    r1 = tr.result()
+    assert r1.num_ok == batch.batch_size and np.isfinite(r1.objf)
+    net = kf.Network(xcfg, max_frames=1200)
+    synth.init_network(net)
+    T = batch.total_frames
+    fbuf = kf.upload_fp16(batch.features_host().astype(np.float16))
+    ibuf = kf.upload_fp16(batch.ivectors_host().astype(np.float16))
+    net.forward_ivector(fbuf.ptr, T, ibuf.ptr, np.append(np.asarray(batch.frame_offsets, np.int32), T))
+    obj = chain.Chain(chain.DenGraph(den), max_seqs=8, max_frames=401)
+    row0, frames = trainer.chain_rows(batch.frame_offsets, batch.num_frames, batch.frames_per_seq, 3, 30)
+    g = kf.DeviceBuffer(T * 200 * 2)
+    kf.core.bridge_gpu_memset(g.ptr, 0, T * 200 * 2)
+    obj.compute(chain.NumBatch(batch.num_fsts()), net.activation("output")[0], 200, T, row0, frames, 3, g.ptr, 200)
+    r2 = obj.result()
+    assert (r1.objf, r1.den_logprob) == (r2.objf, r2.den_logprob)
+    tr2 = trainer.EgsTrainer(xcfg, den, max_egs=8, max_frames=1200,
+                             config=trainer.TrainConfig(learning_rate=2e-4, momentum=0.0))
+    synth.init_network(tr2.net)
+    objs = []
+    for _ in range(4):
+        tr2.step(batch)
+        r = tr2.result()
+        objs.append(r.objf / r.frames)
+    assert all(np.isfinite(objs)) and objs[-1] > objs[0], objs
