@@ -431,6 +431,10 @@ struct SellDev {  // sliced ELL, 64 rows per slice, rows sorted by degree
     int nsl;
     const int *perm, *len, *off;
     const uint2 *arc;     // {f1 | f2 << 16, tp}
+    // f and b only, when 64 + S + P < 16384: the same records with f1, f2 replaced by
+    // the LDS byte addresses of their operands in the NS = 1 recursion layout
+    // (value row at byte 256, exp row after it), so the gathers need no address VALU
+    const uint2 *arc_s;
     const float *initp;   // init[perm[c]] in slice order (0 for padding rows), f and b only
 };
 struct DenDev {
@@ -648,6 +652,11 @@ __device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, in
     }
 }
 
+// float at LDS byte address `a` of the dynamic LDS (a pre-scaled record field)
+__device__ __forceinline__ float lds_at(const unsigned char *smem, int a) {
+    return *reinterpret_cast<const float *>(smem + a);
+}
+
 // gather-sum over one slice of a SELL table (fixed arc order); arcs may be a
 // global table or the LDS cache (callers branch, so each call's space is static)
 template <class Term>
@@ -765,7 +774,10 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     auto astore = [&](int q) { return r.alpha_store + (size_t)(unit * NS + q) * (r.max_frames + 1) * rs; };
     auto asum = [&](int q) { return r.asum_store + (size_t)(unit * NS + q) * (r.max_frames + 1); };
 
-    const SellLds F = stage_sell(g.f, gi, G, nk, sbase, X.cache_f);
+    const bool scaled = NS == 1 && g.f.arc_s != nullptr;
+    SellDev tf = g.f;
+    if (scaled) tf.arc = g.f.arc_s;
+    const SellLds F = stage_sell(tf, gi, G, nk, sbase, X.cache_f);
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
     const float as0 = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
@@ -813,12 +825,19 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
             pq[q] = 0.f;
         }
         auto term = [&](int q, int src, int pdf, float tp) { return va[q * S + src] * tp * xe[q * PP + pdf]; };
+        auto term_s = [&](int, int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
         for (int k = wave; k < nk; k += DEN_WAVES) {
             const int j = gi + G * k;
             const int st = F.perm[j * 64 + lane];
             float acc[NS];
-            if (k < F.kc) sell_slice_ns<NS>(F.cache, F.len[j], F.coff[k], lane, acc, term);
-            else sell_slice_ns<NS>(g.f.arc, F.len[j], F.off[j], lane, acc, term);
+            if (scaled) {
+                if (k < F.kc) sell_slice_ns<NS>(F.cache, F.len[j], F.coff[k], lane, acc, term_s);
+                else sell_slice_ns<NS>(tf.arc, F.len[j], F.off[j], lane, acc, term_s);
+            } else if (k < F.kc) {
+                sell_slice_ns<NS>(F.cache, F.len[j], F.coff[k], lane, acc, term);
+            } else {
+                sell_slice_ns<NS>(g.f.arc, F.len[j], F.off[j], lane, acc, term);
+            }
 #pragma unroll
             for (int q = 0; q < NS; ++q) {
                 const float v = (st >= 0 && live[q]) ? acc[q] * inv[q] : 0.0f;
@@ -942,7 +961,10 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
     auto bstore = [&](int q) { return r.beta_store + (size_t)(unit * NS + q) * (r.max_frames + 1) * rs; };
     const float leaky = r.leaky;
 
-    const SellLds B = stage_sell(g.b, gi, G, nk, sbase, X.cache_b);
+    const bool scaled = NS == 1 && g.b.arc_s != nullptr;
+    SellDev tbl = g.b;
+    if (scaled) tbl.arc = g.b.arc_s;
+    const SellLds B = stage_sell(tbl, gi, G, nk, sbase, X.cache_b);
     // BetaDashLastFrame up to the per-frame factor: beta'[T] = 1, <init, 1> = sum(init)
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
@@ -979,12 +1001,19 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
             pq[q] = 0.f;
         }
         auto term = [&](int q, int dst, int pdf, float tp) { return vb[q * S + dst] * tp * xe[q * PP + pdf]; };
+        auto term_s = [&](int, int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
         for (int k = wave; k < nk; k += DEN_WAVES) {  // kernel_den_backward_transitions
             const int j = gi + G * k;
             const int st = B.perm[j * 64 + lane];
             float acc[NS];
-            if (k < B.kc) sell_slice_ns<NS>(B.cache, B.len[j], B.coff[k], lane, acc, term);
-            else sell_slice_ns<NS>(g.b.arc, B.len[j], B.off[j], lane, acc, term);
+            if (scaled) {
+                if (k < B.kc) sell_slice_ns<NS>(B.cache, B.len[j], B.coff[k], lane, acc, term_s);
+                else sell_slice_ns<NS>(tbl.arc, B.len[j], B.off[j], lane, acc, term_s);
+            } else if (k < B.kc) {
+                sell_slice_ns<NS>(B.cache, B.len[j], B.coff[k], lane, acc, term);
+            } else {
+                sell_slice_ns<NS>(g.b.arc, B.len[j], B.off[j], lane, acc, term);
+            }
             const float ipj = B.initp[j * 64 + lane];
 #pragma unroll
             for (int q = 0; q < NS; ++q) {
@@ -1398,6 +1427,23 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
     put(d.f, sf);
     put(d.b, sb);
     put(d.q, sq);
+    // pre-scaled copies for the NS = 1 recursions: value row at byte 256 (64 floats of
+    // reduction scratch before it), exp row at 256 + 4 S (den_fwd_body / den_bwd_body)
+    const bool fit16 = 256 + 4 * ((size_t)S + P + 1) < 65536;
+    const bool want_s = !getenv("KF_DEN_SCALED") || atoi(getenv("KF_DEN_SCALED"));
+    auto scaled = [&](const Sell &h) {
+        std::vector<uint2> a(h.arcs);
+        for (auto &r : a) {
+            const uint32_t f1 = r.x & 0xFFFF, f2 = r.x >> 16;
+            r.x = (256 + 4 * f1) | ((256 + 4 * ((uint32_t)S + f2)) << 16);
+        }
+        return a;
+    };
+    if (fit16 && want_s) {
+        d.f.arc_s = dev_upload(scaled(sf), t->owned);
+        d.b.arc_s = dev_upload(scaled(sb), t->owned);
+        ok = ok && d.f.arc_s && d.b.arc_s;
+    }
     std::vector<float> zf(sf.perm.size(), 0.0f), zb(sb.perm.size(), 0.0f);
     d.f.initp = dev_upload(zf, t->owned);  // filled by den_tables_set_init
     d.b.initp = dev_upload(zb, t->owned);
