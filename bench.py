@@ -73,6 +73,13 @@ def pmc_traffic(kernel_class):
         return None
 
 
+def ivector_input(xcfg):
+    """dim of the xconfig's `input name=ivector` (Kaldi's front end), else 0."""
+    import re
+    m = re.search(r"^\s*input\s+name=ivector\s+dim=(\d+)", xcfg, re.M)
+    return int(m.group(1)) if m else 0
+
+
 def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
     """The C oracle (a port of the reference's CNN-TDNN math and chain objective)
     timed on host cores: forward, objective on the subsampled frames, backward."""
@@ -90,8 +97,13 @@ def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
     g, init = den
     row0, nfr, stride = synth.chain_layout(1, frames)
     rows = row0[0] + np.arange(nfr[0]) * stride
+    D = ivector_input(xcfg)
+    iv = (np.random.default_rng(5).standard_normal((1, D)) * 2).astype(np.float32) if D else None
     t0 = time.perf_counter()
-    on.forward(feats)
+    if D:
+        on.forward(feats, ivectors=iv, seq_off=np.array([0, frames], np.int32))
+    else:
+        on.forward(feats)
     out = on.act("output")
     deriv, _ = oracle.chain_objf(g, init, num_fst, out[rows])
     og = np.zeros_like(out)
@@ -99,8 +111,9 @@ def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
     on.backward(og)
     dt = time.perf_counter() - t0
     on.close()
+    name = "cnn_tdnn_17f with the ivector front end" if D else "cnn_tdnn_17f"
     return {"value": round(frames / dt, 2), "unit": "frames/sec", "cores": threads, "kind": "port",
-            "sample": f"C oracle train step (fwd, chain objective, bwd) of cnn_tdnn_17f on {frames} "
+            "sample": f"C oracle train step (fwd, chain objective, bwd) of {name} on {frames} "
                       f"frames (1 eg), fp32 math, {threads} threads for the GEMMs, {dt:.1f} s"}
 
 
@@ -146,8 +159,18 @@ def main():
     gbuf = torch.zeros((T, P), dtype=torch.float16, device="cuda")
     torch.cuda.synchronize()
 
+    # Kaldi's ivector front end: one ivector per eg, one sequence per eg
+    ivd = ivector_input(xcfg)
+    if ivd:
+        ivecs = (np.random.default_rng(99 + rank).standard_normal((a.egs, ivd)) * 2).astype(np.float16)
+        ibuf = torch.from_numpy(ivecs.view(np.int16)).to("cuda")
+        seq_off = np.arange(a.egs + 1, dtype=np.int32) * FRAMES_PER_EG
+
     def step():
-        net.forward(fbuf.data_ptr(), T)
+        if ivd:
+            net.forward_ivector(fbuf.data_ptr(), T, ibuf.data_ptr(), seq_off)
+        else:
+            net.forward(fbuf.data_ptr(), T)
         if a.mode == "forward":
             return
         objective.compute(nbatch, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
@@ -198,6 +221,8 @@ def main():
         fwd_only = a.mode == "forward"
         workload = ("cnn_tdnn_17f forward only (configs[1])" if fwd_only else
                     "cnn_tdnn_17f train step (fwd+bwd+SGD)") + f", {a.egs} egs x 1500 frames per GPU"
+        if ivd:
+            workload += f", Kaldi ivector front end ({ivd}-dim ivector per eg)"
         out = {
             "metric": METRIC_FWD if fwd_only else METRIC, "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),

@@ -13,11 +13,12 @@ from conftest import max_abs_rel, rel_fro
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("T,B", [(150, 3), (301, 5)])
-def test_ivector_network_forward_backward(gpu, T, B):
+@pytest.mark.parametrize("cfg,T,B", [("tiny_ivec.xconfig", 150, 3), ("tiny_ivec.xconfig", 301, 5),
+                                      ("cnn_tdnn_17f_ivec.xconfig", 240, 2)])
+def test_ivector_network_forward_backward(gpu, cfg, T, B):
     kf = gpu
     from kfp16 import synth
-    xcfg = synth.load_xconfig("tiny_ivec.xconfig")
+    xcfg = synth.load_xconfig(cfg)
     net = kf.Network(xcfg, max_frames=T)
     params, bns = synth.init_network(net)
     feats = synth.make_features(T, 40)
@@ -47,7 +48,8 @@ def test_ivector_network_forward_backward(gpu, T, B):
     on.close()
     on = O.OracleNet(xcfg, tp, bns, round_mode=O.ROUND_FUSED, threads=16)
     on.forward(feats.astype(np.float32), force_masks=masks, ivectors=ivec.astype(np.float32), seq_off=seq)
-    og = (np.random.default_rng(7).standard_normal((T, 200)) * 0.05).astype(np.float16)
+    P = [dout for name, ty, din, dout in net.layers if name == "output"][0]
+    og = (np.random.default_rng(7).standard_normal((T, P)) * 0.05).astype(np.float16)
     gbuf = kf.upload_fp16(og)
     net.backward(gbuf.ptr)
     got = net.read_grads()
