@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("cfg,T,B", [("tiny_ivec.xconfig", 150, 3), ("tiny_ivec.xconfig", 301, 5),
-                                      ("cnn_tdnn_17f_ivec.xconfig", 240, 2)])
+                                      ("cnn_tdnn_17f_ivec.xconfig", 240, 2),
+                                      ("cnn_tdnn_17f_kaldi.xconfig", 240, 2)])
 def test_ivector_network_forward_backward(gpu, cfg, T, B):
     kf = gpu
     from kfp16 import synth
@@ -59,6 +60,9 @@ def test_ivector_network_forward_backward(gpu, cfg, T, B):
     bad = {k: v for k, v in errs.items() if v > 5e-3}
     assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
     assert np.abs(got["ivector-linear.W"]).sum() > 0
+    for k in got:  # the xent branch (Kaldi recipe config) gets no gradient
+        if k.startswith(("prefinal-xent.", "output-xent.")):
+            assert not np.any(got[k]), k
 
 
 def test_ivector_input_required(gpu):
