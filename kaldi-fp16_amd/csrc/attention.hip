@@ -53,19 +53,35 @@ __device__ __forceinline__ const h16 *row_ptr(const AttD &d, int r, int h) {
     return d.proj + (long long)r * d.ldp + (long long)h * d.A;
 }
 
+// The ctx dot products of a frame (length kd or vd) are split over the wave: 2^lg lanes
+// per context position (2^lg * ctx <= 64), each summing a strided part, then a
+// butterfly within the lane group. Returns, in lane o < ctx, <a, row(r_o) + off>.
+__device__ __forceinline__ int att_lg(int ctx) {
+    int lg = 6;
+    while ((ctx << lg) > 64) --lg;
+    return lg;
+}
+__device__ __forceinline__ float split_dot(const AttD &d, int t, int h, int lane, int lg, const h16 *a, int off,
+                                           int n) {
+    const int G = 1 << lg, o = lane >> lg, sub = lane & (G - 1);
+    float dot = 0.f;
+    if (o < d.ctx) {
+        const int r = t + (o - d.nleft) * d.stride;
+        if (r >= 0 && r < d.T) {
+            const h16 *k = row_ptr(d, r, h) + off;
+            for (int j = sub; j < n; j += G) dot += (float)a[j] * (float)k[j];
+        }
+    }
+    for (int m = G >> 1; m > 0; m >>= 1) dot += __shfl_xor(dot, m);
+    return __shfl(dot, min(lane, d.ctx - 1) << lg);
+}
+
 // softmax weights of (t, h) into w[ctx] (lane o holds w_o; also returned); lanes >= ctx: 0
 __device__ __forceinline__ float att_weights(const AttD &d, int t, int h, int lane) {
     const h16 *q = row_ptr(d, t, h) + d.kd + d.vd;  // query key part, then query context
+    const float dot = split_dot(d, t, h, lane, att_lg(d.ctx), q, 0, d.kd);
     float b = -INFINITY;
-    if (lane < d.ctx) {
-        const int r = t + (lane - d.nleft) * d.stride;
-        float dot = 0.f;
-        if (r >= 0 && r < d.T) {
-            const h16 *k = row_ptr(d, r, h);
-            for (int j = 0; j < d.kd; ++j) dot += (float)q[j] * (float)k[j];
-        }
-        b = (float)q[d.kd + lane] + d.key_scale * dot;
-    }
+    if (lane < d.ctx) b = (float)q[d.kd + lane] + d.key_scale * dot;
     const float mx = wave_max(b);
     const float e = lane < d.ctx ? expf(b - mx) : 0.f;
     const float s = wave_sum(e);
@@ -123,18 +139,9 @@ __global__ __launch_bounds__(64 * kWaves) void k_att_bwd_q(AttD d, const h16 *dz
     for (int h = 0; h < d.H; ++h) {
         const float w = att_weights(d, t, h, lane);
         const h16 *g = dz + (long long)t * ldz + (long long)h * od;  // [dz_v (vd) | dz_w (ctx)]
+        const float gv = split_dot(d, t, h, lane, att_lg(d.ctx), g, d.kd, d.vd);  // <dz_v, value(r_o)>
         float dw = 0.f;
-        int r = -1;
-        if (lane < d.ctx) {
-            r = t + (lane - d.nleft) * d.stride;
-            dw = (float)g[d.vd + lane];
-            if (r >= 0 && r < d.T) {
-                const h16 *v = row_ptr(d, r, h) + d.kd;
-                float acc = 0.f;
-                for (int j = 0; j < d.vd; ++j) acc += (float)g[j] * (float)v[j];
-                dw += acc;
-            }
-        }
+        if (lane < d.ctx) dw = (float)g[d.vd + lane] + gv;
         const float wdw = wave_sum(lane < d.ctx ? w * dw : 0.f);
         const float db = lane < d.ctx ? w * (dw - wdw) : 0.f;
         h16 *dq = dproj + (long long)t * d.ldp + (long long)h * d.A + d.kd + d.vd;

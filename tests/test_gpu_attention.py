@@ -9,16 +9,18 @@ import numpy as np
 import pytest
 
 from conftest import rel_fro
+import oracle
 from test_gpu_nnet import _forward_parity, _oracle
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("T", [96, 301])
-def test_attention_network_forward_backward(gpu, T):
+@pytest.mark.parametrize("cfg,T", [("tiny_att.xconfig", 96), ("tiny_att.xconfig", 301),
+                                   ("cnn_tdnn_17f_att.xconfig", 240)])
+def test_attention_network_forward_backward(gpu, cfg, T):
     kf = gpu
     from kfp16 import synth
-    xcfg = synth.load_xconfig("tiny_att.xconfig")
+    xcfg = synth.load_xconfig(cfg)
     net = kf.Network(xcfg, max_frames=T)
     params, bns = synth.init_network(net)
     feats = synth.make_features(T, 40)
@@ -29,15 +31,34 @@ def test_attention_network_forward_backward(gpu, T):
     on.close()
     on = _oracle(xcfg, params, bns, feats)
     on.forward(feats.astype(np.float32), force_masks=masks)
-    og = (np.random.default_rng(7).standard_normal((T, 200)) * 0.05).astype(np.float16)
+    P = [dout for name, ty, din, dout in net.layers if name == "output"][0]
+    og = (np.random.default_rng(7).standard_normal((T, P)) * 0.05).astype(np.float16)
     gbuf = kf.upload_fp16(og)
     net.backward(gbuf.ptr)
     got = net.read_grads()
     on.backward(og.astype(np.float32))
     ref = on.grads()
     errs = {k: rel_fro(got[k], ref[k]) for k in ref}
-    bad = {k: v for k, v in errs.items() if v > 5e-3}
-    assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
+    if cfg == "tiny_att.xconfig":
+        bad = {k: v for k, v in errs.items() if v > 5e-3}
+        assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
+        return
+    # At full width (8 heads, key 64, value 128) the softmax backward w (dw - <w, dw>)
+    # cancels, and fp16 rounding of its inputs moves the gradients at and below the layer
+    # by ~1e-2 in the oracle's own F mode against fp32 (scripts/att_precision.py). The
+    # bar is then: no further from the fp32 oracle than the F restatement is, x1.25.
+    on.close()
+    on = oracle.OracleNet(xcfg, {k: synth.trunc_fp16(v) for k, v in params.items()}, bns,
+                          round_mode=oracle.ROUND_NONE, threads=16)
+    on.forward(feats.astype(np.float32), force_masks=masks)
+    on.backward(og.astype(np.float32))
+    f32 = on.grads()
+    bad = {}
+    for k in ref:
+        g_err, f_err = rel_fro(got[k], f32[k]), rel_fro(ref[k], f32[k])
+        if g_err > max(5e-3, 1.25 * f_err) or g_err > 3e-2:
+            bad[k] = (g_err, f_err)
+    assert not bad, "grad errors vs fp32 (gpu, F): " + ", ".join(f"{k}={a:.2e}/{b:.2e}" for k, (a, b) in bad.items())
 
 
 def test_attention_import_key_scale(gpu):
