@@ -52,6 +52,17 @@ __device__ __forceinline__ float wave_sum(float v) {
 __device__ __forceinline__ const h16 *row_ptr(const AttD &d, int r, int h) {
     return d.proj + (long long)r * d.ldp + (long long)h * d.A;
 }
+// context position o of frame t: inside the sequence? and element `col` of its head-h
+// row, loaded unconditionally (row clamped into [0, T), o clamped to ctx - 1) so that
+// a group of loads can be in flight together; callers select with ctx_live
+__device__ __forceinline__ bool ctx_live(const AttD &d, int t, int o) {
+    const int r = t + (o - d.nleft) * d.stride;
+    return r >= 0 && r < d.T;
+}
+__device__ __forceinline__ float ctx_load(const AttD &d, int t, int h, int o, int col) {
+    const int r = t + (min(o, d.ctx - 1) - d.nleft) * d.stride;
+    return (float)row_ptr(d, min(max(r, 0), d.T - 1), h)[col];
+}
 
 // The ctx dot products of a frame (length kd or vd) are split over the wave: 2^lg lanes
 // per context position (2^lg * ctx <= 64), each summing a strided part, then a
@@ -109,9 +120,13 @@ __global__ __launch_bounds__(64 * kWaves) void k_att_fwd(AttD d, h16 *out, long 
         if (c < width) {
             const int h = c / od, j = c - h * od;
             if (j < d.vd) {
-                for (int o = 0; o < d.ctx; ++o) {
-                    const int r = t + (o - d.nleft) * d.stride;
-                    if (r >= 0 && r < d.T) y += w[h * d.ctx + o] * (float)row_ptr(d, r, h)[d.kd + j];
+                for (int o0 = 0; o0 < d.ctx; o0 += 8) {  // 8 row loads in flight, same order
+                    float v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) v[i] = ctx_load(d, t, h, o0 + i, d.kd + j);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (o0 + i < d.ctx && ctx_live(d, t, o0 + i)) y += w[h * d.ctx + o0 + i] * v[i];
                 }
             } else {
                 y = w[h * d.ctx + (j - d.vd)];
@@ -154,10 +169,16 @@ __global__ __launch_bounds__(64 * kWaves) void k_att_bwd_q(AttD d, const h16 *dz
         for (int j0 = 0; j0 < d.kd; j0 += 64) {
             const int j = j0 + lane;
             float acc = 0.f;
-            for (int o = 0; o < d.ctx; ++o) {
-                const float dbo = __shfl(db, o);
-                const int ro = t + (o - d.nleft) * d.stride;
-                if (j < d.kd && ro >= 0 && ro < d.T) acc += dbo * (float)row_ptr(d, ro, h)[j];
+            const int jc = min(j, d.kd - 1);
+            for (int o0 = 0; o0 < d.ctx; o0 += 8) {  // 8 row loads in flight, same order
+                float v[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = ctx_load(d, t, h, o0 + i, jc);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float dbo = __shfl(db, min(o0 + i, 63));
+                    if (j < d.kd && o0 + i < d.ctx && ctx_live(d, t, o0 + i)) acc += dbo * v[i];
+                }
             }
             if (j < d.kd) dq[j] = (h16)(d.key_scale * acc);
         }
@@ -177,14 +198,26 @@ __global__ __launch_bounds__(64 * kWaves) void k_att_bwd_kv(AttD d, const h16 *d
             const int j = j0 + lane;
             float acc = 0.f;
             if (j < d.kd + d.vd) {
-                for (int o = 0; o < d.ctx; ++o) {
-                    const int t = r - (o - d.nleft) * d.stride;
-                    if (t < 0 || t >= d.T) continue;
-                    const long long s = ((long long)t * d.H + h) * d.ctx + o;
-                    if (j < d.kd)  // key: s * db_o(t) * qkey(t)
-                        acc += dbst[s] * (float)row_ptr(d, t, h)[d.kd + d.vd + j];
-                    else           // value: w_o(t) * dz_v(t)
-                        acc += wst[s] * (float)dz[(long long)t * ldz + (long long)h * od + (j - d.kd)];
+                for (int o0 = 0; o0 < d.ctx; o0 += 8) {  // 8 gathers in flight, same order
+                    float c[8], v[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int oc = min(o0 + i, d.ctx - 1);
+                        const int tc = min(max(r - (oc - d.nleft) * d.stride, 0), d.T - 1);
+                        const long long s = ((long long)tc * d.H + h) * d.ctx + oc;
+                        if (j < d.kd) {  // key: s * db_o(t) * qkey(t)
+                            c[i] = dbst[s];
+                            v[i] = (float)row_ptr(d, tc, h)[d.kd + d.vd + j];
+                        } else {         // value: w_o(t) * dz_v(t)
+                            c[i] = wst[s];
+                            v[i] = (float)dz[(long long)tc * ldz + (long long)h * od + (j - d.kd)];
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const int t = r - (o0 + i - d.nleft) * d.stride;
+                        if (o0 + i < d.ctx && t >= 0 && t < d.T) acc += c[i] * v[i];
+                    }
                 }
                 if (j < d.kd) acc *= d.key_scale;
                 dk[j] = (h16)acc;
