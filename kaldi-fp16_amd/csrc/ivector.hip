@@ -52,20 +52,30 @@ __global__ void k_combine_fm(const h16 *a, long long lda, const h16 *b, long lon
     }
 }
 
-// one thread per (sequence, column of b); frames of the sequence in order
-__global__ void k_combine_fm_bwd(const h16 *dy, long long ldy, const int *seq_off, int B, h16 *db, long long ldb,
-                                 int height, int n1, int n2) {
-    const int nb = height * n2;
-    const long long total = (long long)B * nb;
-    const int nf = n1 + n2;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-         i += (long long)gridDim.x * blockDim.x) {
-        const int s = (int)(i / nb), c = (int)(i - (long long)s * nb);
+// one block per (sequence, 64 columns of b): 16 frame groups x 64 columns; group q sums
+// frames q, q+16, ... of the sequence in order, then the 16 partials are added in
+// group order (deterministic)
+constexpr int kFmGroups = 16;
+__global__ __launch_bounds__(64 * kFmGroups) void k_combine_fm_bwd(const h16 *dy, long long ldy, const int *seq_off,
+                                                                 int B, h16 *db, long long ldb, int height, int n1,
+                                                                 int n2) {
+    __shared__ float part[kFmGroups][64];
+    const int nb = height * n2, nchunk = (nb + 63) / 64;
+    const int s = blockIdx.x / nchunk, c = (blockIdx.x % nchunk) * 64 + (threadIdx.x & 63);
+    const int q = threadIdx.x >> 6, nf = n1 + n2;
+    float acc = 0.f;
+    if (s < B && c < nb) {
         const int h = c / n2, g = c - h * n2;
-        const int col = h * nf + n1 + g;
-        float acc = 0.f;
-        for (int t = seq_off[s]; t < seq_off[s + 1]; ++t) acc += (float)dy[(long long)t * ldy + col];
-        db[(long long)s * ldb + c] = (h16)acc;
+        const h16 *col = dy + h * nf + n1 + g;
+        for (int t = seq_off[s] + q; t < seq_off[s + 1]; t += kFmGroups) acc += (float)col[(long long)t * ldy];
+    }
+    part[q][threadIdx.x & 63] = acc;
+    __syncthreads();
+    if (q == 0 && s < B && c < nb) {
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < kFmGroups; ++k) sum += part[k][threadIdx.x];
+        db[(long long)s * ldb + c] = (h16)sum;
     }
 }
 
@@ -74,21 +84,33 @@ struct SmallConv {
     int dt[KF_MAX_PARTS], dh[KF_MAX_PARTS];
 };
 
+// one thread per 8 consecutive columns of a row (kp % 8 == 0): one 16-byte store
 __global__ void k_im2col_small(const h16 *x, long long ldx, SmallConv c, h16 *P) {
     const long long rows = (long long)c.T * c.hout;
-    const long long total = rows * c.kp;
+    const int kg = c.kp / 8;
+    const long long total = rows * kg;
+    const int kr = c.ntaps * c.fin;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
-        const long long m = i / c.kp;
-        const int k = (int)(i - m * c.kp);
+        const long long m = i / kg;
+        const int k0 = (int)(i - m * kg) * 8;
         const int t = (int)(m / c.hout), ho = (int)(m - (long long)t * c.hout);
-        h16 v = (h16)0.f;
-        if (k < c.ntaps * c.fin) {
-            const int tap = k / c.fin, ch = k - tap * c.fin;
-            const int ts = t + c.dt[tap], hs = ho * c.sub + c.dh[tap];
-            if (ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin) v = x[(long long)ts * ldx + hs * c.fin + ch];
+        half8 o;
+        int tap = k0 / c.fin, ch = k0 - tap * c.fin;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            h16 v = (h16)0.f;
+            if (k0 + e < kr) {
+                const int ts = t + c.dt[tap], hs = ho * c.sub + c.dh[tap];
+                if (ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin) v = x[(long long)ts * ldx + hs * c.fin + ch];
+            }
+            o[e] = v;
+            if (++ch == c.fin) {
+                ch = 0;
+                ++tap;
+            }
         }
-        P[i] = v;
+        *reinterpret_cast<half8 *>(P + m * c.kp + k0) = o;
     }
 }
 
@@ -202,9 +224,9 @@ extern "C" int kf_combine_feature_maps_backward(const void *dy, long long ldy, c
         kf_report_error("kf_combine_feature_maps_backward: bad arguments");
         return -1;
     }
-    const long long total = (long long)B * height * nf2;
-    k_combine_fm_bwd<<<kf_blocks(total, 256, 16384), 256, 0, kf_stream()>>>(
-        (const h16 *)dy, ldy, dev_seq_off, B, (h16 *)db, ldb, height, nf1, nf2);
+    const int nchunk = (height * nf2 + 63) / 64;
+    k_combine_fm_bwd<<<B * nchunk, 64 * kFmGroups, 0, kf_stream()>>>((const h16 *)dy, ldy, dev_seq_off, B,
+                                                                     (h16 *)db, ldb, height, nf1, nf2);
     return launch_check("kf_combine_feature_maps_backward");
 }
 
@@ -212,7 +234,11 @@ extern "C" int kf_im2col_small(const void *x, long long ldx, int T, int hin, int
                                int ntaps, const int *dt, const int *dh, void *P, int kp) {
     SmallConv c;
     if (!x || !P || !small_conv(c, T, hin, hout, sub, fin, ntaps, dt, dh, kp, "kf_im2col_small")) return -1;
-    const long long total = (long long)T * hout * kp;
+    if (kp % 8 || ((uintptr_t)P & 15)) {
+        kf_report_error("kf_im2col_small: kp must be a multiple of 8 and P 16-byte aligned");
+        return -1;
+    }
+    const long long total = (long long)T * hout * (kp / 8);
     k_im2col_small<<<kf_blocks(total, 256, 16384), 256, 0, kf_stream()>>>((const h16 *)x, ldx, c, (h16 *)P);
     return launch_check("kf_im2col_small");
 }
