@@ -4,22 +4,35 @@
 Metric (BASELINE.json): frames/sec CNN-TDNN fwd+bwd, 40-dim x 1500-frame egs,
 1/2/4/8 MI355X. One step = TrainStep (train_step.go:142-283): forward, chain
 LF-MMI objective + derivative (numerator and leaky-HMM denominator per eg,
-backward.go:224-371), backward, gradient all-reduce (N > 1) and SGD, over one
-minibatch of 64 synthetic egs (96,000 frames) per GPU, on the pinned synthetic
-17-TDNN-F model (configs/cnn_tdnn_17f.xconfig) with the synthetic den graph and
-numerator FSTs of SURVEY §8d. Inputs are resident in HBM before the timed region.
+backward.go:224-371), backward with the gradient all-reduce overlapped (N > 1,
+kf_dp over RCCL), and SGD, over one minibatch of 64 synthetic egs (96,000 frames)
+per GPU, on the pinned synthetic 17-TDNN-F model (configs/cnn_tdnn_17f.xconfig)
+with the synthetic den graph and numerator FSTs of SURVEY §8d. Inputs are
+resident in HBM before the timed region.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL all-reduce of the flat fp32
-gradient). Rank 0 prints ONE JSON line.
+Launch:
+  python bench.py [--gpus N --steps K --warmup W]
+    N = 1: one process on GPU 0.
+    N > 1 without WORLD_SIZE in the environment: this process starts N worker
+      processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*) before touching any
+      GPU and exits with their status.
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    one rank per GPU; WORLD_SIZE must equal --gpus.
+  --selftest: the same launch and argument path on CPU (gloo), exchanging a flat
+    gradient buffer by the network's bucket plan (no GPU needed).
+Rank 0 prints ONE JSON line. At N = 1 it also carries sub-results measured in the
+same run for BASELINE configs[0] (CPU affine + the GPU GEMM of the same shape),
+configs[1] (forward only) and configs[4] (3072 model, MXFP8 GEMMs).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-# torch first: kfp16's libraries then bind to the same HIP runtime (kfp16.hip_runtimes)
+# torch first: kfp16's libraries then bind to the same HIP runtime and RCCL (kfp16.hip_runtimes)
 import torch
 import torch.distributed as dist
 
@@ -32,10 +45,11 @@ METRIC = "frames/sec CNN-TDNN fwd+bwd, 40-dim×1500-frame egs, 1/2/4/8 MI355X"
 METRIC_FWD = "frames/sec CNN-TDNN forward only, 40-dim×1500-frame egs, 1 MI355X"
 PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5000.0    # MI355X dense FP8 (MX-scaled K=128 MFMA)
+PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 FRAMES_PER_EG = 1500
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -46,17 +60,57 @@ def parse():
     # 31,360 supervised frames per GPU, 1e-8 keeps the random-init model from diverging
     p.add_argument("--lr", type=float, default=1e-8)
     p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--bucket-mb", type=float, default=16.0,
+                   help="gradient all-reduce bucket size (N > 1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the configs[0]/[1]/[4] sub-results at N = 1")
+    p.add_argument("--extra-steps", type=int, default=5)
     p.add_argument("--cpu-frames", type=int, default=1500)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0, help="0: every host core")
     p.add_argument("--no-prof", action="store_true")
     p.add_argument("--fp8", action="store_true",
                    help="MXFP8 forward GEMMs (configs[4]; use with --xconfig cnn_tdnn_17f_3072.xconfig)")
     p.add_argument("--mode", choices=("train", "forward"), default="train",
                    help="train: the metric's fwd+bwd+SGD step; forward: configs[1], forward only")
-    return p.parse_args()
+    p.add_argument("--selftest", action="store_true",
+                   help="CPU (gloo) check of the launcher and the bucketed gradient exchange")
+    return p.parse_args(argv)
 
 
+# --------------------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """Start n worker processes of this script, one per GPU, and return their exit
+    status. Runs before anything touches a GPU; nothing is exec'd in place."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc
+                for q in live:   # a dead rank leaves the others in a collective: stop them
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
+# --------------------------------------------------------------------------- helpers
 def pmc_traffic(kernel_class):
     """HBM bytes per launch of a kernel class from the newest committed rocprofv3
     PMC summary (profiles/r*_pmc_traffic.json, scripts/pmc_traffic.sh), or None."""
@@ -80,9 +134,43 @@ def ivector_input(xcfg):
     return int(m.group(1)) if m else 0
 
 
+def host_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def roofline(prof, steps, peak_tflops):
+    """Dominant GEMM class: algorithmic FLOPs and algorithmic HBM bytes (kf_prof_collect2)
+    over its HIP-event time on the launch stream; the bound is whichever floor is longer."""
+    dom = max(prof, key=lambda k: prof[k][1])
+    n, ms, fl, by = prof[dom]
+    t_mfma = fl / (peak_tflops * 1e12)
+    t_hbm = by / (PEAK_HBM_GBPS * 1e9)
+    sec = ms * 1e-3
+    tf = fl / sec / 1e12 if sec > 0 else 0.0
+    gbps = by / sec / 1e9 if sec > 0 else 0.0
+    if t_hbm > t_mfma:
+        r = {"bound": "hbm", "achieved": round(gbps, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+             "frac": round(gbps / PEAK_HBM_GBPS, 4)}
+    else:
+        r = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak_tflops, "unit": "TFLOP/s",
+             "frac": round(tf / peak_tflops, 4)}
+    r.update({"kernel": dom, "launches": n, "kernel_ms_per_step": round(ms / steps, 3),
+              "mfma_tflops": round(tf, 2), "mfma_frac": round(tf / peak_tflops, 4),
+              "alg_GBps": round(gbps, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
+              "alg_bytes_per_launch": round(by / max(n, 1)), "flops_per_launch": round(fl / max(n, 1)),
+              "floor_ms_per_step": {"mfma": round(t_mfma * 1e3 / steps, 3), "hbm": round(t_hbm * 1e3 / steps, 3)},
+              "all_gemm_tflops": round(sum(v[2] for v in prof.values()) /
+                                       max(sum(v[1] for v in prof.values()) * 1e-3, 1e-12) / 1e12, 2)})
+    return r
+
+
 def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
-    """The C oracle (a port of the reference's CNN-TDNN math and chain objective)
-    timed on host cores: forward, objective on the subsampled frames, backward."""
+    """The C oracle (a restatement of the reference's CNN-TDNN math and chain objective,
+    not the Go code: no Go toolchain here) timed on host cores: forward, objective on
+    the subsampled frames, backward."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from kfp16 import synth
@@ -112,35 +200,108 @@ def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
     dt = time.perf_counter() - t0
     on.close()
     name = "cnn_tdnn_17f with the ivector front end" if D else "cnn_tdnn_17f"
-    return {"value": round(frames / dt, 2), "unit": "frames/sec", "cores": threads, "kind": "port",
-            "sample": f"C oracle train step (fwd, chain objective, bwd) of {name} on {frames} "
-                      f"frames (1 eg), fp32 math, {threads} threads for the GEMMs, {dt:.1f} s"}
+    return {"value": round(frames / dt, 2), "unit": "frames/sec", "cores": threads, "host_cores": host_cores(),
+            "kind": "port",
+            "sample": f"restatement, not Go: C oracle train step (fwd, chain objective, bwd) of {name} on "
+                      f"{frames} frames (1 eg), fp32 math, GEMM rows split over {threads} threads "
+                      f"(go/gotorch/ops.go:49-81 policy), {dt:.1f} s"}
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
+def config1_affine(threads, reps=50):
+    """BASELINE configs[0]: gotorch.AffineLayer(40, 512).Forward on [1500 x 40] float64
+    (go/gotorch/layers.go:57-70, ops.go:15-81), restated in C (oracle/gotorch_cpu.c),
+    median of `reps`; next to the same affine on the GPU through the reference's
+    ops_gemm ABI (fp16 MFMA, fp32 accumulation), median of `reps` event-timed calls."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import kfp16
+    rng = np.random.default_rng(0)
+    M, K, N = 1500, 40, 512
+    x = rng.standard_normal((M, K))
+    W = rng.standard_normal((K, N)) * np.sqrt(2.0 / (K + N))
+    b = np.zeros(N)
+    L = oracle.lib()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        y = oracle.gotorch_affine_forward(x, W, b, threads, L)
+        ts.append(time.perf_counter() - t0)
+    cpu_ms = float(np.median(ts)) * 1e3
+    # GPU: ops_gemm (ops.h) on fp16 copies, the kaldi-fp16 plumbing of the same layer
+    xa = torch.from_numpy(x.astype(np.float16)).cuda()
+    wa = torch.from_numpy(W.astype(np.float16)).cuda()
+    ya = torch.empty((M, N), dtype=torch.float16, device="cuda")
+    h = kfp16.core.ops_cublas_create()
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        kfp16.check(kfp16.core.ops_gemm(h, M, N, K, 1.0, xa.data_ptr(), K, wa.data_ptr(), N, 0.0,
+                                        ya.data_ptr(), N), "ops_gemm")
+    g = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        kfp16.core.ops_gemm(h, M, N, K, 1.0, xa.data_ptr(), K, wa.data_ptr(), N, 0.0, ya.data_ptr(), N)
+        e1.record(st)
+        e1.synchronize()
+        g.append(e0.elapsed_time(e1))
+    kfp16.core.ops_cublas_destroy(h)
+    err = float(np.abs(ya.float().cpu().numpy() - y).max() / np.abs(y).max())
+    gpu_ms = float(np.median(g))
+    return {"workload": "AffineLayer(40,512).Forward on [1500 x 40] (configs[0])",
+            "cpu_ms_median": round(cpu_ms, 3), "cpu_frames_per_sec": round(M / (cpu_ms * 1e-3), 1),
+            "cpu": {"kind": "port", "cores": threads, "host_cores": host_cores(), "reps": reps,
+                    "sample": "restatement, not Go: oracle/gotorch_cpu.c, float64, matmulParallel rows "
+                              "over the thread count"},
+            "gpu_ops_gemm_ms_median": round(gpu_ms, 4), "gpu_frames_per_sec": round(M / (gpu_ms * 1e-3), 1),
+            "gpu_vs_cpu_max_rel_err": round(err, 5)}
 
+
+# --------------------------------------------------------------------------- selftest (CPU)
+def selftest(a, rank, world):
+    """gloo: the bench's launch / argument path plus the bucketed exchange of a flat
+    gradient buffer laid out and planned by the product (nnet_create_layout,
+    nnet_dp_plan), checked against the rank average."""
     import kfp16
     from kfp16 import dp, synth
-    kfp16.check(kfp16.core.bridge_gpu_init(local), "bridge_gpu_init")
-    stream = torch.cuda.current_stream()
-    kfp16.set_stream(stream.cuda_stream)
-    kfp16.assert_single_hip_runtime()
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == a.gpus == world
+    net = kfp16.Network(synth.load_xconfig(a.xconfig), max_frames=1, layout_only=True)
+    plan = net.dp_plan(int(a.bucket_mb * (1 << 20)))
+    assert dp.covers_exactly(plan, net.num_params)
+    grads = [np.random.default_rng(100 + r).standard_normal(net.num_params).astype(np.float32)
+             for r in range(world)]
+    flat = torch.from_numpy(grads[rank].copy())
+    dp.exchange_by_plan(flat, plan, world)
+    want = np.mean(np.stack(grads), axis=0, dtype=np.float64).astype(np.float32)
+    err = float(np.abs(flat.numpy() - want).max())
+    ok = torch.tensor([1.0 if err < 1e-6 else 0.0])
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    t = dp.max_over_ranks(float(rank), "cpu")
+    if rank == 0:
+        print(json.dumps({"selftest": bool(ok.item() == 1.0), "n_gpus": world, "backend": "gloo",
+                          "xconfig": a.xconfig, "num_params": net.num_params, "buckets": len(plan),
+                          "plan": plan, "max_abs_err": err, "max_over_ranks": t}), flush=True)
+    net.close()
+    dist.destroy_process_group()
+    return 0 if ok.item() == 1.0 else 1
+
+
+# --------------------------------------------------------------------------- one workload
+def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_on, keep=False):
+    """Build the network, den graph and egs of one workload, time `steps` steps.
+    Returns (stats dict, context for the CPU baseline)."""
+    import kfp16
+    from kfp16 import chain, dp, synth
 
     T = a.egs * FRAMES_PER_EG
-    xcfg = synth.load_xconfig(a.xconfig)
+    xcfg = synth.load_xconfig(xconfig)
     net = kfp16.Network(xcfg, max_frames=T)
     params, bns = synth.init_network(net, seed=42)        # identical replicas on every rank
-    if a.fp8:
+    if fp8:
         net.set_fp8(True)
-    grad = torch.zeros(net.num_params, dtype=torch.float32, device="cuda")
-    net.bind_grad_buffer(grad.data_ptr())
+    bucket_bytes = int(a.bucket_mb * (1 << 20))
+    if comm is not None and mode == "train":
+        net.bind_dp(comm, bucket_bytes)                    # bucketed all-reduce inside backward
 
     feats = synth.make_features(T, 40, seed=1234 + rank)   # this rank's shard of egs
     fbuf = torch.from_numpy(feats.view(np.int16)).to("cuda")
@@ -148,7 +309,6 @@ def main():
     # chain supervision: shared den graph, one numerator FST per eg
     # (seed 7 + global eg index); the objective writes the output gradient on the
     # subsampled rows (leftCtx 30, stride 3) — every other row stays zero
-    from kfp16 import chain
     den_g = synth.make_den_graph(num_pdfs=P)
     dgraph = chain.DenGraph(den_g)
     fsts = [synth.make_num_fst(dp.eg_index(rank, a.egs, e), num_pdfs=P) for e in range(a.egs)]
@@ -159,9 +319,8 @@ def main():
     gbuf = torch.zeros((T, P), dtype=torch.float16, device="cuda")
     torch.cuda.synchronize()
 
-    # Kaldi's ivector front end: one ivector per eg, one sequence per eg
     ivd = ivector_input(xcfg)
-    if ivd:
+    if ivd:  # Kaldi's ivector front end: one ivector per eg, one sequence per eg
         ivecs = (np.random.default_rng(99 + rank).standard_normal((a.egs, ivd)) * 2).astype(np.float16)
         ibuf = torch.from_numpy(ivecs.view(np.int16)).to("cuda")
         seq_off = np.arange(a.egs + 1, dtype=np.int32) * FRAMES_PER_EG
@@ -171,27 +330,27 @@ def main():
             net.forward_ivector(fbuf.data_ptr(), T, ibuf.data_ptr(), seq_off)
         else:
             net.forward(fbuf.data_ptr(), T)
-        if a.mode == "forward":
+        if mode == "forward":
             return
         objective.compute(nbatch, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
-        net.backward(gbuf.data_ptr())
-        dp.allreduce_mean_(grad, world)   # the one data-path collective (RCCL)
+        net.backward(gbuf.data_ptr())       # + the overlapped gradient all-reduce (N > 1)
         net.sgd(a.lr, a.momentum)
 
-    for _ in range(a.warmup):
+    for _ in range(warmup):
         step()
-        if os.environ.get("KF_BENCH_CHECK"):
+        if os.environ.get("KF_BENCH_CHECK") and mode == "train":
             r = objective.result()
             print("warmup objf/frame", r.objf / max(r.frames, 1), "ok", r.num_ok, flush=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    if not a.no_prof:
+    if prof_on:
         kfp16.core.kf_prof_reset()
         kfp16.core.kf_prof_enable(1)
+    dp0 = comm.stats() if comm is not None else (0, 0)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -199,33 +358,105 @@ def main():
     elapsed = time.perf_counter() - t0
     kfp16.core.kf_prof_enable(0)
     elapsed = dp.max_over_ranks(elapsed, "cuda")
+    dp1 = comm.stats() if comm is not None else (0, 0)
 
     prof, chain_prof = {}, {}
-    if not a.no_prof:
+    if prof_on:
         for cls, name in ((0, "gemm_fused"), (1, "gemm_wgrad")):
-            n, ms, fl = kfp16.prof_collect(cls)
-            prof[name] = (n, ms, fl)
+            prof[name] = kfp16.prof_collect2(cls)
         for cls, name in ((2, "chain_num"), (3, "chain_den")):
             chain_prof[name] = kfp16.prof_collect(cls)
         kfp16.core.kf_prof_reset()
     stats = [0.0] * 5
-    if a.mode == "train":
+    if mode == "train":
+        # fails if a den exchange timed out in ANY step since the previous result
+        # (warm-up and timed steps): a silently wrong gradient is never reported
         res = objective.result()
         stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
                                   "cuda")
+    out = {"T": T, "elapsed": elapsed, "steps": steps, "prof": prof, "chain_prof": chain_prof,
+           "stats": stats, "ivd": ivd, "dp": (dp1[0] - dp0[0], dp1[1] - dp0[1]),
+           "buckets": len(net.dp_plan(bucket_bytes)) if comm is not None else 0}
+    ctx = (xcfg, params, bns, den_g, P) if keep else None
+    objective.close()
+    net.close()
+    return out, ctx
+
+
+def describe(r, a, world, mode, fp8, xconfig, peak):
+    ms_step = r["elapsed"] / r["steps"] * 1e3
+    value = r["T"] * world * r["steps"] / r["elapsed"]
+    d = {"value": round(value, 1), "ms_per_step": round(ms_step, 3)}
+    if r["prof"]:
+        d["roofline"] = roofline(r["prof"], r["steps"], peak)
+    if mode == "train":
+        st = r["stats"]
+        d["objf_per_frame"] = round(float(st[0]) / max(float(st[3]), 1.0), 5)
+        d["objective_finite_seqs"] = f"{int(st[4])}/{a.egs * world}"
+    return d
+
+
+def main():
+    a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return spawn_ranks(a.gpus, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if a.selftest:
+        return selftest(a, rank, world)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == a.gpus
+    torch.cuda.set_device(local)
+
+    import kfp16
+    from kfp16 import dp
+    kfp16.check(kfp16.core.bridge_gpu_init(local), "bridge_gpu_init")
+    stream = torch.cuda.current_stream()
+    kfp16.set_stream(stream.cuda_stream)
+    kfp16.assert_single_hip_runtime()
+    comm = dp.Communicator.from_process_group(local) if world > 1 else None
+    rccl_ranks = kfp16.core.kf_dp_world(comm.h) if comm is not None else 1
+
+    prof_on = not a.no_prof
+    peak = PEAK_FP8_TFLOPS if a.fp8 else PEAK_FP16_TFLOPS
+    head, ctx = run_workload(a, a.xconfig, a.mode, a.fp8, rank, world, comm, a.steps, a.warmup, prof_on,
+                             keep=True)
+    extra = {}
+    if world == 1 and not a.no_extra and a.xconfig == "cnn_tdnn_17f.xconfig" and a.mode == "train" and not a.fp8:
+        ks, kw = a.extra_steps, 2
+        r, _ = run_workload(a, "cnn_tdnn_17f.xconfig", "forward", False, rank, world, None, ks, kw, prof_on)
+        extra["configs[1]_forward_1536"] = dict(
+            workload="cnn_tdnn_17f forward only, fp16", **describe(r, a, world, "forward", False, "", PEAK_FP16_TFLOPS))
+        r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "train", True, rank, world, None, ks, kw, prof_on)
+        extra["configs[4]_train_3072_mxfp8"] = dict(
+            workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), MXFP8 forward GEMMs, fp16 backward",
+            **describe(r, a, world, "train", True, "", PEAK_FP8_TFLOPS))
+        r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "forward", True, rank, world, None, ks, kw, prof_on)
+        extra["configs[4]_forward_3072_mxfp8"] = dict(
+            workload="cnn_tdnn_17f_3072 forward only, MXFP8 GEMMs",
+            **describe(r, a, world, "forward", True, "", PEAK_FP8_TFLOPS))
 
     if rank == 0:
-        ms_step = elapsed / a.steps * 1e3
-        frames = T * world * a.steps
-        value = frames / elapsed
+        # the box's CPU share (OMP_NUM_THREADS is set to it there; nproc shows the whole host)
+        threads = a.cpu_threads or min(host_cores(), int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or
+                                       host_cores())
+        if world == 1 and not a.no_extra and not a.no_cpu_baseline:
+            extra["configs[0]_affine_40x512"] = config1_affine(threads)
         fwd_only = a.mode == "forward"
         workload = ("cnn_tdnn_17f forward only (configs[1])" if fwd_only else
                     "cnn_tdnn_17f train step (fwd+bwd+SGD)") + f", {a.egs} egs x 1500 frames per GPU"
-        if ivd:
-            workload += f", Kaldi ivector front end ({ivd}-dim ivector per eg)"
+        if head["ivd"]:
+            workload += f", Kaldi ivector front end ({head['ivd']}-dim ivector per eg)"
+        d = describe(head, a, world, a.mode, a.fp8, a.xconfig, peak)
         out = {
-            "metric": METRIC_FWD if fwd_only else METRIC, "value": round(value, 1), "unit": "frames/sec", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3),
+            "metric": METRIC_FWD if fwd_only else METRIC, "value": d["value"], "unit": "frames/sec",
+            "n_gpus": world, "rccl_ranks": rccl_ranks,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": d["ms_per_step"],
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "mxfp8 GEMMs (e4m3 + E8M0), fp16 storage" if a.fp8 else "fp16",
             "data": "synthetic",
@@ -234,40 +465,50 @@ def main():
                        "global_batch_egs": a.egs * world, "parallelism": f"dp{world}",
                        "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)"},
         }
+        for k in ("objf_per_frame", "objective_finite_seqs"):
+            if k in d:
+                out[k] = d[k]
         if not fwd_only:
-            out["objf_per_frame"] = round(float(stats[0]) / max(float(stats[3]), 1.0), 5)
-            out["objective_finite_seqs"] = f"{int(stats[4])}/{a.egs * world}"
-        if chain_prof and not fwd_only:
-            (nn, nms, _), (dn, dms, dbytes) = chain_prof["chain_num"], chain_prof["chain_den"]
+            out["den_exchange_timeouts"] = 0   # kf_chain_result raised otherwise
+        if world > 1:
+            n, v = head["dp"]
+            out["dp"] = {"collective": "kf_dp ncclAllReduce(avg) over RCCL, bucketed, overlapped with backward",
+                         "bucket_mb": a.bucket_mb, "buckets_per_step": head["buckets"],
+                         "allreduce_launches_per_step": round(n / a.steps, 2),
+                         "values_per_step": int(v / a.steps)}
+        cp = head["chain_prof"]
+        if cp and not fwd_only:
+            (nn, nms, _), (dn, dms, dbytes) = cp["chain_num"], cp["chain_den"]
             out["chain"] = {"num_ms_per_step": round(nms / a.steps, 3),
                             "den_ms_per_step": round(dms / a.steps, 3),
-                            "den_algorithmic_GBps": round(dbytes / (dms * 1e-3) / 1e9, 1) if dms else None,
-                            "ok_seqs": int(stats[4])}
-        if prof:
-            dom = max(prof, key=lambda k: prof[k][1])
-            n, ms, fl = prof[dom]
-            ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-            peak = PEAK_FP8_TFLOPS if a.fp8 else PEAK_FP16_TFLOPS
-            out["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                               "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                               # the committed PMC summary is of the default configuration
-                               "traffic": pmc_traffic(dom) if (a.xconfig == "cnn_tdnn_17f.xconfig" and
-                                                              not a.fp8 and a.mode == "train") else None,
-                               "kernel": dom, "launches": n, "kernel_ms_per_step": round(ms / a.steps, 3),
-                               "all_gemm_tflops": round(sum(v[2] for v in prof.values()) /
-                                                        (sum(v[1] for v in prof.values()) * 1e-3) / 1e12, 2)}
+                            # the den streams its arc tables from L2 (~1 MB, resident): L2 bytes
+                            "den_L2_GBps": round(dbytes / (dms * 1e-3) / 1e9, 1) if dms else None,
+                            "den_L2_frac": round(dbytes / (dms * 1e-3) / 34.5e12, 4) if dms else None,
+                            "ok_seqs": int(head["stats"][4])}
+        if "roofline" in d:
+            rl = d["roofline"]
+            # the committed PMC summary is of the default configuration
+            rl["traffic"] = (pmc_traffic(rl["kernel"]) if (a.xconfig == "cnn_tdnn_17f.xconfig" and not a.fp8
+                                                           and a.mode == "train") else None)
+            out["roofline"] = rl
         if world == 1 and not a.no_cpu_baseline and not fwd_only:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
+            from kfp16 import synth
+            xcfg, params, bns, den_g, P = ctx
             den = (den_g, oracle.den_initial_probs(den_g))
-            out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, a.cpu_threads,
+            out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, threads,
                                                den, synth.make_num_fst(0, num_pdfs=P))
+        if extra:
+            out["sub_results"] = extra
         print(json.dumps(out), flush=True)
-    objective.close()
-    net.close()
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

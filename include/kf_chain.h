@@ -97,12 +97,18 @@ int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChainOpts *opts,
 /* Device array of per-sequence statistics of the last compute:
  * float[8] per sequence {num_lp, den_lp, objf, l2_term, weight*frames, frames, oor, ok}. */
 const float *kf_chain_seq_stats(const KfChain *c);
-/* Synchronises the stream and sums the per-sequence statistics. */
+/* Synchronises the stream and sums the per-sequence statistics of the last compute.
+ * Fails (-1) when a den exchange timed out in any compute since the previous call. */
 int kf_chain_result(KfChain *c, KfChainResult *out);
 
 /* diagnostics: phase timestamps of the den forward kernel (sequence 0, block 0,
  * frames 16..47, 8 u64 each, 100 MHz wall clock) into a device buffer; NULL = off */
 void kf_chain_trace(KfChain *c, unsigned long long *dev_buf);
+/* diagnostics (tests): polls a den exchange wait makes before it declares the
+ * partner blocks non-resident (default 2^21; 0 forces the timeout path;
+ * 0xFFFFFFFF restores the default). A timeout in ANY compute since the last
+ * kf_chain_result makes that call fail (the count is sticky across launches). */
+void kf_chain_debug_spin_limit(KfChain *c, unsigned polls);
 
 const char *kf_chain_last_error(void);
 void kf_chain_clear_error(void);

@@ -36,6 +36,11 @@ const char *nnet_last_error(void);
 
 /* parse + resolve an xconfig and allocate weights/activations for max_frames */
 KfNet *nnet_create(const char *xconfig_text, int max_frames);
+/* the same network without device storage (no GPU needed): layers, the flat
+ * parameter layout and the data-parallel bucket plan can be queried; forward,
+ * backward, sgd and the parameter setters fail on it. The MI355X kernels' shape
+ * constraints (dims multiples of 8 / 32) are not enforced here. */
+KfNet *nnet_create_layout(const char *xconfig_text, int max_frames);
 /* parse + resolve only, no device work: "name type in out" per layer, then
  * "params N"; returns the bytes needed (incl. NUL) or -1 */
 int nnet_parse_summary(const char *xconfig_text, char *out, int outlen);
@@ -86,6 +91,17 @@ int nnet_sgd(KfNet *net, float lr, float momentum);
  * the producing epilogues write those copies, weights are re-quantised on every
  * parameter change. Backward stays fp16 (it reads the fp16 activations). 0 = off. */
 int nnet_set_fp8(KfNet *net, int on);
+
+/* Data parallel (kf_dp.h). nnet_bind_dp: nnet_backward exchanges the
+ * gradient in buckets of >= bucket_bytes, each all-reduced (average over ranks) on
+ * the communicator's stream as soon as the backward has enqueued the weight-gradient
+ * kernels of every parameter in it, in reverse layer order; it returns with the
+ * compute stream waiting for the last bucket. dp = NULL unbinds.
+ * nnet_dp_plan: that bucket plan (kf_dp_plan's outputs; works on a layout-only net). */
+typedef struct KfDp KfDp;
+int nnet_bind_dp(KfNet *net, KfDp *dp, long long bucket_bytes);
+int nnet_dp_plan(const KfNet *net, long long bucket_bytes, int max_buckets, int *after_step,
+                 long long *begin, long long *end);
 
 /* diagnostics (tests): back-propagate through the top n layers only; device
  * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott", "aux", "mask",

@@ -219,6 +219,9 @@ int kf_scale_cols(const void *x, long long ldx, const float *scale, void *y, lon
  * (class 0 = kf_gemm_fused, 1 = kf_gemm_wgrad); collect sums since reset */
 void kf_prof_enable(int on);
 int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
+/* the same plus the algorithmic HBM bytes of those launches (GEMM classes: each
+ * operand's source tensor read once, epilogue tensors read / written once) */
+int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes);
 void kf_prof_reset(void);
 
 const char *kf_last_error(void);

@@ -537,8 +537,10 @@ static size_t den_post_lds_bytes(int S, int P, int nslq, int pair = 1) {
 // payload word is stored write-through (sc1) by its wave, every storing wave
 // drains vmcnt, the workgroup barriers, one lane adds to the sequence's counter
 // (agent scope); consumers poll that counter relaxed (bounded, s_sleep), barrier,
-// and read every payload word with sc1 loads. Counters and the timeout word are
-// zeroed by hipMemsetAsync before every launch.
+// and read every payload word with sc1 loads. Counters and the per-launch timeout
+// word are zeroed by hipMemsetAsync before every launch; a block that gives up also
+// adds to a sticky word that only kf_chain_result / the den ABI read and clear, so a
+// timed-out launch is reported even when later launches succeed.
 // ---------------------------------------------------------------------------
 typedef __attribute__((address_space(1))) unsigned int gu32_t;
 #define RLX_AGENT __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT
@@ -552,7 +554,10 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 
 struct DenX {
     float *buf;     // [nseq][2][G][blk]; blk = ns*spg*64 + 64 (tail: lane s = partial sum of s)
-    unsigned *cnt;  // [nseq] arrivals, then [1] timeout word (zeroed before each launch)
+    unsigned *cnt;  // [nseq] arrivals (zeroed before each launch)
+    unsigned *tmo;  // per-launch timeout word (zeroed before each launch)
+    unsigned *sticky;  // timed-out blocks since the last read (never zeroed by a launch)
+    unsigned spin_limit;  // polls before a wait gives up (kf_chain_debug_spin_limit)
     int G, lgG, spg, blk, nseq;  // nseq: exchange units (groups of ns sequences)
     int ns, nseqs;               // sequences per unit, sequences in all
     unsigned cache_f, cache_b;  // LDS bytes for resident arc records (fwd / bwd kernels)
@@ -589,16 +594,16 @@ __device__ __forceinline__ void den_publish(const DenX &X, float *tail, const fl
 // wait for `target` arrivals (one lane polls); false on timeout, uniform
 __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target, int *lds_flag) {
     if (threadIdx.x == 0) {
-        unsigned *tmo = X.cnt + X.nseq;
         int ok = 1;
         for (unsigned it = 0;; ++it) {
             if (__hip_atomic_load((gu32_t *)&X.cnt[seq], RLX_AGENT) >= target) break;
-            if ((it & 255) == 255 && __hip_atomic_load((gu32_t *)tmo, RLX_AGENT)) {
+            if ((it & 255) == 255 && __hip_atomic_load((gu32_t *)X.tmo, RLX_AGENT)) {
                 ok = 0;
                 break;
             }
-            if (it > (1u << 21)) {  // ~seconds: a partner block is not resident
-                __hip_atomic_store((gu32_t *)tmo, 1u, RLX_AGENT);
+            if (it >= X.spin_limit) {  // ~seconds by default: a partner block is not resident
+                __hip_atomic_store((gu32_t *)X.tmo, 1u, RLX_AGENT);
+                __hip_atomic_fetch_add((gu32_t *)X.sticky, 1u, RLX_AGENT);
                 ok = 0;
                 break;
             }
@@ -1536,7 +1541,7 @@ struct DenXBuf {
         X.lds_f = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_f + X.cache_f);
         X.lds_b = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_b + X.cache_b);
         size_t nb = (size_t)X.nseq * 2 * G * X.blk * 4;
-        size_t nc = (((size_t)X.nseq + 1) * 4 + 15) / 16 * 16;
+        size_t nc = (((size_t)X.nseq + 2) * 4 + 15) / 16 * 16;  // sticky, timeout, counters
         if (nb > buf_cap) {
             if (buf) hipFree(buf);
             buf = nullptr;
@@ -1545,24 +1550,38 @@ struct DenXBuf {
             buf_cap = nb;
         }
         if (nc > cnt_cap) {
-            if (cnt) hipFree(cnt);
-            cnt = nullptr;
-            cnt_cap = 0;
-            if (hipMalloc(&cnt, nc) != hipSuccess) return false;
+            unsigned *grown = nullptr;
+            if (hipMalloc(&grown, nc) != hipSuccess) return false;
+            hipMemsetAsync(grown, 0, nc, kf_stream());
+            if (cnt) {  // the sticky count survives the reallocation
+                hipMemcpyAsync(grown, cnt, 4, hipMemcpyDeviceToDevice, kf_stream());
+                hipStreamSynchronize(kf_stream());
+                hipFree(cnt);
+            }
+            cnt = grown;
             cnt_cap = nc;
         }
         X.buf = buf;
-        X.cnt = cnt;
-        units = X.nseq;
+        X.sticky = cnt;
+        X.tmo = cnt + 1;
+        X.cnt = cnt + 2;
+        X.spin_limit = spin_limit;
         return true;
     }
-    void zero(hipStream_t st) { hipMemsetAsync(cnt, 0, cnt_cap, st); }
-    int units = 0;  // of the last make(): the timeout word follows the unit counters
-    bool timed_out(hipStream_t st, int /*nseq*/) {
+    // counters and the per-launch timeout word; never the sticky word
+    void zero(hipStream_t st) { hipMemsetAsync(cnt + 1, 0, cnt_cap - 4, st); }
+    unsigned spin_limit = 1u << 21;
+    // blocks that timed out since the last call (stream-ordered read, then cleared)
+    unsigned take_timeouts(hipStream_t st) {
+        if (!cnt) return 0;
         unsigned v = 0;
-        hipMemcpyAsync(&v, cnt + units, 4, hipMemcpyDeviceToHost, st);
+        hipMemcpyAsync(&v, cnt, 4, hipMemcpyDeviceToHost, st);
         hipStreamSynchronize(st);
-        return v != 0;
+        if (v) {
+            hipMemsetAsync(cnt, 0, 4, st);
+            hipStreamSynchronize(st);
+        }
+        return v;
     }
 };
 
@@ -2296,7 +2315,7 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
         den_set_error("den_forward_backward: %s", hipGetErrorString(e));
         return -1e30f;
     }
-    if (xbuf.timed_out(st, 1) || (h_post && xbuf2.timed_out(st, 1))) {
+    if (xbuf.take_timeouts(st) + (h_post ? xbuf2.take_timeouts(st) : 0u)) {
         den_set_error("den_forward_backward: cross-workgroup exchange timed out");
         return -1e30f;
     }
@@ -2678,6 +2697,14 @@ extern "C" void kf_chain_trace(KfChain *c, unsigned long long *buf) {
     if (c) c->trace = buf;
 }
 
+// diagnostics (tests): polls an exchange wait makes before it gives up; 0 forces the
+// timeout path on the first wait that is not already satisfied. 0xFFFFFFFF = default.
+extern "C" void kf_chain_debug_spin_limit(KfChain *c, unsigned polls) {
+    if (!c) return;
+    const unsigned v = polls == 0xFFFFFFFFu ? (1u << 21) : polls;
+    c->xbuf.spin_limit = c->xbuf2.spin_limit = v;
+}
+
 extern "C" const float *kf_chain_seq_stats(const KfChain *c) { return c ? c->stats : nullptr; }
 
 extern "C" int kf_chain_result(KfChain *c, KfChainResult *out) {
@@ -2690,8 +2717,11 @@ extern "C" int kf_chain_result(KfChain *c, KfChainResult *out) {
         kfc_set_error("kf_chain_result: stream error");
         return -1;
     }
-    if (n && c->xbuf.cnt && (c->xbuf.timed_out(st, n) || c->xbuf2.timed_out(st, n))) {
-        kfc_set_error("kf_chain_result: den cross-workgroup exchange timed out (blocks not resident)");
+    // every compute since the last result: the sticky count is never reset by a launch
+    if (const unsigned nt = c->xbuf.take_timeouts(st) + c->xbuf2.take_timeouts(st)) {
+        kfc_set_error("kf_chain_result: den cross-workgroup exchange timed out in %u block(s) since the last "
+                      "result (blocks not resident); the objective and gradients of those computes are invalid",
+                      nt);
         return -1;
     }
     memset(out, 0, sizeof(*out));

@@ -990,6 +990,7 @@ struct ProfRec {
     hipEvent_t a, b;
     int cls;
     double flops;
+    double bytes;  // algorithmic HBM bytes: unique operand sources + epilogue reads / writes
 };
 bool g_prof = false;
 std::vector<ProfRec> g_prof_recs;
@@ -1026,10 +1027,10 @@ void kf_prof_stop(int idx) {
 }
 
 extern "C" void kf_prof_enable(int on) { g_prof = on != 0; }
-// sums per class since the last collect: count, milliseconds, flops
-extern "C" int kf_prof_collect(int cls, long long *count, double *ms, double *flops) {
+// sums per class since the last collect: count, milliseconds, flops, algorithmic bytes
+extern "C" int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes) {
     long long c = 0;
-    double t = 0, f = 0;
+    double t = 0, f = 0, by = 0;
     for (auto &r : g_prof_recs) {
         if (r.cls != cls) continue;
         hipEventSynchronize(r.b);
@@ -1038,11 +1039,38 @@ extern "C" int kf_prof_collect(int cls, long long *count, double *ms, double *fl
         c++;
         t += e;
         f += r.flops;
+        by += r.bytes;
     }
     if (count) *count = c;
     if (ms) *ms = t;
     if (flops) *flops = f;
+    if (bytes) *bytes = by;
     return 0;
+}
+extern "C" int kf_prof_collect(int cls, long long *count, double *ms, double *flops) {
+    return kf_prof_collect2(cls, count, ms, flops, nullptr);
+}
+
+// Algorithmic HBM bytes of one GEMM launch: each operand's SOURCE tensor read once
+// (an implicit splice / im2col operand reads its [T x hsrc x part] source, not the
+// K-expanded view), the epilogue's tensors read / written once, the fp32 weight
+// gradient written once. The floor a perfect-reuse kernel would move.
+static double op_src_bytes(const OpD &o, int f8) {
+    // geometry is in 2-byte units, also for MXFP8 (there: payload bytes)
+    double b = o.simple ? (double)o.nrows * o.ncols * 2.0 : (double)o.T * (o.hsrc > 0 ? o.hsrc : 1) * o.pw * 2.0;
+    if (f8) b += b / 32.0;  // one E8M0 scale per 32 e4m3 values
+    return b;
+}
+static double epi_bytes(const KfEpilogue &E, long long M, long long N) {
+    const double mn = (double)M * N;
+    double b = 0;
+    if (E.out) b += mn * 2 * (E.beta != 0.f ? 2 : 1);
+    if (E.out2) b += mn * 2;
+    if (E.resid) b += mn * 2;
+    if (E.mask_out) b += mn / 8;
+    if (E.mask_in) b += mn / 8;
+    if (E.out8) b += mn + mn / 32;
+    return b;
 }
 extern "C" void kf_prof_reset(void) {
     for (auto &r : g_prof_recs) {
@@ -1159,6 +1187,8 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
         rec.b = prof_event();
         rec.cls = WGRAD ? KF_PROF_WGRAD : KF_PROF_FUSED;
         rec.flops = 2.0 * M * N * (double)K * (F8 ? 2 : 1);  // K counts 2-byte units
+        // A is [M x K] (or its K-major view), B is [K x N]; wgrad writes fp32 dW [M x N]
+        rec.bytes = op_src_bytes(A, F8) + op_src_bytes(B, F8) + (WGRAD ? (double)M * N * 4 : epi_bytes(E, M, N));
         hipEventRecord(rec.a, kf_stream());
     }
     gemm_kernel<BM, BN, WM, WN, AKC, BKC, WGRAD, ST, AM, BMODE, F8>
@@ -1191,6 +1221,7 @@ static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const Ha
         rec.b = prof_event();
         rec.cls = KF_PROF_FUSED;
         rec.flops = 2.0 * M * N * (double)H.ntaps * H.pw;
+        rec.bytes = (double)H.T * H.hsrc * H.pw * 2.0 + (double)H.ntaps * H.pw * N * 2.0 + epi_bytes(E, M, N);
         hipEventRecord(rec.a, kf_stream());
     }
     conv_halo_kernel<BM, BN, WM, WN, BKC, BMODE, BROW>

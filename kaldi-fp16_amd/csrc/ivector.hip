@@ -220,7 +220,8 @@ extern "C" int kf_combine_feature_maps(const void *a, long long lda, const void 
 extern "C" int kf_combine_feature_maps_backward(const void *dy, long long ldy, const int *dev_seq_off, int B,
                                                 void *db, long long ldb, int height, int nf1, int nf2) {
     if (B <= 0) return 0;
-    if (!dy || !dev_seq_off || !db || height <= 0 || nf1 < 0 || nf2 <= 0) {
+    if (!dy || !dev_seq_off || !db || height <= 0 || nf1 < 0 || nf2 <= 0 ||
+        ldy < (long long)height * (nf1 + nf2) || ldb < (long long)height * nf2) {
         kf_report_error("kf_combine_feature_maps_backward: bad arguments");
         return -1;
     }

@@ -13,6 +13,7 @@
 //     fp32 gradient / fp32 velocity allocation, so the optimiser is one launch
 //     and the data-parallel gradient exchange is one contiguous buffer.
 // Memory comes from the bridge_* ABI, as the Go layer does (internal/gpu/tensor.go).
+#include <climits>
 #include <cmath>
 #include <functional>
 #include <cstdio>
@@ -201,6 +202,10 @@ struct KfNet {
     void *dbott = nullptr, *edge = nullptr;
     size_t edge_half = 0;
     int fp8 = 0;
+    // data parallel (kf_dp.h): gradient buckets exchanged during the backward
+    KfDp *dp = nullptr;
+    std::vector<int> dp_after;  // bucket j is issued after backward step dp_after[j]
+    std::vector<long long> dp_begin, dp_end;
     std::vector<void *> allocs;
 
     void *dalloc(size_t bytes) {
@@ -229,6 +234,13 @@ bool ck(int rc, const char *what) {
         return false;
     }
     return true;
+}
+
+// a network from nnet_create_layout has no device storage
+bool on_device(const KfNet *net, const char *what) {
+    if (net && net->master) return true;
+    set_err(std::string(what) + ": " + (net ? "layout-only network (nnet_create_layout)" : "null network"));
+    return false;
 }
 
 // makeIDCTMatrix, forward.go:1190-1210
@@ -328,19 +340,21 @@ int att_affine(const Layer &L) {
 
 }  // namespace
 
-extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
-    g_nnet_err[0] = 0;
-    std::unique_ptr<KfNet> net(new KfNet);
+// Parse, resolve and lay out the network on the host: layers, inputs, the flat
+// parameter layout, the backward path. No device work (nnet_create_layout).
+// device = false (nnet_create_layout): the MI355X kernels' shape constraints (dims that
+// are multiples of 8 / 32, IDCT <= 64) are not enforced; the layout does not depend on them.
+static bool build_topology(KfNet *net, const char *xconfig_text, int max_frames, bool device) {
     std::vector<kf::LayerConfig> cfgs;
     std::string err;
     if (!kf::ParseXConfig(xconfig_text ? xconfig_text : "", cfgs, err) ||
         !kf::ResolveLayers(cfgs, net->all, err)) {
         set_err("parse xconfig: " + err);
-        return nullptr;
+        return false;
     }
     if (max_frames <= 0) {
         set_err("max_frames must be positive");
-        return nullptr;
+        return false;
     }
     net->max_T = max_frames;
     std::map<std::string, int> index;  // layer name -> index in net->layers (-1 = input)
@@ -349,7 +363,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             if (L.name == "ivector") {  // per-sequence input (Kaldi's ivector-dim input)
                 if (net->ivec_dim) {
                     set_err("more than one ivector input");
-                    return nullptr;
+                    return false;
                 }
                 net->ivec_dim = L.out_dim;
                 index[L.name] = -2;
@@ -357,7 +371,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             }
             if (net->feat_dim) {
                 set_err("more than one frame-level input layer (only 'input' and 'ivector' are supported)");
-                return nullptr;
+                return false;
             }
             net->feat_dim = L.out_dim;
             index[L.name] = -1;
@@ -371,24 +385,24 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             // (or frame-level) input (Kaldi's Append(idct-batchnorm, ivector-batchnorm))
             if (L.type != LayerType::CombineFeatureMaps || L.input_names.size() != 2) {
                 set_err("layer " + L.name + ": Append is supported as the input of combine-feature-maps, of two layers");
-                return nullptr;
+                return false;
             }
             auto a = index.find(L.input_names[0]), b = index.find(L.input_names[1]);
             if (a == index.end() || b == index.end() || is_seq(a->second)) {
                 set_err("layer " + L.name + ": Append inputs not found, or the first one is per-sequence");
-                return nullptr;
+                return false;
             }
             nl.input = a->second;
             nl.input2 = b->second;
         } else {
             if (L.input_names.size() != 1) {
                 set_err("layer " + L.name + ": one input expected");
-                return nullptr;
+                return false;
             }
             auto it = index.find(L.input_names[0]);
             if (it == index.end()) {
                 set_err("layer " + L.name + ": input not found");
-                return nullptr;
+                return false;
             }
             nl.input = it->second;
             // ReplaceIndex(x, t, 0) of a per-sequence source, or anything fed by one
@@ -396,7 +410,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             if (nl.per_seq && L.type != LayerType::Linear && L.type != LayerType::Batchnorm) {
                 set_err("layer " + L.name + ": only linear-component and batchnorm-component run on the "
                         "per-sequence (ivector) branch");
-                return nullptr;
+                return false;
             }
         }
         if (L.type == LayerType::CombineFeatureMaps) {
@@ -406,16 +420,16 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             if (nl.input2 == -100 || L.height <= 0 || da != L.height * L.nf1 || db != L.height * L.nf2) {
                 set_err("combine-feature-maps " + L.name + ": needs Append(a, b) with dims height*num-filters1 "
                         "and height*num-filters2");
-                return nullptr;
+                return false;
             }
         }
         const int din = L.in_dim, dout = L.out_dim;
         const std::string &n = L.name;
         switch (L.type) {
             case LayerType::IDCT:
-                if (din != dout || din > 64 || din % 8) {
+                if (din != dout || (device && (din > 64 || din % 8))) {
                     set_err("idct-layer " + n + ": dim must equal input dim, <= 64, multiple of 8");
-                    return nullptr;
+                    return false;
                 }
                 break;
             case LayerType::Batchnorm:
@@ -423,9 +437,9 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
                 nl.bn_rms = (float)L.target_rms;
                 break;
             case LayerType::ConvReluBN: {
-                if (L.hin <= 0 || L.fin <= 0 || L.fin * L.hin != din || L.fout % 8) {
+                if (L.hin <= 0 || L.fin <= 0 || L.fin * L.hin != din || (device && L.fout % 8)) {
                     set_err("conv layer " + n + ": inconsistent height-in / filters");
-                    return nullptr;
+                    return false;
                 }
                 for (int a : L.time_offsets)
                     for (int b : L.height_offsets) {
@@ -434,37 +448,37 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
                     }
                 if (nl.dt.empty() || nl.dt.size() > KF_MAX_PARTS) {
                     set_err("conv layer " + n + ": need 1..9 (time x height) offsets");
-                    return nullptr;
+                    return false;
                 }
                 if (L.fin != 1 && L.fin % 32) {  // small fin: im2col + GEMM (csrc/ivector.hip)
                     nl.kp = (int)((nl.dt.size() * L.fin + 63) / 64 * 64);
                 }
                 const int K = (int)nl.dt.size() * L.fin;
-                nl.pW = add_param(net.get(), n + ".W", K, L.fout);
-                nl.pb = add_param(net.get(), n + ".Bias", 1, L.fout);
+                nl.pW = add_param(net, n + ".W", K, L.fout);
+                nl.pb = add_param(net, n + ".Bias", 1, L.fout);
                 identity_bn(nl.hbn, L.fout);
                 break;
             }
             case LayerType::TDNNF: {
                 const int s = L.time_stride, bn = L.bottleneck;
-                if (bn % 32 || din % 32 || dout % 8) {
+                if (device && (bn % 32 || din % 32 || dout % 8)) {
                     set_err("tdnnf layer " + n + ": dims must be multiples of 32");
-                    return nullptr;
+                    return false;
                 }
-                nl.pW = add_param(net.get(), n + ".LinearW", s > 0 ? 2 * din : din, bn);
-                nl.pW2 = add_param(net.get(), n + ".AffineW", s > 0 ? 2 * bn : bn, dout);
-                nl.pb2 = add_param(net.get(), n + ".AffineBias", 1, dout);
+                nl.pW = add_param(net, n + ".LinearW", s > 0 ? 2 * din : din, bn);
+                nl.pW2 = add_param(net, n + ".AffineW", s > 0 ? 2 * bn : bn, dout);
+                nl.pb2 = add_param(net, n + ".AffineBias", 1, dout);
                 nl.bypass = L.bypass_scale > 0 && din == dout;
                 identity_bn(nl.hbn, dout);
                 break;
             }
             case LayerType::Linear:
-                nl.pW = add_param(net.get(), n + ".W", din, dout);
+                nl.pW = add_param(net, n + ".W", din, dout);
                 break;
             case LayerType::Prefinal:
-                nl.pW = add_param(net.get(), n + ".BigW", din, L.big_dim);
-                nl.pb = add_param(net.get(), n + ".BigBias", 1, L.big_dim);
-                nl.pW2 = add_param(net.get(), n + ".SmallW", L.big_dim, L.small_dim);
+                nl.pW = add_param(net, n + ".BigW", din, L.big_dim);
+                nl.pb = add_param(net, n + ".BigBias", 1, L.big_dim);
+                nl.pW2 = add_param(net, n + ".SmallW", L.big_dim, L.small_dim);
                 identity_bn(nl.hbn, L.big_dim);
                 identity_bn(nl.hbn2, L.small_dim);
                 nl.has_bn2 = true;
@@ -473,19 +487,19 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
                 if (L.include_log_softmax) {
                     // the xent branch (log-softmax output) is a "next" row
                 }
-                nl.pW = add_param(net.get(), n + ".W", din, dout);
-                nl.pb = add_param(net.get(), n + ".Bias", 1, dout);
+                nl.pW = add_param(net, n + ".W", din, dout);
+                nl.pb = add_param(net, n + ".Bias", 1, dout);
                 break;
             case LayerType::Attention: {
                 const int ctx = 1 + L.num_left + L.num_right, A = att_affine(L);
-                if (L.num_heads <= 0 || L.key_dim <= 0 || L.value_dim < 0 || L.att_stride <= 0 || ctx > 64 ||
-                    L.num_heads * ctx > 1024 || A % 8 || dout % 8 || din % 8) {
+                if (L.num_heads <= 0 || L.key_dim <= 0 || L.value_dim < 0 || L.att_stride <= 0 ||
+                    (device && (ctx > 64 || L.num_heads * ctx > 1024 || A % 8 || dout % 8 || din % 8))) {
                     set_err("attention layer " + n + ": needs heads > 0, key-dim > 0, context <= 64, "
                             "heads*context <= 1024 and affine / output / input dims multiples of 8");
-                    return nullptr;
+                    return false;
                 }
-                nl.pW = add_param(net.get(), n + ".W", din, A);
-                nl.pb = add_param(net.get(), n + ".Bias", 1, A);
+                nl.pW = add_param(net, n + ".W", din, A);
+                nl.pb = add_param(net, n + ".Bias", 1, A);
                 nl.key_scale = L.key_scale > 0 ? (float)L.key_scale : (float)(1.0 / sqrt((double)L.key_dim));
                 identity_bn(nl.hbn, dout);
                 break;
@@ -495,14 +509,14 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
                 break;
             default:
                 set_err("layer " + n + ": type not supported on the MI355X path");
-                return nullptr;
+                return false;
         }
         index[L.name] = (int)net->layers.size();
         net->layers.push_back(nl);
     }
     if (net->layers.empty()) {
         set_err("no layers");
-        return nullptr;
+        return false;
     }
     for (size_t i = 0; i < net->layers.size() && net->chain_out < 0; ++i)
         if (net->layers[i].L.type == LayerType::Output && net->layers[i].L.name == "output") net->chain_out = (int)i;
@@ -529,6 +543,11 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
         };
         for (size_t i = 0; i < net->layers.size(); ++i) net->layers[i].needs_dx = below(net->layers[i].input);
     }
+    return true;
+}
+
+// Device storage of a laid-out network: parameters, activations, masks, BN, scratch.
+static bool alloc_device(KfNet *net, int max_frames) {
     // flat parameter storage
     const long long P = net->nparams > 0 ? net->nparams : 64;
     net->master = (float *)net->dalloc(P * 4);
@@ -537,7 +556,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
     net->w16 = net->dalloc(P * 2);
     if (!net->master || !net->grad || !net->vel || !net->w16) {
         set_err("alloc params: " + std::string(bridge_last_error() ? bridge_last_error() : ""));
-        return nullptr;
+        return false;
     }
     bridge_gpu_memset(net->master, 0, P * 4);
     bridge_gpu_memset(net->grad, 0, P * 4);
@@ -556,7 +575,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             nl.act = net->dalloc(T * dout * 2);
             if (!nl.act) {
                 set_err("alloc activation " + L.name);
-                return nullptr;
+                return false;
             }
         }
         int mwidth = 0;
@@ -569,7 +588,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             nl.att_scratch = (float *)net->dalloc((size_t)2 * T * L.num_heads * ctx * 4);
             if (!nl.aux || !nl.dproj || !nl.att_scratch) {
                 set_err("alloc attention buffers");
-                return nullptr;
+                return false;
             }
         }
         if (L.type == LayerType::ConvReluBN && nl.kp) {
@@ -578,7 +597,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             nl.gwpad = (float *)net->dalloc((size_t)nl.kp * L.fout * 4);
             if (!nl.im2col || !nl.wpad || !nl.gwpad) {
                 set_err("alloc small-fin conv buffers");
-                return nullptr;
+                return false;
             }
             bridge_gpu_memset(nl.wpad, 0, (size_t)nl.kp * L.fout * 2);
         }
@@ -586,7 +605,7 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             nl.gdb = net->dalloc((size_t)T * L.height * L.nf2 * 2);
             if (!nl.gdb) {
                 set_err("alloc combine gradient");
-                return nullptr;
+                return false;
             }
         }
         if (L.type == LayerType::Prefinal) mwidth = L.big_dim;
@@ -603,24 +622,24 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
             nl.idct = net->dalloc(h.size() * 2);
             if (bridge_transfer_fp16(nl.idct, h.data(), h.size())) {
                 set_err("upload idct");
-                return nullptr;
+                return false;
             }
         }
         if (L.type == LayerType::Batchnorm &&
-            !upload_bn(net.get(), nl.hbn, nl.bn_eps, nl.bn_rms, dout, dout, nl.bn_scale, nl.bn_shift))
-            return nullptr;
+            !upload_bn(net, nl.hbn, nl.bn_eps, nl.bn_rms, dout, dout, nl.bn_scale, nl.bn_shift))
+            return false;
         if (L.type == LayerType::ConvReluBN &&
-            !upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, L.fout, dout, nl.bn_scale, nl.bn_shift))
-            return nullptr;
+            !upload_bn(net, nl.hbn, nl.bn_eps, 1.f, L.fout, dout, nl.bn_scale, nl.bn_shift))
+            return false;
         if ((L.type == LayerType::TDNNF || L.type == LayerType::Attention) &&
-            !upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, dout, dout, nl.bn_scale, nl.bn_shift))
-            return nullptr;
+            !upload_bn(net, nl.hbn, nl.bn_eps, 1.f, dout, dout, nl.bn_scale, nl.bn_shift))
+            return false;
         if (L.type == LayerType::Prefinal &&
-            (!upload_bn(net.get(), nl.hbn, nl.bn_eps, 1.f, L.big_dim, L.big_dim, nl.bn_scale,
+            (!upload_bn(net, nl.hbn, nl.bn_eps, 1.f, L.big_dim, L.big_dim, nl.bn_scale,
                         nl.bn_shift) ||
-             !upload_bn(net.get(), nl.hbn2, nl.bn2_eps, 1.f, L.small_dim, L.small_dim,
+             !upload_bn(net, nl.hbn2, nl.bn2_eps, 1.f, L.small_dim, L.small_dim,
                         nl.bn2_scale, nl.bn2_shift)))
-            return nullptr;
+            return false;
     }
     // gradient buffers carry two spare rows for the splice-transpose edge sums
     for (int i = 0; i < 2; ++i) {
@@ -632,8 +651,23 @@ extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
     net->edge = net->dalloc(net->edge_half * 2);
     if (!net->dz[0] || !net->dz[1] || !net->g[0] || !net->g[1] || !net->dbott || !net->edge) {
         set_err("alloc backward scratch");
-        return nullptr;
+        return false;
     }
+    return true;
+}
+
+extern "C" KfNet *nnet_create(const char *xconfig_text, int max_frames) {
+    g_nnet_err[0] = 0;
+    std::unique_ptr<KfNet> net(new KfNet);
+    if (!build_topology(net.get(), xconfig_text, max_frames, true) || !alloc_device(net.get(), max_frames))
+        return nullptr;
+    return net.release();
+}
+
+extern "C" KfNet *nnet_create_layout(const char *xconfig_text, int max_frames) {
+    g_nnet_err[0] = 0;
+    std::unique_ptr<KfNet> net(new KfNet);
+    if (!build_topology(net.get(), xconfig_text, max_frames, false)) return nullptr;
     return net.release();
 }
 
@@ -667,6 +701,7 @@ extern "C" int nnet_param_info(const KfNet *net, int idx, char *name, int namele
 
 static bool quantise_weights(KfNet *net, bool alloc);
 extern "C" int nnet_set_params(KfNet *net, const float *host) {
+    if (!on_device(net, "set_params")) return -1;
     const long long P = net->nparams;
     std::vector<uint16_t> h(P, 0);
     std::vector<float> m(P, 0.f);
@@ -685,6 +720,7 @@ extern "C" int nnet_set_params(KfNet *net, const float *host) {
 }
 
 extern "C" int nnet_get_params(const KfNet *net, float *host) {
+    if (!on_device(net, "get_params")) return -1;
     // D2H through the bridge (fp32 read = 2x fp16 count on a 4-byte aligned buffer)
     std::vector<uint16_t> tmp(net->nparams * 2);
     if (bridge_read_fp16(tmp.data(), net->master, net->nparams * 2)) {
@@ -699,6 +735,7 @@ extern "C" int nnet_get_params(const KfNet *net, float *host) {
 // weight_loader.go:88-97, :760-770): host fp32 [dim x dim] in the y = x . M orientation,
 // stored fp16 by truncation like every weight (tensor.go:158-173).
 extern "C" int nnet_set_idct(KfNet *net, const char *layer, const float *m, int rows, int cols) {
+    if (!on_device(net, "set_idct")) return -1;
     for (auto &nl : net->layers) {
         if (nl.L.name != layer) continue;
         if (nl.L.type != LayerType::IDCT || !nl.idct) break;
@@ -734,6 +771,7 @@ extern "C" int nnet_set_key_scale(KfNet *net, const char *layer, float key_scale
 extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float *mean,
                            const float *var, const float *gamma, const float *beta, float eps,
                            float target_rms) {
+    if (!on_device(net, "set_bn")) return -1;
     for (auto &nl : net->layers) {
         if (nl.L.name != layer) continue;
         const Layer &L = nl.L;
@@ -896,6 +934,7 @@ static bool quantise_weights(KfNet *net, bool alloc) {
 }
 
 extern "C" int nnet_set_fp8(KfNet *net, int on) {
+    if (!on_device(net, "set_fp8")) return -1;
     if (!on) {
         net->fp8 = 0;
         return 0;
@@ -937,6 +976,12 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
 // seq_row0 host int[B+1] frame offsets (seq_row0[0] = 0, seq_row0[B] = T)
 extern "C" int nnet_forward_ivector(KfNet *net, const void *features, int T, const void *ivectors, int B,
                                     const int *seq_row0) {
+    if (!on_device(net, "forward_ivector")) return -1;
+    // validate everything before touching the device or the network's state
+    if (T <= 0 || T > net->max_T) {
+        set_err("forward_ivector: T=" + std::to_string(T) + " outside (0, max_frames]");
+        return -1;
+    }
     if (!net->ivec_dim || !ivectors || B <= 0 || B > T || !seq_row0 || seq_row0[0] != 0 || seq_row0[B] != T) {
         set_err("forward_ivector: needs an ivector input layer, B in [1, T] and seq_row0[0] = 0, seq_row0[B] = T");
         return -1;
@@ -962,6 +1007,7 @@ extern "C" int nnet_forward_ivector(KfNet *net, const void *features, int T, con
     return forward_impl(net, features, T);
 }
 static int forward_impl(KfNet *net, const void *features, int T) {
+    if (!on_device(net, "forward")) return -1;
     if (T <= 0 || T > net->max_T) {
         set_err("forward: T=" + std::to_string(T) + " outside (0, max_frames]");
         return -1;
@@ -1222,6 +1268,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
 }  // namespace
 
 static int backward_impl(KfNet *net, const void *out_grad, int max_layers);
+static bool dp_issue(KfNet *net, size_t &next, int step);
 extern "C" int nnet_backward(KfNet *net, const void *out_grad) {
     return backward_impl(net, out_grad, 1 << 30);
 }
@@ -1245,6 +1292,7 @@ extern "C" const void *nnet_debug_tensor(KfNet *net, const char *what, int layer
     return nullptr;
 }
 static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
+    if (!on_device(net, "backward")) return -1;
     const int T = net->T;
     if (T <= 0) {
         set_err("backward before forward");
@@ -1255,6 +1303,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     const void *dz = out_grad;  // gradient w.r.t. pre-activation of the current layer
     const void *gcur = out_grad;  // stored gradient w.r.t. the current layer's output
     int flip = 0, done = 0;
+    size_t dp_next = 0;
     for (const auto &r : net->offpath) bridge_gpu_memset(net->grad + r.first, 0, (size_t)r.second * 4);
     (void)n;
     for (int li = net->chain_out; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
@@ -1541,10 +1590,19 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 set_err("backward: unsupported layer " + L.name);
                 return -1;
         }
+        // gradient buckets complete at this step go to the communication stream
+        if (net->dp && !dp_issue(net, dp_next, done)) return -1;
         if (!want_dx) break;  // nothing trainable below
         dz = dz_next;
         gcur = g_next;
         flip ^= 1;
+    }
+    if (net->dp) {  // the rest, then the compute stream waits for every bucket (SGD reads them)
+        if (!dp_issue(net, dp_next, INT_MAX)) return -1;
+        if (kf_dp_join(net->dp) != 0) {
+            set_err(std::string("dp join: ") + (kf_dp_last_error() ? kf_dp_last_error() : ""));
+            return -1;
+        }
     }
     return 0;
 }
@@ -1554,6 +1612,7 @@ extern "C" float *nnet_master_buffer(KfNet *net) { return net->master; }
 extern "C" void *nnet_weight_buffer(KfNet *net) { return net->w16; }
 
 extern "C" int nnet_sgd(KfNet *net, float lr, float momentum) {
+    if (!on_device(net, "sgd")) return -1;
     if (!ck(kf_sgd_flat(net->master, net->w16, net->grad, net->vel, lr, momentum, net->nparams), "sgd"))
         return -1;
     // the MXFP8 weight copies follow every parameter change
@@ -1601,10 +1660,90 @@ extern "C" int nnet_parse_summary(const char *xconfig_text, char *out, int outle
 // Use caller-owned device memory (>= num_params fp32) as the gradient buffer,
 // e.g. a torch tensor handed to the data-parallel all-reduce.
 extern "C" int nnet_bind_grad_buffer(KfNet *net, float *dev) {
+    if (!on_device(net, "bind_grad_buffer")) return -1;
     if (!dev) {
         set_err("bind_grad_buffer: null");
         return -1;
     }
     net->grad = dev;
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// data parallel (kf_dp.h): the backward's parameter groups in the
+// order backward_impl visits them, cut into all-reduce buckets by kf_dp_plan
+// ---------------------------------------------------------------------------
+namespace {
+// [lo, hi) of the flat buffer written by backward step i (lo = hi: none)
+void backward_groups(const KfNet *net, std::vector<long long> &lo, std::vector<long long> &hi) {
+    lo.clear();
+    hi.clear();
+    auto add = [&](const NetLayer &q, long long &a, long long &b) {
+        for (int pi : {q.pW, q.pb, q.pW2, q.pb2}) {
+            if (pi < 0) continue;
+            const ParamRef &p = net->params[pi];
+            const long long e = p.off + (long long)align_up((size_t)p.rows * p.cols, 64);
+            if (a == b) {
+                a = p.off;
+                b = e;
+            } else {
+                a = std::min(a, p.off);
+                b = std::max(b, e);
+            }
+        }
+    };
+    for (int li = net->chain_out; li >= 0; li = net->layers[li].input) {
+        const NetLayer &nl = net->layers[li];
+        long long a = 0, b = 0;
+        add(nl, a, b);
+        if (nl.L.type == LayerType::CombineFeatureMaps)  // the ivector branch is written at this step
+            for (int cur = nl.input2; cur >= 0; cur = net->layers[cur].input) add(net->layers[cur], a, b);
+        lo.push_back(a);
+        hi.push_back(b);
+    }
+}
+}  // namespace
+
+extern "C" int nnet_dp_plan(const KfNet *net, long long bucket_bytes, int max_buckets, int *after_step,
+                            long long *begin, long long *end) {
+    if (!net || bucket_bytes < 0) {
+        set_err("dp_plan: bad arguments");
+        return -1;
+    }
+    std::vector<long long> lo, hi;
+    backward_groups(net, lo, hi);
+    const int nb = kf_dp_plan((int)lo.size(), lo.data(), hi.data(), net->nparams, bucket_bytes / 4, max_buckets,
+                              after_step, begin, end);
+    if (nb < 0) set_err(std::string("dp_plan: ") + (kf_dp_last_error() ? kf_dp_last_error() : ""));
+    return nb;
+}
+
+extern "C" int nnet_bind_dp(KfNet *net, KfDp *dp, long long bucket_bytes) {
+    if (!on_device(net, "bind_dp")) return -1;
+    net->dp = nullptr;
+    net->dp_after.clear();
+    net->dp_begin.clear();
+    net->dp_end.clear();
+    if (!dp) return 0;
+    std::vector<int> after(256);
+    std::vector<long long> b(256), e(256);
+    const int nb = nnet_dp_plan(net, bucket_bytes, 256, after.data(), b.data(), e.data());
+    if (nb < 0) return -1;
+    net->dp_after.assign(after.begin(), after.begin() + nb);
+    net->dp_begin.assign(b.begin(), b.begin() + nb);
+    net->dp_end.assign(e.begin(), e.begin() + nb);
+    net->dp = dp;
+    return 0;
+}
+
+// issue every bucket planned to follow backward step `step` (INT_MAX: all left)
+static bool dp_issue(KfNet *net, size_t &next, int step) {
+    for (; next < net->dp_after.size() && net->dp_after[next] <= step; ++next)
+        if (kf_dp_allreduce_mean_async(net->dp, net->grad + net->dp_begin[next],
+                                       (size_t)(net->dp_end[next] - net->dp_begin[next])) != 0) {
+            const char *e = kf_dp_last_error();
+            set_err(std::string("dp all-reduce: ") + (e ? e : ""));
+            return false;
+        }
+    return true;
 }

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "../../include/bridge.h"
+#include "../../include/kf_dp.h"
 #include "../../include/kf_nnet.h"
 #include "../../include/kf_ops.h"
 #include "../../include/ops.h"

@@ -93,9 +93,28 @@ _sig(nnet, "nnet_set_fp8", _i, _vp, _i)
 _sig(nnet, "nnet_bind_grad_buffer", _i, _vp, _vp)
 _sig(nnet, "nnet_backward_n", _i, _vp, _vp, _i)
 _sig(nnet, "nnet_debug_tensor", _vp, _vp, C.c_char_p, _i)
+_sig(nnet, "nnet_create_layout", _vp, C.c_char_p, _i)
+_sig(nnet, "nnet_bind_dp", _i, _vp, _vp, _ll)
+_sig(nnet, "nnet_dp_plan", _i, _vp, _ll, _i, C.POINTER(_i), C.POINTER(_ll), C.POINTER(_ll))
+# kf_dp.h (RCCL data parallel)
+_sig(core, "kf_dp_last_error", C.c_char_p)
+_sig(core, "kf_dp_unique_id", _i, C.c_char_p)
+_sig(core, "kf_dp_create", _vp, _i, _i, C.c_char_p, _i)
+_sig(core, "kf_dp_free", None, _vp)
+_sig(core, "kf_dp_rank", _i, _vp)
+_sig(core, "kf_dp_world", _i, _vp)
+_sig(core, "kf_dp_allreduce_mean_async", _i, _vp, _vp, _sz)
+_sig(core, "kf_dp_join", _i, _vp)
+_sig(core, "kf_dp_allreduce_mean", _i, _vp, _vp, _sz)
+_sig(core, "kf_dp_allreduce_sum_f64", _i, _vp, _vp, _sz)
+_sig(core, "kf_dp_stats", _i, _vp, C.POINTER(_ll), C.POINTER(_ll))
+_sig(core, "kf_dp_plan", _i, _i, C.POINTER(_ll), C.POINTER(_ll), _ll, _ll, _i, C.POINTER(_i),
+     C.POINTER(_ll), C.POINTER(_ll))
 _sig(core, "kf_prof_enable", None, _i)
 _sig(core, "kf_prof_collect", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double))
 _sig(core, "kf_prof_reset", None)
+_sig(core, "kf_prof_collect2", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double),
+     C.POINTER(C.c_double))
 
 
 def _err(lib_fn):
@@ -180,6 +199,13 @@ def prof_collect(cls: int):
     return n.value, ms.value, fl.value
 
 
+def prof_collect2(cls: int):
+    """(launches, ms, algorithmic flops, algorithmic HBM bytes) of a kernel class"""
+    n, ms, fl, by = _ll(), C.c_double(), C.c_double(), C.c_double()
+    core.kf_prof_collect2(cls, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
+    return n.value, ms.value, fl.value, by.value
+
+
 def set_stream(stream_handle) -> None:
     core.kf_set_stream(C.c_void_p(stream_handle) if stream_handle else None)
 
@@ -192,8 +218,11 @@ def sync() -> None:
 class Network:
     """internal/nnet Network (forward.go:15-21) behind the nnet_* C-ABI."""
 
-    def __init__(self, xconfig: str, max_frames: int):
-        self.h = nnet.nnet_create(xconfig.encode(), int(max_frames))
+    def __init__(self, xconfig: str, max_frames: int, layout_only: bool = False):
+        """layout_only: nnet_create_layout — no device storage, no GPU needed (layer,
+        parameter and data-parallel bucket queries only)."""
+        create = nnet.nnet_create_layout if layout_only else nnet.nnet_create
+        self.h = create(xconfig.encode(), int(max_frames))
         if not self.h:
             raise KfError("nnet_create: " + _err(nnet.nnet_last_error))
         self.max_frames = int(max_frames)
@@ -311,6 +340,21 @@ class Network:
 
     def sgd(self, lr: float, momentum: float):
         check(nnet.nnet_sgd(self.h, float(lr), float(momentum)), "nnet_sgd")
+
+    def dp_plan(self, bucket_bytes: int, max_buckets: int = 256):
+        """[(after_step, begin, end)]: the gradient buckets nnet_backward exchanges
+        (kf_nnet.h nnet_dp_plan), in issue order."""
+        a, b, e = (_i * max_buckets)(), (_ll * max_buckets)(), (_ll * max_buckets)()
+        n = nnet.nnet_dp_plan(self.h, int(bucket_bytes), max_buckets, a, b, e)
+        if n < 0:
+            raise KfError("nnet_dp_plan: " + _err(nnet.nnet_last_error))
+        return [(a[i], b[i], e[i]) for i in range(n)]
+
+    def bind_dp(self, comm, bucket_bytes: int):
+        """Exchange the gradient over `comm` (kfp16.dp.Communicator) in buckets during
+        nnet_backward; comm None unbinds."""
+        check(nnet.nnet_bind_dp(self.h, comm.h if comm is not None else None, int(bucket_bytes)),
+              "nnet_bind_dp")
 
 
 def parse_summary(xconfig: str):

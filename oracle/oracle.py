@@ -52,7 +52,26 @@ def lib(native: bool = False):
         _lib.orc_net_free.argtypes = [C.c_void_p]
         _lib.orc_sgd.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_longlong]
         _lib.orc_mx_qdq_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_int]
+        _lib.gt_matmul.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
+        _lib.gt_affine_forward.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                           C.c_void_p, C.c_void_p, C.c_int]
     return _lib
+
+
+def gotorch_affine_forward(x: np.ndarray, W: np.ndarray, b: np.ndarray, workers: int, lib_=None):
+    """gotorch.AffineLayer.Forward (go/gotorch/layers.go:57-70) restated in C
+    (gotorch_cpu.c): float64, rows split over `workers` threads as matmulParallel."""
+    L = lib_ or lib()
+    x = np.ascontiguousarray(x, np.float64)
+    W = np.ascontiguousarray(W, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    M, K = x.shape
+    N = W.shape[1]
+    y = np.empty((M, N), np.float64)
+    cache = np.empty_like(x)
+    L.gt_affine_forward(x.ctypes.data, M, K, W.ctypes.data, b.ctypes.data, N, y.ctypes.data,
+                        cache.ctypes.data, int(workers))
+    return y
 
 
 ORC = dict(IDCT=1, BATCHNORM=2, CONV=3, TDNNF=4, LINEAR=5, PREFINAL=6, OUTPUT=7, ATTENTION=8, COMBINE=9)

@@ -20,7 +20,34 @@ HEADERS = {
     "kf_nnet.h": "libkaldi_fp16_nnet.so",
     "kf_egs.h": "libkaldi_fp16_egs.so",
     "kf_model.h": "libkaldi_fp16_nnet.so",
+    "kf_dp.h": "libkaldi_fp16.so",
 }
+
+# the reference's libkaldi_fp16_den.so re-exports the den_* ABI that this build
+# keeps inside libkaldi_fp16.so (its Go side links -lkaldi_fp16: chain_loss.go:5)
+REF_LIB = {"libkaldi_fp16.so": "libkaldi_fp16.so", "libkaldi_fp16_cgo.so": "libkaldi_fp16_cgo.so",
+           "libkaldi_fp16_den.so": "libkaldi_fp16.so"}
+
+
+def _is_kernel_stub(name):
+    """__global__ functions of the .cu files (host launch stubs): not callable ABI"""
+    return name.endswith("_kernel") or name.startswith("kernel_")
+
+
+def test_reference_exports_present():
+    """Every C symbol the reference's shipped libraries export (nm -D, fixture
+    tests/golden/reference_exports.txt) is exported by the build's library that
+    replaces it, except CUDA kernel launch stubs."""
+    fx = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_exports.txt")
+    rows = [l.split() for l in open(fx) if l.strip()]
+    assert len(rows) > 100
+    libs = {n: ctypes.CDLL(os.path.join(kfp16.LIBDIR, n)) for n in set(REF_LIB.values())}
+    missing = [(l, s) for l, s in rows if not _is_kernel_stub(s) and not hasattr(libs[REF_LIB[l]], s)]
+    assert not missing, missing
+    stubs = [s for _, s in rows if _is_kernel_stub(s)]
+    assert sorted(set(stubs)) == sorted({"add_kernel", "fp16_to_fp32_kernel", "fp32_to_fp16_kernel",
+                                         "kernel_fp16_to_fp32", "kernel_fp32_to_fp16", "relu_kernel",
+                                         "scale_kernel", "sigmoid_kernel", "softmax_kernel", "tanh_kernel"})
 
 
 @pytest.mark.parametrize("header", sorted(HEADERS))

@@ -230,3 +230,28 @@ def test_batched_objective_repeatable(gpu, den):
         ch.result()
         outs.append(gpu.read_fp16(og.ptr, x.shape))
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_den_exchange_timeout_is_sticky(gpu, den):
+    """A den exchange that gives up (forced: zero polls allowed) makes the next
+    kf_chain_result fail even when a later compute succeeds; the result call that
+    reports it clears the count (chain_den.cu:496-706 must never yield a silently
+    wrong gradient)."""
+    from kfp16 import KfError, chain
+    negs = 4
+    g, init, P, row0, frames, stride, fsts, x = _batch_setup(gpu, den, negs, seed=21)
+    dx = gpu.upload_fp16(x)
+    og = gpu.DeviceBuffer(x.size * 2)
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=negs, max_frames=490)
+    nb = chain.NumBatch(fsts)
+    ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+    good = ch.result()
+    ch.debug_spin_limit(0)           # every unsatisfied wait times out at once
+    ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+    ch.debug_spin_limit(None)
+    ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)  # a good launch after it
+    with pytest.raises(KfError, match="timed out"):
+        ch.result()
+    again = ch.result()               # reported once, then cleared
+    assert again.num_ok == good.num_ok == negs
+    assert again.objf == good.objf
