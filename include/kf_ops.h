@@ -224,6 +224,13 @@ int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
 int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes);
 void kf_prof_reset(void);
 
+/* the panel GEMM for short-reduction wide-output fused products (K = 64 / 128 / 160 / 256 / 320,
+ * csrc/panel.hip): 1 when enabled (KF_PANEL=1; off by default: measured slower than the
+ * tiled GEMM on the MI355X). kf_gemm_debug_panel:
+ * 0 off, 1 on, -1 back to the environment's choice (tests: bit-identical A/B). */
+int kf_panel_enabled(void);
+void kf_gemm_debug_panel(int mode);
+
 const char *kf_last_error(void);
 void kf_clear_error(void);
 

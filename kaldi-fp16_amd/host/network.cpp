@@ -74,6 +74,10 @@ struct NetLayer {
     // MXFP8 forward (nnet_set_fp8): output / aux copies written by the producing
     // GEMM epilogue, and the weights quantised [N][K] with each splice part padded
     Mx a8, x8, w8, w8b;
+    // k-contiguous (transposed) fp16 copy of a short-K forward weight, [N x K], for the
+    // panel GEMM (csrc/panel.hip); refreshed from w16 before a forward after any change
+    void *wt = nullptr;
+    int wt_pi = -1, wt_K = 0, wt_N = 0;
 };
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -202,6 +206,7 @@ struct KfNet {
     void *dbott = nullptr, *edge = nullptr;
     size_t edge_half = 0;
     int fp8 = 0;
+    bool wt_dirty = true;  // the transposed weight copies need a refresh (NetLayer::wt)
     // data parallel (kf_dp.h): gradient buckets exchanged during the backward
     KfDp *dp = nullptr;
     std::vector<int> dp_after;  // bucket j is issued after backward step dp_after[j]
@@ -641,6 +646,29 @@ static bool alloc_device(KfNet *net, int max_frames) {
                         nl.bn2_scale, nl.bn2_shift)))
             return false;
     }
+    // transposed copies of the short-K forward weights (TDNN-F affine, prefinal big)
+    for (auto &nl : net->layers) {
+        const Layer &L = nl.L;
+        int pi = -1, K = 0, N = 0;
+        if (L.type == LayerType::TDNNF) {
+            pi = nl.pW2;
+            K = L.time_stride > 0 ? 2 * L.bottleneck : L.bottleneck;
+            N = L.out_dim;
+        } else if (L.type == LayerType::Prefinal) {
+            pi = nl.pW;
+            K = L.in_dim;
+            N = L.big_dim;
+        }
+        if (pi < 0 || K > 512 || K % 32 || N % 32) continue;
+        nl.wt = net->dalloc((size_t)K * N * 2);
+        if (!nl.wt) {
+            set_err("alloc transposed weights " + L.name);
+            return false;
+        }
+        nl.wt_pi = pi;
+        nl.wt_K = K;
+        nl.wt_N = N;
+    }
     // gradient buffers carry two spare rows for the splice-transpose edge sums
     for (int i = 0; i < 2; ++i) {
         net->dz[i] = net->dalloc((T + 2) * maxw * 2);
@@ -716,6 +744,7 @@ extern "C" int nnet_set_params(KfNet *net, const float *host) {
         return -1;
     }
     bridge_gpu_memset(net->vel, 0, P * 4);
+    net->wt_dirty = true;
     return net->fp8 && !quantise_weights(net, false) ? -1 : 0;
 }
 
@@ -855,10 +884,6 @@ bool mx_weights(KfNet *net, Mx &m, int pi, int nparts, int rows, int N, bool all
                 "quantise weights"))
             return false;
     return true;
-}
-bool gemm_layer(LayerType t) {
-    return t == LayerType::TDNNF || t == LayerType::Linear || t == LayerType::Prefinal ||
-           t == LayerType::Output;
 }
 // the layer's output can carry an MXFP8 copy (its epilogue has 32-column blocks)
 bool f8_producer(const NetLayer &nl) {
@@ -1006,8 +1031,21 @@ extern "C" int nnet_forward_ivector(KfNet *net, const void *features, int T, con
     net->B = B;
     return forward_impl(net, features, T);
 }
+// k-contiguous (transposed) copies of the short-K forward weights: the tiled GEMM's
+// k-contiguous B path beats its reduction-major one on these shapes (TDNN-F affine
+// forward with the full epilogue 243 -> 225 us, scripts/panel_bench.py), and the
+// panel GEMM (csrc/panel.hip, KF_PANEL=1) reads only B^T rows
+static bool refresh_wt(KfNet *net) {
+    if (!net->wt_dirty) return true;
+    for (auto &nl : net->layers)
+        if (nl.wt && !ck(ops_transpose(wptr(net, nl.wt_pi), nl.wt, nl.wt_K, nl.wt_N), "transpose weights"))
+            return false;
+    net->wt_dirty = false;
+    return true;
+}
 static int forward_impl(KfNet *net, const void *features, int T) {
     if (!on_device(net, "forward")) return -1;
+    if (!refresh_wt(net)) return -1;
     if (T <= 0 || T > net->max_T) {
         set_err("forward: T=" + std::to_string(T) + " outside (0, max_frames]");
         return -1;
@@ -1108,7 +1146,9 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 KfOperand A2 = f8b ? op_mx(nl.x8, T, np, 0, s)
                                    : s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 1)
                                            : op_base(nl.aux, bn, T, bn, 1);
-                KfOperand B2 = f8b ? op_mxw(nl.w8b, dout) : op_base(wptr(net, nl.pW2), dout, kaff, dout, 0);
+                KfOperand B2 = f8b             ? op_mxw(nl.w8b, dout)
+                       : nl.wt               ? op_base(nl.wt, kaff, dout, kaff, 1)
+                                             : op_base(wptr(net, nl.pW2), dout, kaff, dout, 0);
                 KfEpilogue E2 = epi0();
                 if (net->fp8) set_out8(E2, nl.a8);
                 E2.out = nl.act;
@@ -1164,7 +1204,9 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 const int big = L.big_dim, small = L.small_dim;
                 const Mx *x8 = in8(net, nl);
                 KfOperand A = x8 ? op_mx(*x8, T, 1, 0, 0) : op_base(x, din, T, din, 1);
-                KfOperand B = x8 ? op_mxw(nl.w8, big) : op_base(wptr(net, nl.pW), big, din, big, 0);
+                KfOperand B = x8                    ? op_mxw(nl.w8, big)
+                              : nl.wt               ? op_base(nl.wt, din, big, din, 1)
+                                                    : op_base(wptr(net, nl.pW), big, din, big, 0);
                 KfEpilogue E = epi0();
                 if (net->fp8) set_out8(E, nl.x8);
                 E.out = nl.aux;
@@ -1609,12 +1651,16 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
 
 extern "C" float *nnet_grad_buffer(KfNet *net) { return net->grad; }
 extern "C" float *nnet_master_buffer(KfNet *net) { return net->master; }
-extern "C" void *nnet_weight_buffer(KfNet *net) { return net->w16; }
+extern "C" void *nnet_weight_buffer(KfNet *net) {
+    net->wt_dirty = true;  // the caller may write the weights through it
+    return net->w16;
+}
 
 extern "C" int nnet_sgd(KfNet *net, float lr, float momentum) {
     if (!on_device(net, "sgd")) return -1;
     if (!ck(kf_sgd_flat(net->master, net->w16, net->grad, net->vel, lr, momentum, net->nparams), "sgd"))
         return -1;
+    net->wt_dirty = true;
     // the MXFP8 weight copies follow every parameter change
     return net->fp8 && !quantise_weights(net, false) ? -1 : 0;
 }

@@ -16,7 +16,7 @@ def kclass(name):
     if m:
         args = [a.strip() for a in m.group(1).split(",")]
         return "gemm_wgrad" if len(args) > 6 and args[6] == "true" else "gemm_fused"
-    if "conv_halo_kernel" in name:  # the conv forward / input-gradient GEMMs (kf_prof class 0)
+    if "conv_halo_kernel" in name or "panel_kernel" in name:  # fused GEMMs too (kf_prof class 0)
         return "gemm_fused"
     for k in ("k_den_fb", "k_den_fwd", "k_den_bwd", "k_den_post", "k_num_fb", "k_conv_c1_wgrad", "k_conv_c1_fwd",
               "k_slab_reduce", "k_sgd_flat"):
