@@ -42,6 +42,9 @@ int bridge_transfer_fp16(void *dst_device, const uint16_t *src_host, size_t coun
 int bridge_read_fp16(uint16_t *dst_host, const void *src_device, size_t count);
 int bridge_transfer_int32(void *dst_device, const int32_t *src_host, size_t count);
 int bridge_transfer_float32(void *dst_device, const float *src_host, size_t count);
+/* MI355X addition: float32 device -> host, synchronous on the library stream. Replaces the
+ * direct cudaMemcpy D2H of internal/nnet/denominator_gpu.go:78-86. */
+int bridge_read_float32(float *dst_host, const void *src_device, size_t count);
 
 /*
  * One-allocation minibatch buffer (bridge.h:34-50, bridge.cu:177-267).

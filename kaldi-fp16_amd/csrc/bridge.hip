@@ -138,6 +138,10 @@ int bridge_transfer_fp16(void *dst_device, const uint16_t *src_host, size_t coun
 int bridge_read_fp16(uint16_t *dst_host, const void *src_device, size_t count) {
     return copy_sync(dst_host, src_device, count * 2, hipMemcpyDeviceToHost, "FP16 D2H", count);
 }
+int bridge_read_float32(float *dst_host, const void *src_device, size_t count) {
+    return copy_sync(dst_host, src_device, count * 4, hipMemcpyDeviceToHost, "float32 D2H",
+                     count);
+}
 int bridge_transfer_int32(void *dst_device, const int32_t *src_host, size_t count) {
     return copy_sync(dst_device, src_host, count * 4, hipMemcpyHostToDevice, "int32 H2D", count);
 }

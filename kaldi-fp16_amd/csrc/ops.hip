@@ -93,16 +93,24 @@ __global__ void k_softmax(h16 *data, int cols, int logmode) {
     float mx = -INFINITY;
     for (int j = threadIdx.x; j < cols; j += blockDim.x) mx = fmaxf(mx, h2f(row[j]));
     mx = block_reduce(mx, true, sh);
-    float s = 0.f;
-    for (int j = threadIdx.x; j < cols; j += blockDim.x) s += expf(h2f(row[j]) - mx);
-    s = block_reduce(s, false, sh);
     if (logmode) {
+        float s = 0.f;
+        for (int j = threadIdx.x; j < cols; j += blockDim.x) s += expf(h2f(row[j]) - mx);
+        s = block_reduce(s, false, sh);
         const float lse = mx + logf(s);
         for (int j = threadIdx.x; j < cols; j += blockDim.x) row[j] = f2h(h2f(row[j]) - lse);
     } else {
-        const float inv = 1.f / s;
-        for (int j = threadIdx.x; j < cols; j += blockDim.x)
-            row[j] = f2h(expf(h2f(row[j]) - mx) * inv);
+        // the reference's two rounding points (ops.cu:70-118): exp is stored as fp16,
+        // the sum is taken over the unrounded fp32 values, then fp16(fp16(e) * (1/sum))
+        float s2 = 0.f;
+        for (int j = threadIdx.x; j < cols; j += blockDim.x) {
+            const float e = expf(h2f(row[j]) - mx);
+            row[j] = f2h(e);
+            s2 += e;
+        }
+        s2 = block_reduce(s2, false, sh);
+        const float inv = 1.f / s2;
+        for (int j = threadIdx.x; j < cols; j += blockDim.x) row[j] = f2h(h2f(row[j]) * inv);
     }
 }
 
@@ -185,12 +193,18 @@ __global__ void k_subsample_rows(h16 *dst, const h16 *src, int out_rows, int col
 }
 
 __global__ void k_act_bwd(const h16 *x, h16 *g, long long n, int kind) {
+    // no fma contraction: LLVM would fold fpext(fp16 product) into an fp32 fma and
+    // drop the intermediate fp16 rounding the reference's __hmul chain performs
+#pragma clang fp contract(off)
     GRID_STRIDE(i, n) {
         const float xv = h2f(x[i]), gv = h2f(g[i]);
+        // fp16 arithmetic as the reference's __hmul / __hsub chain
+        // (backward_wrappers.cu:41-74): every product / difference rounds to fp16
+        // (a product of two fp16 values is exact in fp32, so one RNE matches __hmul)
         float r;
         if (kind == ACT_RELU) r = xv > 0.f ? gv : 0.f;
-        else if (kind == ACT_SIGMOID) r = gv * xv * (1.f - xv);
-        else r = gv * (1.f - xv * xv);
+        else if (kind == ACT_SIGMOID) r = h2f(f2h(gv * xv)) * h2f(f2h(1.f - xv));
+        else r = gv * h2f(f2h(1.f - h2f(f2h(xv * xv))));
         g[i] = f2h(r);
     }
 }

@@ -59,6 +59,7 @@ _sig(core, "bridge_transfer_fp16", _i, _vp, _vp, _sz)
 _sig(core, "bridge_read_fp16", _i, _vp, _vp, _sz)
 _sig(core, "bridge_transfer_int32", _i, _vp, _vp, _sz)
 _sig(core, "bridge_transfer_float32", _i, _vp, _vp, _sz)
+_sig(core, "bridge_read_float32", _i, _vp, _vp, _sz)
 _sig(core, "bridge_gpu_memset", None, _vp, _i, _sz)
 _sig(core, "bridge_fp16_to_fp32_gpu", _i, _vp, _vp, _sz)
 _sig(core, "bridge_fp32_to_fp16_gpu", _i, _vp, _vp, _sz)
@@ -175,8 +176,7 @@ def read_fp16(ptr, shape) -> np.ndarray:
 
 def read_f32(ptr, shape) -> np.ndarray:
     out = np.empty(shape, dtype=np.float32)
-    # bridge has no fp32 read: read the bytes as twice as many fp16 words
-    check(core.bridge_read_fp16(out.ctypes.data, ptr, out.size * 2), "read_f32")
+    check(core.bridge_read_float32(out.ctypes.data, ptr, out.size), "read_f32")
     return out
 
 
