@@ -255,3 +255,35 @@ def test_den_exchange_timeout_is_sticky(gpu, den):
     again = ch.result()               # reported once, then cleared
     assert again.num_ok == good.num_ok == negs
     assert again.objf == good.objf
+
+
+def test_backward_test_fixture_through_abi(gpu):
+    """internal/nnet/backward_test.go:28-140's FST and output (tests/golden/backward_test_fd.npz)
+    through the GPU ABI the Go chain path calls (chain_num_forward_backward and its _det
+    form; labels pdf0 + 1, chain.h). The ABI rounds the fp32 output to fp16 first
+    (chain.cu / chain_det.cu:412-477), so the log-prob is compared with the restated
+    computeChainLossCPU's on the fp16-rounded output (|d| <= 1e-5 per frame) and with the
+    fixture's float32 value within the fp16 rounding of T outputs; posteriors are the
+    fixture's one-hot num_post."""
+    import os
+    from kfp16 import ops_abi  # noqa: F401  (binds chain_num_forward_backward_det)
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "backward_test_fd.npz"))
+    x = z["nnet"]
+    T, P = x.shape
+    S = T + 1
+    f = dict(S=S, A=T, row_ptr=z["row_ptr"][:S + 1], dst=z["col_idx"], pdf1=z["pdf0"] + 1,
+             logw=z["weights"], final_state=np.arange(S, dtype=np.int32),
+             final_w=np.zeros(S, np.float32), start=0)
+    keep = []
+    fst = _device_fst(gpu, f, keep)
+    dx = gpu.upload_f32(x)
+    path = x[np.arange(T), z["pdf0"]]
+    lp16 = float(path.astype(np.float16).astype(np.float64).sum())
+    for fn in (gpu.core.chain_num_forward_backward, gpu.core.chain_num_forward_backward_det):
+        post = gpu.DeviceBuffer(T * P * 4)
+        lp = fn(fst.row_ptr, fst.col_idx, fst.weights, fst.labels, fst.final_states,
+                fst.final_weights, S, T, S, dx.ptr, post.ptr, T, P, None)
+        assert abs(lp - lp16) <= 1e-5 * T
+        assert abs(lp - float(z["num_logprob"])) <= T * 2.0 ** -12
+        gpu.sync()
+        np.testing.assert_allclose(gpu.read_f32(post.ptr, (T, P)), z["num_post"], atol=1e-6)
