@@ -385,7 +385,52 @@ static bool build_topology(KfNet *net, const char *xconfig_text, int max_frames,
         NetLayer nl;
         nl.L = L;
         auto is_seq = [&](int idx) { return idx == -2 || (idx >= 0 && net->layers[idx].per_seq); };
-        if (L.input.kind == kf::InputRef::Append) {
+        auto dim_of = [&](int idx) {
+            return idx == -2 ? net->ivec_dim : idx >= 0 ? net->layers[idx].L.out_dim : net->feat_dim;
+        };
+        if (L.input.kind == kf::InputRef::Append && L.type != LayerType::CombineFeatureMaps) {
+            // General Append(a, b, ...) (forward.go:264-310: column concat of the inputs, in
+            // order; network_backward.go:147-170 splits the gradient back). Each further
+            // part is appended by a hidden combine-feature-maps node of height 1, which
+            // is exactly a column concat [a | b] with b broadcast to the frames of its
+            // sequence when b is per-sequence (an ivector given per frame is B = T
+            // sequences of one frame: the reference's [T x dim] ivector Append).
+            if (L.input_names.size() < 2) {
+                set_err("layer " + L.name + ": Append needs two or more inputs");
+                return false;
+            }
+            std::vector<int> parts;
+            for (const auto &nm : L.input_names) {
+                auto it = index.find(nm);
+                if (it == index.end()) {
+                    set_err("layer " + L.name + ": Append input " + nm + " not found");
+                    return false;
+                }
+                parts.push_back(it->second);
+            }
+            if (is_seq(parts[0])) {
+                set_err("layer " + L.name + ": the first Append input must be frame-level");
+                return false;
+            }
+            int cur = parts[0];
+            for (size_t k = 1; k < parts.size(); ++k) {
+                NetLayer hc;
+                hc.L.type = LayerType::CombineFeatureMaps;
+                hc.L.name = L.name + ".append" + (parts.size() > 2 ? std::to_string(k) : std::string());
+                hc.L.height = 1;
+                hc.L.nf1 = dim_of(cur);
+                hc.L.nf2 = dim_of(parts[k]);
+                hc.L.in_dim = hc.L.out_dim = hc.L.nf1 + hc.L.nf2;
+                hc.L.input.kind = kf::InputRef::Append;
+                hc.input = cur;
+                hc.input2 = parts[k];
+                net->layers.push_back(hc);
+                index[hc.L.name] = cur = (int)net->layers.size() - 1;
+            }
+            nl.L.input.kind = kf::InputRef::Simple;
+            nl.L.input_names = {net->layers[cur].L.name};
+        }
+        if (nl.L.input.kind == kf::InputRef::Append) {
             // only combine-feature-maps takes an Append, of a frame-level and a per-sequence
             // (or frame-level) input (Kaldi's Append(idct-batchnorm, ivector-batchnorm))
             if (L.type != LayerType::CombineFeatureMaps || L.input_names.size() != 2) {
@@ -400,11 +445,11 @@ static bool build_topology(KfNet *net, const char *xconfig_text, int max_frames,
             nl.input = a->second;
             nl.input2 = b->second;
         } else {
-            if (L.input_names.size() != 1) {
+            if (nl.L.input_names.size() != 1) {
                 set_err("layer " + L.name + ": one input expected");
                 return false;
             }
-            auto it = index.find(L.input_names[0]);
+            auto it = index.find(nl.L.input_names[0]);
             if (it == index.end()) {
                 set_err("layer " + L.name + ": input not found");
                 return false;
@@ -1298,6 +1343,18 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
         case LayerType::Prefinal:
             if (pl.has_bn2) E.scale2 = pl.bn2_scale;
             return true;
+        case LayerType::Batchnorm:
+            // batchnorm-component (frozen statistics): the gradient at its input is the
+            // output gradient times its per-column scale (backward_wrappers.cu:105-115),
+            // applied in the producing GEMM's epilogue; the step through the BN layer is
+            // then a pass-through (backward_impl). Its own input must take a raw gradient.
+            if (pl.input < 0 || !(net->layers[pl.input].L.type == LayerType::Linear)) {
+                set_err("backward: gradient through batchnorm-component " + L.name +
+                        " into a layer other than linear-component is not supported");
+                return false;
+            }
+            E.scale2 = pl.bn_scale;
+            return true;
         case LayerType::Linear:
         case LayerType::CombineFeatureMaps:  // raw gradient; its backward splits it (ivector branch)
             return true;
@@ -1621,6 +1678,11 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 want_dx = false;
                 break;
             case LayerType::Batchnorm:
+                if (want_dx) {  // dz already is the gradient at the BN input (dx_epilogue)
+                    if (net->dp && !dp_issue(net, dp_next, done)) return -1;
+                    continue;   // same dz / gcur buffers for the layer below: no flip
+                }
+                break;
             case LayerType::IDCT:
             case LayerType::SpecAugment:
                 if (want_dx) {

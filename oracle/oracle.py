@@ -126,15 +126,27 @@ def parse_xconfig(text: str):
             dims[name] = int(kv["dim"])
             prev = name
             continue
-        inp2 = None
+        inp2, parts = None, None
         if inp.startswith("Append(") and inp.endswith(")"):       # xconfig.go:304-313
             parts = inp[7:-1].split(",")
             inp, inp2 = parts[0], parts[1]
-            din = dims[inp] + dims[inp2]
+            din = sum(dims[q] for q in parts)
         else:
             if inp.startswith("ReplaceIndex(") and inp.endswith(")"):   # xconfig.go:315-320
                 inp = inp[13:-1].split(",")[0]
             din = dims[inp]
+        if parts is not None and kind != "combine-feature-maps-layer":
+            # general Append (forward.go:264-310): a hidden height-1 combine node per
+            # further part, the same graph the product builds (host/network.cpp)
+            cur = parts[0]
+            for k in range(1, len(parts)):
+                hn = name + ".append" + (str(k) if len(parts) > 2 else "")
+                layers.append(dict(kind="combine-feature-maps-layer", name=hn, input=cur, input2=parts[k],
+                                   in_dim=dims[cur] + dims[parts[k]], out_dim=dims[cur] + dims[parts[k]],
+                                   height=1, nf1=dims[cur], nf2=dims[parts[k]], kv={}, hidden=True))
+                dims[hn] = dims[cur] + dims[parts[k]]
+                cur = hn
+            inp, inp2 = cur, None
         L = dict(kind=kind, name=name, input=inp, input2=inp2, in_dim=din, kv=kv)
         if kind == "idct-layer":
             L["out_dim"] = int(kv.get("dim", din))
