@@ -682,6 +682,11 @@ int kf_prof_start(int cls, double work) {
     g_prof_recs.push_back(rec);
     return (int)g_prof_recs.size() - 1;
 }
+int kf_prof_start2(int cls, double flops, double bytes) {
+    const int i = kf_prof_start(cls, flops);
+    if (i >= 0) g_prof_recs[i].bytes = bytes;
+    return i;
+}
 void kf_prof_stop(int idx) {
     if (idx < 0 || idx >= (int)g_prof_recs.size()) return;
     hipEventRecord(g_prof_recs[idx].b, kf_stream());
@@ -1099,6 +1104,18 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
 #undef KF_FUSED
 }
 
+// split-K reduce of kf_gemm_wgrad's slabs (also used by conv_wgrad.hip)
+void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int M, int N, float *dW,
+                     long long ldw, float *bias_grad, int accumulate) {
+    k_slab_reduce<<<kf_blocks((long long)M * N / 4 + 1, 256, 4096), 256, 0, kf_stream()>>>(
+        slab, splits, M, N, dW, ldw, accumulate);
+    if (bias_grad)
+        k_slab_reduce_cols<<<(N + 63) / 64, 256, 0, kf_stream()>>>(bias_slab, splits, N, bias_grad, accumulate);
+}
+
+int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
+                           float *bias_grad, int accumulate);
+
 extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              float *dW, long long ldw, float *bias_grad, int accumulate) {
     if (M <= 0 || N <= 0) return 0;
@@ -1109,6 +1126,11 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         return -1;
     }
     if (!mn_gen_ok(a, "A") || !mn_gen_ok(b, "B")) return -1;
+    // 3x3 convolutions: the source halo in LDS instead of nine im2col slabs
+    {
+        const int hr = kf_conv_wgrad_halo_try(M, N, K, a, b, dW, ldw, bias_grad, accumulate);
+        if (hr != 0) return hr < 0 ? -1 : 0;
+    }
     static const int wbig = getenv("KF_GEMM_WBIG") ? atoi(getenv("KF_GEMM_WBIG")) : 1;
     static const int w160 = getenv("KF_GEMM_W160") ? atoi(getenv("KF_GEMM_W160")) : 1;
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
@@ -1180,11 +1202,7 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     else KF_WG(OP_GEN, OP_GEN);
 #undef KF_WG
     if (rc) return rc;
-    k_slab_reduce<<<kf_blocks((long long)M * N / 4 + 1, 256, 4096), 256, 0, kf_stream()>>>(
-        G.slab, splits, M, N, dW, ldw, accumulate);
-    if (bias_grad)
-        k_slab_reduce_cols<<<(N + 63) / 64, 256, 0, kf_stream()>>>(G.bias_slab, splits, N,
-                                                                   bias_grad, accumulate);
+    kf_wgrad_reduce(G.slab, G.bias_slab, splits, M, N, dW, ldw, bias_grad, accumulate);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         kf_set_error("wgrad reduce: %s", hipGetErrorString(e));

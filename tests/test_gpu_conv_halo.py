@@ -95,3 +95,32 @@ def test_conv_halo_input_grad(gpu, hin, fin, hout, sub, fout, T):
                                            C.byref(e2)))
     ref = _col2im_ref(dz.astype(np.float64) @ W.astype(np.float64).T, T, hin, hout, sub, fin)
     _check(kf.read_fp16(gx.ptr, (T * hin, fin)).astype(np.float64), ref, 9 * fout)
+
+
+# weight gradient (conv_wgrad_halo_kernel, taken by kf_gemm_wgrad for 9-tap im2col
+# operands with 64-channel parts): small T (one split, partial last K-step) and
+# larger T (many splits over the reduction, K-steps straddling frames)
+WSHAPES = SHAPES + [(40, 64, 40, 1, 64, 203), (40, 64, 20, 2, 128, 171), (20, 128, 20, 1, 128, 150),
+                    (20, 128, 10, 2, 256, 333), (10, 256, 10, 1, 256, 257)]
+
+
+@pytest.mark.parametrize("hin,fin,hout,sub,fout,T", WSHAPES)
+def test_conv_halo_wgrad(gpu, hin, fin, hout, sub, fout, T):
+    kf = gpu
+    rng = np.random.default_rng(11 + hin * fout + T)
+    x = _h(rng.standard_normal((T, hin * fin)))
+    M, K = T * hout, 9 * fin
+    dz = _h(rng.standard_normal((M, fout)))
+    dx, ddz = kf.upload_fp16(x), kf.upload_fp16(dz)
+    gW = kf.DeviceBuffer(K * fout * 4)
+    gb = kf.DeviceBuffer(fout * 4)
+    a = kf.operand(dx.ptr, hin * fin, M, K, 0, nparts=9, part_width=fin, T=T, hout=hout, hsrc=hin,
+                   hmul=sub, hdiv=1, tpolicy=0, dt=[o[0] for o in OFFS], dh=[o[1] for o in OFFS])
+    b = kf.operand(ddz.ptr, fout, M, fout, 0)
+    kf.check(kf.core.kf_gemm_wgrad(K, fout, M, C.byref(a), C.byref(b), gW.ptr, fout, gb.ptr, 0))
+    P = im2col(x.astype(np.float64), T, hin, fin, hout, sub, OFFS)
+    _check(kf.read_f32(gW.ptr, (K, fout)), P.T @ dz.astype(np.float64), M)
+    _check(kf.read_f32(gb.ptr, (fout,)), dz.astype(np.float64).sum(0), M)
+    # accumulate = 1 adds onto the existing gradient
+    kf.check(kf.core.kf_gemm_wgrad(K, fout, M, C.byref(a), C.byref(b), gW.ptr, fout, gb.ptr, 1))
+    _check(kf.read_f32(gW.ptr, (K, fout)), 2 * (P.T @ dz.astype(np.float64)), M)
