@@ -231,6 +231,15 @@ void kf_prof_reset(void);
 int kf_panel_enabled(void);
 void kf_gemm_debug_panel(int mode);
 
+/* the row-panel GEMM for the same shapes with K = 160 / 256 / 320 and N % 32 == 0
+ * (csrc/rowpanel.hip: A rows in registers, weights and epilogue row operands streamed by
+ * LDS-DMA per 32-column block). Off by default (KF_ROWPANEL=1 turns it on): slower than
+ * the tiled GEMM on the MI355X. kf_gemm_debug_rowpanel: 0 off, 1 on, -1
+ * back to the environment's choice. kf_rowpanel_trace: phase timestamps of one block
+ * (diagnostics, scripts/rp_trace.py); NULL turns them off. */
+void kf_gemm_debug_rowpanel(int mode);
+void kf_rowpanel_trace(unsigned long long *buf);
+
 const char *kf_last_error(void);
 void kf_clear_error(void);
 

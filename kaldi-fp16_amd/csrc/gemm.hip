@@ -738,6 +738,9 @@ static double epi_bytes(const KfEpilogue &E, long long M, long long N) {
     if (E.out8) b += mn + mn / 32;
     return b;
 }
+double kf_gemm_alg_bytes(const OpD &a, const OpD &b, const KfEpilogue &E, long long M, long long N) {
+    return op_src_bytes(a, 0) + op_src_bytes(b, 0) + epi_bytes(E, M, N);
+}
 extern "C" void kf_prof_reset(void) {
     for (auto &r : g_prof_recs) {
         hipEventSynchronize(r.b);
@@ -993,6 +996,9 @@ static int gemm_big() {
     return e ? atoi(e) : 1;
 }
 
+int kf_rowpanel_try(int M, int N, int K, const OpD &a, const OpD &b, int am, int bm, bool bkc,
+                    const KfEpilogue &E);
+
 extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              const KfEpilogue *epi) {
     if (M <= 0 || N <= 0) return 0;
@@ -1057,6 +1063,10 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
             g_prof_recs.push_back(rec);
         }
         return rc;
+    }
+    {
+        const int hr = kf_rowpanel_try(M, N, K, a, b, am, bm, B->kcontig != 0, E);
+        if (hr != 0) return hr < 0 ? -1 : 0;
     }
     if (!E.out8) {
         const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);

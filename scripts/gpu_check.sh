@@ -25,6 +25,6 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 3}
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-    step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-prof
+    step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-prof --no-extra
 fi
 echo "== done"

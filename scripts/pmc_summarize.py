@@ -16,6 +16,8 @@ def kclass(name):
     if m:
         args = [a.strip() for a in m.group(1).split(",")]
         return "gemm_wgrad" if len(args) > 6 and args[6] == "true" else "gemm_fused"
+    if "conv_wgrad_halo_kernel" in name:  # conv weight gradients (kf_prof class 1)
+        return "gemm_wgrad"
     if "conv_halo_kernel" in name or "panel_kernel" in name:  # fused GEMMs too (kf_prof class 0)
         return "gemm_fused"
     for k in ("k_den_fb", "k_den_fwd", "k_den_bwd", "k_den_post", "k_num_fb", "k_conv_c1_wgrad", "k_conv_c1_fwd",
