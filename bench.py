@@ -192,6 +192,7 @@ def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
         on.forward(feats, ivectors=iv, seq_off=np.array([0, frames], np.int32))
     else:
         on.forward(feats)
+    t_fwd = time.perf_counter() - t0
     out = on.act("output")
     deriv, _ = oracle.chain_objf(g, init, num_fst, out[rows])
     og = np.zeros_like(out)
@@ -201,10 +202,12 @@ def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
     on.close()
     name = "cnn_tdnn_17f with the ivector front end" if D else "cnn_tdnn_17f"
     return {"value": round(frames / dt, 2), "unit": "frames/sec", "cores": threads, "host_cores": host_cores(),
+            "forward_frames_per_sec": round(frames / t_fwd, 2),
             "kind": "port",
             "sample": f"restatement, not Go: C oracle train step (fwd, chain objective, bwd) of {name} on "
-                      f"{frames} frames (1 eg), fp32 math, GEMM rows split over {threads} threads "
-                      f"(go/gotorch/ops.go:49-81 policy), {dt:.1f} s"}
+                      f"{frames} frames (1 eg), fp32 math (SURVEY 8d: gotorch-style float32/float64 layers), "
+                      f"GEMM rows split over {threads} threads (go/gotorch/ops.go:49-81 policy), {dt:.1f} s; "
+                      f"forward alone {t_fwd:.1f} s"}
 
 
 def config1_affine(threads, reps=50):

@@ -112,19 +112,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wgrad_halo_kernel(OpD B,
     // ring's counted waits see the same number of loads per step on every wave.
     // The row -> (frame, height) map does not depend on the K-step: each lane keeps
     // its pieces' frame index and in-frame byte offset (-1: a padding height).
-    int pf[HPW_MAX], poff[HPW_MAX];
+    // packed (frame << 20) | in-frame byte offset, -1 for a padding height (host-checked:
+    // offsets < 2^20, frames < 2^11)
+    int pfo[HPW_MAX];
     static_for<HPW_MAX>([&](auto I) {
         constexpr int i = decltype(I)::value;
         const int R = 8 * (wave + i * WNW) + (lane >> 3);
-        pf[i] = 0;
-        poff[i] = -1;
+        pfo[i] = -1;
         if (i < H.hpw && R < H.rows) {
             const int f = R / H.hpos, pos = R - f * H.hpos;
             const int par = pos / H.hpe, idx = pos - par * H.hpe;
             const int sh = idx * H.hmul + par - H.pad;
             const int kc = (lane & 7) ^ hsw(R);  // logical chunk of this slot
-            pf[i] = f;
-            if ((unsigned)sh < (unsigned)H.hsrc) poff[i] = (sh * H.fin + cc * BK + kc * 8) * 2;
+            if ((unsigned)sh < (unsigned)H.hsrc) pfo[i] = (f << 20) | ((sh * H.fin + cc * BK + kc * 8) * 2);
         }
     });
     const unsigned ldb = (unsigned)(H.ld * 2);
@@ -135,9 +135,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wgrad_halo_kernel(OpD B,
             constexpr int i = decltype(I)::value;
             if (i < H.hpw) {
                 const int q = wave + i * WNW;
-                const int t = tb + pf[i];
-                const unsigned voff = poff[i] >= 0 && (unsigned)t < (unsigned)H.T
-                                          ? (unsigned)t * ldb + (unsigned)poff[i] : BAD;
+                const int t = tb + (pfo[i] >> 20);
+                const unsigned voff = pfo[i] >= 0 && (unsigned)t < (unsigned)H.T
+                                          ? (unsigned)t * ldb + (unsigned)(pfo[i] & 0xFFFFF) : BAD;
                 char *d = q < H.npieces ? dst + q * 1024 : dummy;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
                     rx, (__attribute__((address_space(3))) void *)d, 16, voff, 0, 0, 0);
@@ -272,7 +272,7 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     // tiles on 8 waves for every layer (cnn6 1330 -> 1238 us, cnn4 690 -> 640 us);
     // KF_WHALO_BN=128 selects the 8-wave form (A/B)
     static const int bn_env = getenv("KF_WHALO_BN") ? atoi(getenv("KF_WHALO_BN")) : 64;
-    const int BN = bn_env == 128 && N % 128 == 0 ? 128 : 64;
+    int BN = bn_env == 128 && N % 128 == 0 ? 128 : 64;
     int dtmin = 1 << 20, dtmax = -(1 << 20), dhmin = 1 << 20, dhmax = -(1 << 20);
     for (int p = 0; p < WTAPS; ++p) {
         dtmin = std::min(dtmin, a.dt[p]);
@@ -309,13 +309,16 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     H.mout = K;
     // BN = 64: 4-wave workgroups, two per CU; BN = 128: 8 waves, one per CU.
     // Stages: 3 where they fit in LDS (KF_WHALO_NS overrides), else 2.
+    // a halo too large for 4 waves' registers (cnn3: 37 pieces) takes the 8-wave form
+    if (BN == 64 && (H.npieces + 3) / 4 > HPW_MAX && N % 128 == 0) BN = 128;
     const int nw = BN == 64 ? 4 : 8;
     H.hpw = (H.npieces + nw - 1) / nw;
-    if (H.hpw > HPW_MAX) return 0;
+    if (H.hpw > HPW_MAX || H.nf >= 2048 || (long long)a.hsrc * a.pw * 2 >= (1 << 20)) return 0;
     static const int ns_env = getenv("KF_WHALO_NS") ? atoi(getenv("KF_WHALO_NS")) : 0;
     const size_t stage = (size_t)H.halo_bytes + (size_t)BN * BK * 2;
     const size_t cap = BN == 64 ? 80 * 1024 : 160 * 1024;  // BN = 64: leave room for 2 per CU
-    int ns = ns_env ? ns_env : (3 * stage + 1024 <= cap ? 3 : 2);
+    // (8-wave tiles: 2 stages, measured faster than 3)
+    int ns = ns_env ? ns_env : (BN == 64 && 3 * stage + 1024 <= cap ? 3 : 2);
     if (ns < 2 || ns > 3) ns = 2;
     const size_t lds = ns * stage + 1024;
     if (lds > 160 * 1024 || (ns - 2) * (H.hpw + BN / 8 / nw) > 15) return 0;

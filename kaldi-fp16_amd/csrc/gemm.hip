@@ -549,8 +549,16 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        if (H.nbuf == 1 && c > 0 && p == 0) {
+            // one halo image (two do not fit beside the B ring): every wave is past the
+            // previous chunk's last fragment reads, so reload it in place and wait
+            halo_issue(c, 0, 0, H.npieces);
+            wait_vmcnt<0>();
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        }
         if (st + 1 < steps) issue_b(st + 1, bring + ((st + 1) & 1) * B_STAGE);
-        if (c + 1 < H.nch) {
+        if (H.nbuf > 1 && c + 1 < H.nch) {
             const int q0 = p * H.slice;
             halo_issue(c + 1, (c + 1) & 1, q0, min(H.npieces, q0 + H.slice));
         }
@@ -971,7 +979,14 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
         H.halo_bytes = H.npieces * 1024;
         const int nw = BN_ == 64 ? 4 : 8, wtn = BN_ == 64 ? 64 : BN_ == 128 ? 64 : 64;
         const size_t epi = 16 * BN_ + 32 * (wtn + 4) * 4 * nw;
-        const size_t lds = std::max((size_t)H.nbuf * H.halo_bytes + 2 * BN_ * BK * 2, epi);
+        size_t lds = std::max((size_t)H.nbuf * H.halo_bytes + 2 * BN_ * BK * 2, epi);
+        // two halo images too large (cnn5's stride-2 forward: 80 KB each beside a 64 KB
+        // B ring): one image, reloaded between channel chunks (KF_HALO_ONE=0: im2col GEMM)
+        static const int one = getenv("KF_HALO_ONE") ? atoi(getenv("KF_HALO_ONE")) : 1;
+        if (lds > 160 * 1024 && H.nbuf == 2 && one) {
+            H.nbuf = 1;
+            lds = std::max((size_t)H.halo_bytes + 2 * BN_ * BK * 2, epi);
+        }
         if (lds > 160 * 1024) continue;
 #define KF_HALO(BKC_, BMODE_, BROW_)                                                                     \
         do {                                                                                      \
