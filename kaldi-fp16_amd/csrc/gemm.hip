@@ -968,10 +968,16 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     }
     // 32-bit source offsets: the largest byte offset the halo can form
     if (((long long)a.T * a.ld + (long long)a.hsrc * a.pw) * 2 >= (1LL << 32) - 64) return 0;
-    const int BN_ = N <= 64 ? 64 : N <= 128 ? 128 : 256;
+    static const int bn_max = getenv("KF_HALO_BNMAX") ? atoi(getenv("KF_HALO_BNMAX")) : 256;
+    static const int bm_env = getenv("KF_HALO_BM") ? atoi(getenv("KF_HALO_BM")) : 256;
+    const int BN_ = (N <= 64 || bn_max <= 64) ? 64 : (N <= 128 || bn_max <= 128) ? 128 : 256;
     // 256-row tiles only: where the two halo images do not fit beside a 256-column B ring
     // (cnn5's stride-2 forward) the 128-row halo tile measured slower than im2col
-    for (int BM_ : {256}) {
+    // 128-row tiles for the strided convs' per-residue input gradients (3 or 6 taps; two
+    // workgroups per CU): cnn3 461 -> 332 and 588 -> 460 us, cnn5 370 -> 317 and
+    // 536 -> 468 us; 256-row tiles for everything else (KF_HALO_BM=128 forces 128)
+    const bool residue = brow && a.nparts < 9;
+    for (int BM_ : {bm_env == 128 || residue ? 128 : 256}) {
         H.nf = (BM_ - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
         H.rows = H.nf * H.hpos;
         H.npieces = (H.rows + 7) / 8;
