@@ -463,10 +463,36 @@ struct HaloArgs {
     int bshift[KF_MAX_PARTS];  // BROW: row shift of tap p's weight block (op_wrows)
 };
 
+// s_waitcnt vmcnt(n) for a wave-uniform run-time n <= 15
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+    switch (n) {
+        case 0: wait_vmcnt<0>(); break;
+        case 1: wait_vmcnt<1>(); break;
+        case 2: wait_vmcnt<2>(); break;
+        case 3: wait_vmcnt<3>(); break;
+        case 4: wait_vmcnt<4>(); break;
+        case 5: wait_vmcnt<5>(); break;
+        case 6: wait_vmcnt<6>(); break;
+        case 7: wait_vmcnt<7>(); break;
+        case 8: wait_vmcnt<8>(); break;
+        case 9: wait_vmcnt<9>(); break;
+        case 10: wait_vmcnt<10>(); break;
+        case 11: wait_vmcnt<11>(); break;
+        case 12: wait_vmcnt<12>(); break;
+        case 13: wait_vmcnt<13>(); break;
+        case 14: wait_vmcnt<14>(); break;
+        case 15: wait_vmcnt<15>(); break;
+        default: wait_vmcnt<0>(); break;
+    }
+}
+
 // BROW: B is op_wrows' shifted weight rows (input gradient); the kernel then stages
 // it as a plain 64-column operand whose base moves per step (scalar), instead of
 // re-deriving every chunk's part offsets as the general stager would each step.
-template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW>
+// ST: B ring stages. With ST > 2 the waits are counted (every wave knows how many
+// loads it issued in each step: its share of that step's halo slice plus its B
+// chunks), so ST - 2 weight stages stay in flight across each barrier.
+template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW, int ST>
 __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N, OpD B, KfEpilogue E,
                                                                     HaloArgs H, int n_mtiles,
                                                                     int n_ntiles) {
@@ -475,8 +501,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
     constexpr int TM = WTM / 16, TN = WTN / 16;
     constexpr int B_STAGE = BN * BK * 2;
     using SB = Stager<BKC, BN, BMODE, NW>;
+    static_assert(SB::EVEN, "uniform B loads per wave");
     extern __shared__ __attribute__((aligned(16))) char dsm[];
-    char *bring = dsm + H.nbuf * H.halo_bytes;  // 2 B stages after the halo images
+    char *bring = dsm + H.nbuf * H.halo_bytes;  // ST B stages after the halo images
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -542,11 +569,33 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
             sb.issue(B, rb, p1 * H.pw + c1 * BK, K, dst, wave, lane);
         }
     };
+    // this wave's halo loads in the slice issued at step s (0 when none is issued)
+    auto halo_count = [&](int s) {
+        const int cs = s / H.ntaps, ps = s - cs * H.ntaps;
+        if (H.nbuf < 2 || cs + 1 >= H.nch) return 0;
+        const int q0 = ps * H.slice, q1 = min(H.npieces, q0 + H.slice);
+        return q1 - q0 > wave ? (q1 - q0 - wave + NW - 1) / NW : 0;
+    };
     halo_issue(0, 0, 0, H.npieces);
-    issue_b(0, bring);
+    static_for<ST - 1>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        if (i < steps) issue_b(i, bring + i * B_STAGE);
+    });
+    // loads this wave issued in the last two steps (for the counted waits of ST = 3, 4)
+    int n1 = (ST >= 3 && ST - 2 < steps) ? SB::NC : 0, n2 = (ST >= 4 && ST - 3 < steps) ? SB::NC : 0;
+    int sb_st = 0;  // B stage of step st
     for (int st = 0; st < steps; ++st) {
         const int c = st / H.ntaps, p = st - c * H.ntaps;
-        wait_vmcnt<0>();
+        if constexpr (ST == 2) {
+            wait_vmcnt<0>();
+        } else {
+            // B(st) was issued ST - 1 steps ago; younger: everything of the last ST - 2
+            // steps. At a chunk start the halo of chunk c (its last slice issued first in
+            // step st - 1) must have landed too: younger than it, only step st - 1's B.
+            int younger = ST == 3 ? n1 : n1 + n2;
+            if (c > 0 && p == 0) younger = min(younger, st - 1 + ST - 1 < steps ? (int)SB::NC : 0);
+            wait_vmcnt_rt(younger);
+        }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if (H.nbuf == 1 && c > 0 && p == 0) {
@@ -557,13 +606,23 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (st + 1 < steps) issue_b(st + 1, bring + ((st + 1) & 1) * B_STAGE);
+        // the halo slice first, then the B stage (the order the waits above count)
         if (H.nbuf > 1 && c + 1 < H.nch) {
             const int q0 = p * H.slice;
             halo_issue(c + 1, (c + 1) & 1, q0, min(H.npieces, q0 + H.slice));
         }
+        const bool issue = st + ST - 1 < steps;
+        if (issue) {
+            const int sn = sb_st == 0 ? ST - 1 : sb_st - 1;  // (st + ST - 1) % ST
+            issue_b(st + ST - 1, bring + sn * B_STAGE);
+        }
+        if constexpr (ST >= 3) {
+            n2 = n1;
+            n1 = halo_count(st) + (issue ? SB::NC : 0);
+        }
         const char *ta = dsm + (H.nbuf > 1 ? (c & 1) : 0) * H.halo_bytes;
-        const char *tb = bring + (st & 1) * B_STAGE;
+        const char *tb = bring + sb_st * B_STAGE;
+        sb_st = sb_st + 1 == ST ? 0 : sb_st + 1;
         const int ct = __builtin_amdgcn_readfirstlane(H.ctap[p]);
         static_for<BK / 32>([&](auto S) {
             constexpr int s = decltype(S)::value;
@@ -889,7 +948,7 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
 // 1 when launched, 0 when not applicable (the caller runs the im2col GEMM), -1 on error.
 // KF_CONV_HALO=0 disables it (A/B).
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW>
+template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW, int ST>
 static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const HaloArgs &H, size_t lds) {
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     ProfRec rec{};
@@ -901,7 +960,7 @@ static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const Ha
         rec.bytes = (double)H.T * H.hsrc * H.pw * 2.0 + (double)H.ntaps * H.pw * N * 2.0 + epi_bytes(E, M, N);
         hipEventRecord(rec.a, kf_stream());
     }
-    conv_halo_kernel<BM, BN, WM, WN, BKC, BMODE, BROW>
+    conv_halo_kernel<BM, BN, WM, WN, BKC, BMODE, BROW, ST>
         <<<dim3(mt * nt), 64 * WM * WN, lds, kf_stream()>>>(M, N, B, E, H, mt, nt);
     if (g_prof) {
         hipEventRecord(rec.b, kf_stream());
@@ -994,16 +1053,33 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
             lds = std::max((size_t)H.halo_bytes + 2 * BN_ * BK * 2, epi);
         }
         if (lds > 160 * 1024) continue;
+        // KF_HALO_ST=4: a 4-stage B ring on 256-row tiles where it fits (two weight stages
+        // in flight across each barrier). Off: measured slower (cnn2 fwd / dgrad 517 / 521
+        // -> 884 / 986 us at one workgroup per CU instead of two, no layer faster)
+        static const int st_env = getenv("KF_HALO_ST") ? atoi(getenv("KF_HALO_ST")) : 2;
+        int ST_ = 2;
+        {
+            const int nw_ = BN_ == 64 ? 4 : 8, nc = BN_ / 8 / nw_;
+            const int hpw = (H.nbuf > 1 ? (H.slice + nw_ - 1) / nw_ : 0);
+            const size_t lds4 = std::max((size_t)H.nbuf * H.halo_bytes + 4 * BN_ * BK * 2, epi);
+            if (st_env >= 4 && BM_ == 256 && lds4 <= 160 * 1024 && 2 * (hpw + nc) <= 15) {
+                ST_ = 4;
+                lds = lds4;
+            }
+        }
 #define KF_HALO(BKC_, BMODE_, BROW_)                                                                     \
         do {                                                                                      \
             if (BN_ == 64)                                                                        \
-                return BM_ == 256 ? launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds)  \
-                                  : launch_halo<128, 64, 4, 1, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds); \
+                return BM_ == 128 ? launch_halo<128, 64, 4, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds)  \
+                       : ST_ == 4 ? launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_, 4>(M, N, bp, E, H, lds)  \
+                                  : launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds); \
             if (BN_ == 128)                                                                       \
-                return BM_ == 256 ? launch_halo<256, 128, 4, 2, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds) \
-                                  : launch_halo<128, 128, 4, 2, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds); \
-            return BM_ == 256 ? launch_halo<256, 256, 2, 4, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds)     \
-                              : launch_halo<128, 256, 2, 4, BKC_, BMODE_, BROW_>(M, N, bp, E, H, lds);    \
+                return BM_ == 128 ? launch_halo<128, 128, 4, 2, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds) \
+                       : ST_ == 4 ? launch_halo<256, 128, 4, 2, BKC_, BMODE_, BROW_, 4>(M, N, bp, E, H, lds) \
+                                  : launch_halo<256, 128, 4, 2, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds); \
+            return BM_ == 128 ? launch_halo<128, 256, 2, 4, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds)     \
+                   : ST_ == 4 ? launch_halo<256, 256, 2, 4, BKC_, BMODE_, BROW_, 4>(M, N, bp, E, H, lds)     \
+                              : launch_halo<256, 256, 2, 4, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds);    \
         } while (0)
         if (bkc) KF_HALO(true, OP_SIMPLE, true);
         KF_HALO(false, OP_SIMPLE, false);
