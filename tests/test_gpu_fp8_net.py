@@ -119,3 +119,68 @@ def test_config5_fp8_forward_and_objective(gpu):
     assert r8["ok"] == 1 and d <= FP8_OBJF_TOL, (r8["objf"] / nfr[0], r16["objf"] / nfr[0])
     on.close()
     net.close()
+
+
+FP8_GRAD_TOL = 0.15    # weight gradients vs the oracle's MXFP8 emulation (chaotic e4m3 flips, as above)
+
+
+def _fp8_backward_errors(kfp16, xcfg, T, seed=7):
+    """MXFP8 forward, fp16 backward of a fixed output gradient on the GPU; the oracle
+    replays the GPU's ReLU decisions in its fp16 and its MXFP8-emulating forward and
+    back-propagates the same gradient. Returns ({param: err vs MX emulation},
+    {param: err vs fp16}, the params of layers up to the first fp8 layer)."""
+    from kfp16 import synth
+    net, params, bns, feats, fbuf = _net(kfp16, xcfg, T)
+    net.set_fp8(True)
+    net.forward(fbuf.ptr, T)
+    masks = net.relu_masks()
+    P = net.layers[-1][3]
+    og = (np.random.default_rng(seed).standard_normal((T, P)) * 0.05).astype(np.float16)
+    gbuf = kfp16.upload_fp16(og)
+    net.backward(gbuf.ptr)
+    got = net.read_grads()
+    first = next(i for i, L in enumerate(net.layers) if L[1] in FP8_TYPES)
+    early = {L[0] for L in net.layers[:first + 1]}
+    net.close()
+    tp = {k: synth.trunc_fp16(v) for k, v in params.items()}
+    refs = []
+    for mx8 in (True, False):
+        on = oracle.OracleNet(xcfg, tp, bns, round_mode=oracle.ROUND_FUSED, threads=16, mx8=mx8)
+        on.forward(feats.astype(np.float32), force_masks=masks)
+        on.backward(og.astype(np.float32))
+        refs.append(on.grads())
+        on.close()
+    emx = {k: rel_fro(got[k], refs[0][k]) for k in refs[0]}
+    e16 = {k: rel_fro(got[k], refs[1][k]) for k in refs[1]}
+    early_params = {k for k in emx if k.split(".")[0] in early}
+    return emx, e16, early_params
+
+
+def _check_fp8_grads(emx, e16, early_params, early_tol):
+    msg = "; ".join(f"{k} {emx[k]:.3g}/{e16[k]:.3g}" for k in emx)
+    print("fp8 backward grad errors (vs MX emulation / vs fp16):", msg)
+    for k in emx:
+        assert emx[k] <= FP8_GRAD_TOL, msg
+        if k in early_params:
+            assert emx[k] <= early_tol, msg
+        else:  # the backward differentiates the fp8 forward it ran after
+            assert emx[k] <= max(e16[k], 5e-3), msg
+    # the gradients really carry the fp8 forward (not a silently fp16 one)
+    assert max(e16.values()) > 1e-2, msg
+
+
+def test_tiny_fp8_backward(gpu):
+    """configs[4]'s train step runs the fp16 backward on the MXFP8 forward's
+    activations: its weight gradients follow the oracle's MX emulation (replayed ReLU
+    decisions), within the fp16 bar up to the first fp8 layer"""
+    from kfp16 import synth
+    emx, e16, early = _fp8_backward_errors(gpu, synth.load_xconfig("tiny.xconfig"), 300)
+    _check_fp8_grads(emx, e16, early, early_tol=2e-2)
+
+
+@pytest.mark.slow
+def test_config5_fp8_backward(gpu):
+    """the same on the configs[4] model (cnn_tdnn_17f_3072), 150 frames"""
+    from kfp16 import synth
+    emx, e16, early = _fp8_backward_errors(gpu, synth.load_xconfig("cnn_tdnn_17f_3072.xconfig"), 150)
+    _check_fp8_grads(emx, e16, early, early_tol=2e-2)
