@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
                                                                KfEpilogue E, WgradArgs G,
                                                                int n_mtiles, int n_ntiles) {
     constexpr int NW = WM * WN, NTH = 64 * NW;
-    using SCS = ScaleStager<BM, BN, NW, AM>;
+    using SCS = ScaleStager<F8 ? BM : 64, F8 ? BN : 64, NW, AM>;  // used by MXFP8 only
     constexpr int SCB = F8 ? SCS::BYTES : 0;
     static_assert(!F8 || (AKC && BKC && !WGRAD && BMODE == OP_SIMPLE && AM != OP_GEN),
                   "MXFP8: k-contiguous plain / spliced A, plain B");
