@@ -466,6 +466,7 @@ struct DenRun {
     h16 *out_grad;
     long long ldg;
     KfChainOpts opts;
+    int early;              // fetch the next frame's output row at frame start (KF_DEN_EARLY)
 };
 
 enum { DEN_ABI = 0, DEN_PRODUCT = 1 };
@@ -817,8 +818,17 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     const bool tr = r.trace && unit == 0 && gi == 0 && tid == 0;
 #define DEN_TP(i) \
     if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
+    // the next frame's output row is fetched at the start of each frame, so its latency
+    // hides under the arc phase (the first slices come from the LDS record cache, so the
+    // record loads' vmcnt waits do not queue behind it); KF_DEN_EARLY=0: after publish
+    const bool early = r.early != 0;
     for (int t = 0; t < Tmax; ++t) {
         DEN_TP(0);
+        if (early) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q)
+                if (t + 1 < Ts[q]) pre[q].fetch(nnet + (r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
+        }
         const int buf = (t + 1) & 1;
         float *blk = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
         float inv[NS], pq[NS];
@@ -858,9 +868,11 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         }
         den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, red, unit);
         DEN_TP(2);
+        if (!early) {
 #pragma unroll
-        for (int q = 0; q < NS; ++q)
-            if (t + 1 < Ts[q]) pre[q].fetch(nnet + (r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
+            for (int q = 0; q < NS; ++q)
+                if (t + 1 < Ts[q]) pre[q].fetch(nnet + (r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
+        }
         DEN_TP(3);
         if (!den_wait(X, unit, (unsigned)(G * (t + 1)), flag)) return;
         DEN_TP(4);
@@ -994,7 +1006,13 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
         }
     }
     __syncthreads();
+    const bool early = r.early != 0;  // as den_fwd_body
     for (int t = Tmax - 1, it = 0; t >= 0; --t, ++it) {
+        if (early) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q)
+                if (t < Ts[q] && t > 0) pre[q].fetch(nnet + (r0[q] + (long long)(t - 1) * r.stride) * r.ld, P);
+        }
         const int buf = t & 1;
         float *blk = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
         float inv[NS], pq[NS];
@@ -1033,9 +1051,11 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
             if (lane == 0) red[q * DEN_WAVES + wave] = w;
         }
         den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, red, unit);
+        if (!early) {
 #pragma unroll
-        for (int q = 0; q < NS; ++q)
-            if (live[q] && t > 0) pre[q].fetch(nnet + (r0[q] + (long long)(t - 1) * r.stride) * r.ld, P);
+            for (int q = 0; q < NS; ++q)
+                if (live[q] && t > 0) pre[q].fetch(nnet + (r0[q] + (long long)(t - 1) * r.stride) * r.ld, P);
+        }
         if (!den_wait(X, unit, (unsigned)(G * (it + 1)), flag)) return;
         float tb[NS];
 #pragma unroll
@@ -1378,6 +1398,11 @@ T *dev_upload(const std::vector<T> &v, std::vector<void *> &owned) {
     owned.push_back(p);
     if (!v.empty()) hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
     return (T *)p;
+}
+
+static int den_early() {
+    static const int v = getenv("KF_DEN_EARLY") ? atoi(getenv("KF_DEN_EARLY")) : 1;
+    return v;
 }
 
 struct DenTables {
