@@ -32,33 +32,51 @@ def test_attention_network_forward_backward(gpu, cfg, T):
     on = _oracle(xcfg, params, bns, feats)
     on.forward(feats.astype(np.float32), force_masks=masks)
     P = [dout for name, ty, din, dout in net.layers if name == "output"][0]
-    og = (np.random.default_rng(7).standard_normal((T, P)) * 0.05).astype(np.float16)
-    gbuf = kf.upload_fp16(og)
-    net.backward(gbuf.ptr)
-    got = net.read_grads()
-    on.backward(og.astype(np.float32))
-    ref = on.grads()
-    errs = {k: rel_fro(got[k], ref[k]) for k in ref}
     if cfg == "tiny_att.xconfig":
+        og = (np.random.default_rng(7).standard_normal((T, P)) * 0.05).astype(np.float16)
+        gbuf = kf.upload_fp16(og)
+        net.backward(gbuf.ptr)
+        got = net.read_grads()
+        on.backward(og.astype(np.float32))
+        ref = on.grads()
+        errs = {k: rel_fro(got[k], ref[k]) for k in ref}
         bad = {k: v for k, v in errs.items() if v > 5e-3}
         assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
         return
     # At full width (8 heads, key 64, value 128) the softmax backward w (dw - <w, dw>)
     # cancels, and fp16 rounding of its inputs moves the gradients at and below the layer
-    # by ~1e-2 in the oracle's own F mode against fp32 (scripts/att_precision.py). The
-    # bar is then: no further from the fp32 oracle than the F restatement is, x1.25.
+    # by ~1e-2 in the oracle's own F mode against fp32 (scripts/att_precision.py): the GPU
+    # and the F restatement are then two independent fp16 draws around the fp32 gradient,
+    # and their ratio of errors for one output gradient is noise (scripts/att_diag.py over
+    # seeds 7-12: geometric means 1.19, 0.87, 1.10, 0.84, 0.91, 0.68, per-parameter
+    # maxima up to 1.48). The bar is statistical: over three seeds the geometric mean of
+    # |gpu - fp32| / |F - fp32| over all parameters <= 1.15 (the GPU is on average no
+    # noisier than the fp16 restatement), each parameter <= max(5e-3, 1.6 F) and 3e-2.
     on.close()
-    on = oracle.OracleNet(xcfg, {k: synth.trunc_fp16(v) for k, v in params.items()}, bns,
-                          round_mode=oracle.ROUND_NONE, threads=16)
-    on.forward(feats.astype(np.float32), force_masks=masks)
-    on.backward(og.astype(np.float32))
-    f32 = on.grads()
-    bad = {}
-    for k in ref:
-        g_err, f_err = rel_fro(got[k], f32[k]), rel_fro(ref[k], f32[k])
-        if g_err > max(5e-3, 1.25 * f_err) or g_err > 3e-2:
-            bad[k] = (g_err, f_err)
+    logs, bad = [], {}
+    for seed in (7, 8, 9):
+        og = (np.random.default_rng(seed).standard_normal((T, P)) * 0.05).astype(np.float16)
+        gbuf = kf.upload_fp16(og)
+        net.forward(fbuf.ptr, T)
+        net.backward(gbuf.ptr)
+        got = net.read_grads()
+        grads = {}
+        for mode in (oracle.ROUND_FUSED, oracle.ROUND_NONE):
+            on = _oracle(xcfg, params, bns, feats, mode=mode)
+            on.forward(feats.astype(np.float32), force_masks=masks)
+            on.backward(og.astype(np.float32))
+            grads[mode] = on.grads()
+            on.close()
+        ref, f32 = grads[oracle.ROUND_FUSED], grads[oracle.ROUND_NONE]
+        for k in ref:
+            g_err, f_err = rel_fro(got[k], f32[k]), rel_fro(ref[k], f32[k])
+            if f_err > 0 and g_err > 0:
+                logs.append(np.log(g_err / f_err))
+            if g_err > max(5e-3, 1.6 * f_err) or g_err > 3e-2:
+                bad[(seed, k)] = (g_err, f_err)
+    gm = float(np.exp(np.mean(logs)))
     assert not bad, "grad errors vs fp32 (gpu, F): " + ", ".join(f"{k}={a:.2e}/{b:.2e}" for k, (a, b) in bad.items())
+    assert gm <= 1.15, f"GPU gradients noisier than the fp16 restatement: geometric-mean error ratio {gm:.3f}"
 
 
 def test_attention_import_key_scale(gpu):
