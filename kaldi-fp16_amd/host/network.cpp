@@ -1388,6 +1388,11 @@ extern "C" const void *nnet_debug_tensor(KfNet *net, const char *what, int layer
     if (w == "mask") return net->layers[layer].mask;
     if (w == "bn_scale") return net->layers[layer].bn_scale;
     if (w == "bn2_scale") return net->layers[layer].bn2_scale;
+    // the MXFP8 copy this layer's GEMM reads (e4m3 [T x pad128(in)], E8M0 [T x pad128(in)/32])
+    if (w == "x8q" || w == "x8s") {
+        const Mx *m = in8(net, net->layers[layer]);
+        return !m ? nullptr : w == "x8q" ? (const void *)m->q : (const void *)m->s;
+    }
     return nullptr;
 }
 static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {

@@ -491,7 +491,7 @@ int orc_net_forward(OrcNet *net, const float *features) {
             continue;
         }
         /* MXFP8 GEMM input of this layer (the producer's copy), or NULL = fp16 GEMM */
-        const float *x8 = MX && L->input >= 0 ? net->act8[L->input] : NULL;
+        const float *x8 = !MX ? NULL : L->input >= 0 ? net->act8[L->input] : L->input == -1 ? net->feat8 : NULL;
         float *wq = NULL, *wq2 = NULL;
 #define MX_OUT(buf, rows, cols) \
     do { if (MX && mx_producer(L)) net->act8[li] = mx_rows_new(buf, rows, cols); } while (0)

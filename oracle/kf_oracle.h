@@ -107,6 +107,9 @@ typedef struct {
     const float *ivec;
     int B, ivec_dim;
     const int *seq_off;
+    /* MXFP8 copy of the features (dequantised, [T x feat_dim]) for a layer reading the
+     * input directly: lets a test run one layer on the GPU's own fp8 input (mx8 only) */
+    const float *feat8;
 } OrcNet;
 
 /* OCP MXFP8 quantise-dequantise of rows of `cols` (cols % 32 == 0) values:

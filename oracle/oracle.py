@@ -106,7 +106,7 @@ class OrcNet(C.Structure):
                 ("gW2", C.POINTER(_fp)), ("gb2", C.POINTER(_fp)), ("gact", C.POINTER(_fp)),
                 ("force_mask", C.POINTER(C.POINTER(C.c_uint8))), ("mx8", C.c_int),
                 ("act8", C.POINTER(_fp)), ("ivec", _fp), ("B", C.c_int), ("ivec_dim", C.c_int),
-                ("seq_off", C.POINTER(C.c_int))]
+                ("seq_off", C.POINTER(C.c_int)), ("feat8", _fp)]
 
 
 def parse_xconfig(text: str):
@@ -290,9 +290,12 @@ class OracleNet:
         m, v, g, b = spec
         return OrcBN(self._p(m), self._p(v), self._p(g), self._p(b), 1e-3, target_rms)
 
-    def forward(self, features: np.ndarray, force_masks: dict = None, ivectors=None, seq_off=None):
+    def forward(self, features: np.ndarray, force_masks: dict = None, ivectors=None, seq_off=None,
+                features8: np.ndarray = None):
         """force_masks: layer name -> uint8 ReLU decisions to replay (see kf_oracle.h).
-        ivectors [B x dim] and seq_off int[B+1]: the ivector input (ReplaceIndex rows)."""
+        ivectors [B x dim] and seq_off int[B+1]: the ivector input (ReplaceIndex rows).
+        features8: the features' dequantised MXFP8 copy, the GEMM input of a layer reading
+        the input directly when mx8 is on (one-layer tests on the GPU's own fp8 input)."""
         x = np.ascontiguousarray(features, dtype=np.float32)
         fm = None
         if force_masks:
@@ -321,6 +324,11 @@ class OracleNet:
             self.net.seq_off = so.ctypes.data_as(C.POINTER(C.c_int))
         if fm is not None:
             self.net.force_mask = fm
+        if features8 is not None:
+            f8 = np.ascontiguousarray(features8, dtype=np.float32)
+            assert f8.shape == x.shape
+            self.keep.append(f8)
+            self.net.feat8 = f8.ctypes.data_as(_fp)
         rc = lib().orc_net_forward(C.byref(self.net), x.ctypes.data)
         assert rc == 0
 
