@@ -67,6 +67,7 @@ def parse(argv=None):
                    help="skip the configs[0]/[1]/[4] sub-results at N = 1")
     p.add_argument("--extra-steps", type=int, default=5)
     p.add_argument("--cpu-frames", type=int, default=1500)
+    p.add_argument("--gt-frames", type=int, default=48, help="frames of the gotorch-style float64 CPU leg")
     p.add_argument("--cpu-threads", type=int, default=0, help="0: every host core")
     p.add_argument("--no-prof", action="store_true")
     p.add_argument("--fp8", action="store_true",
@@ -167,10 +168,14 @@ def roofline(prof, steps, peak_tflops):
     return r
 
 
-def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
-    """The C oracle (a restatement of the reference's CNN-TDNN math and chain objective,
-    not the Go code: no Go toolchain here) timed on host cores: forward, objective on
-    the subsampled frames, backward."""
+def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst, gt_frames=48):
+    """The CPU baseline: the network in the reference's Go CPU
+    style — oracle/gotorch_net.c, float64, AffineLayer / TDNNLayer / Conv1DLayer loop
+    forms, forward GEMMs over `threads` as matmulParallel, SGD with momentum — timed
+    on a bounded sample (forward, backward from a fixed output gradient, SGD; gotorch has
+    no chain loss). Beside it, the C oracle's fp32 train step (forward, chain objective
+    on the subsampled frames, backward) on a full 1500-frame eg. Restatements, not Go:
+    no Go toolchain here."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from kfp16 import synth
@@ -180,12 +185,36 @@ def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
     except Exception:
         oracle.lib()
     tp = {k: synth.trunc_fp16(v) for k, v in params.items()}
+    D = ivector_input(xcfg)
+    name = "cnn_tdnn_17f with the ivector front end" if D else "cnn_tdnn_17f"
+    res = {"unit": "frames/sec", "cores": threads, "host_cores": host_cores(), "kind": "port"}
+    # gotorch-style float64 leg (the template has no ivector branch)
+    if not D:
+        on = oracle.OracleNet(xcfg, tp, bns, round_mode=oracle.ROUND_NONE, threads=threads)
+        gt = oracle.GotorchNet(on, workers=threads)
+        feats = synth.make_features(gt_frames, 40).astype(np.float64)
+        og = np.random.default_rng(5).standard_normal((gt_frames, on.L[on.chain_output()]["out_dim"])) * 0.01
+        t0 = time.perf_counter()
+        gt.forward(feats)
+        t_fwd = time.perf_counter() - t0
+        gt.backward(og)
+        gt.sgd(1e-8)
+        dt = time.perf_counter() - t0
+        gt.close()
+        on.close()
+        res.update({"value": round(gt_frames / dt, 3), "forward_frames_per_sec": round(gt_frames / t_fwd, 3),
+                    "sample": f"restatement, not Go: {name} in go/gotorch's CPU style (oracle/gotorch_net.c: "
+                              f"float64; TDNN-F halves as TDNNLayer and conv as Conv1DLayer loops, "
+                              f"single-threaded as in layers.go:443-522 / cnn_tdnn.go:85-172; affine forward "
+                              f"GEMMs as matmulParallel over {threads} threads, ops.go:49-81; SGD momentum "
+                              f"0.9) on {gt_frames} frames: forward, backward from a fixed output gradient, "
+                              f"SGD, {dt:.1f} s (forward {t_fwd:.1f} s)"})
+    # the fp32 C oracle's train step with the chain objective, on one full eg
     on = oracle.OracleNet(xcfg, tp, bns, round_mode=oracle.ROUND_FUSED, threads=threads)
     feats = synth.make_features(frames, 40).astype(np.float32)
     g, init = den
     row0, nfr, stride = synth.chain_layout(1, frames)
     rows = row0[0] + np.arange(nfr[0]) * stride
-    D = ivector_input(xcfg)
     iv = (np.random.default_rng(5).standard_normal((1, D)) * 2).astype(np.float32) if D else None
     t0 = time.perf_counter()
     if D:
@@ -200,14 +229,15 @@ def cpu_baseline(xcfg, params, bns, frames, threads, den, num_fst):
     on.backward(og)
     dt = time.perf_counter() - t0
     on.close()
-    name = "cnn_tdnn_17f with the ivector front end" if D else "cnn_tdnn_17f"
-    return {"value": round(frames / dt, 2), "unit": "frames/sec", "cores": threads, "host_cores": host_cores(),
-            "forward_frames_per_sec": round(frames / t_fwd, 2),
-            "kind": "port",
+    fp32 = {"value": round(frames / dt, 2), "forward_frames_per_sec": round(frames / t_fwd, 2),
             "sample": f"restatement, not Go: C oracle train step (fwd, chain objective, bwd) of {name} on "
-                      f"{frames} frames (1 eg), fp32 math (SURVEY 8d: gotorch-style float32/float64 layers), "
-                      f"GEMM rows split over {threads} threads (go/gotorch/ops.go:49-81 policy), {dt:.1f} s; "
+                      f"{frames} frames (1 eg), fp32, GEMM rows split over {threads} threads, {dt:.1f} s; "
                       f"forward alone {t_fwd:.1f} s"}
+    if "value" in res:
+        res["oracle_fp32"] = fp32
+    else:
+        res.update(fp32)
+    return res
 
 
 def config1_affine(threads, reps=50):
@@ -501,7 +531,7 @@ def main():
             xcfg, params, bns, den_g, P = ctx
             den = (den_g, oracle.den_initial_probs(den_g))
             out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, threads,
-                                               den, synth.make_num_fst(0, num_pdfs=P))
+                                               den, synth.make_num_fst(0, num_pdfs=P), a.gt_frames)
         if extra:
             out["sub_results"] = extra
         print(json.dumps(out), flush=True)

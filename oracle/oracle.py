@@ -55,6 +55,14 @@ def lib(native: bool = False):
         _lib.gt_matmul.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]
         _lib.gt_affine_forward.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                            C.c_void_p, C.c_void_p, C.c_int]
+        _lib.gt_net_create.restype = C.c_void_p
+        _lib.gt_net_create.argtypes = [C.c_void_p, C.c_int]
+        _lib.gt_net_free.argtypes = [C.c_void_p]
+        _lib.gt_net_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        _lib.gt_net_backward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        _lib.gt_net_sgd.argtypes = [C.c_void_p, C.c_double, C.c_double]
+        _lib.gt_net_tensor.restype = C.POINTER(C.c_double)
+        _lib.gt_net_tensor.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_longlong)]
     return _lib
 
 
@@ -398,6 +406,64 @@ class OracleNet:
         if self.net is not None:
             lib().orc_net_free(C.byref(self.net))
             self.net = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class GotorchNet:
+    """The network in the reference's Go CPU style (oracle/gotorch_net.c):
+    float64, AffineLayer / TDNNLayer / Conv1DLayer loop forms, matmulParallel forward
+    GEMMs over `workers` threads, SGD with momentum. Built from an OracleNet's layer
+    descriptors and parameters (fp32 values widened to float64)."""
+
+    def __init__(self, onet: "OracleNet", workers: int = 1):
+        self.o = onet
+        self.workers = int(workers)
+        self.h = lib().gt_net_create(C.cast(onet.arr, C.c_void_p), len(onet.L))
+        if not self.h:
+            raise ValueError("gotorch template: unsupported layer (attention / combine / ivector branch)")
+
+    def forward(self, features: np.ndarray):
+        self.x = np.ascontiguousarray(features, dtype=np.float64)
+        assert lib().gt_net_forward(self.h, self.x.ctypes.data, self.x.shape[0], self.workers) == 0
+
+    def _t(self, name, which):
+        n = C.c_longlong(0)
+        p = lib().gt_net_tensor(self.h, self.o.index[name], which, C.byref(n))
+        return None if not p else np.ctypeslib.as_array(p, shape=(n.value,)).copy()
+
+    def act(self, name):
+        return self._t(name, 0).reshape(self.x.shape[0], -1)
+
+    def backward(self, out_grad: np.ndarray):
+        g = np.ascontiguousarray(out_grad, dtype=np.float64)
+        assert lib().gt_net_backward(self.h, self.x.ctypes.data, g.ctypes.data, self.o.chain_output()) == 0
+
+    def sgd(self, lr, momentum=0.9):
+        lib().gt_net_sgd(self.h, lr, momentum)
+
+    def grads(self) -> dict:
+        """flat float64 gradients under the product's parameter names (OracleNet.grads())"""
+        out = {}
+        for L in self.o.L:
+            n, k = L["name"], L["kind"]
+            names = {"conv-relu-batchnorm-layer": [(".W", 1), (".Bias", 2)],
+                     "tdnnf-layer": [(".LinearW", 1), (".AffineW", 3), (".AffineBias", 4)],
+                     "linear-component": [(".W", 1)],
+                     "prefinal-layer": [(".BigW", 1), (".BigBias", 2), (".SmallW", 3)],
+                     "output-layer": [(".W", 1), (".Bias", 2)]}.get(k, [])
+            for suf, which in names:
+                out[n + suf] = self._t(n, which)
+        return out
+
+    def close(self):
+        if self.h:
+            lib().gt_net_free(self.h)
+            self.h = None
 
     def __del__(self):
         try:
