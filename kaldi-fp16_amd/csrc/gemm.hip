@@ -46,6 +46,11 @@ struct WgradArgs {
     float *slab;        // [splits][M][N] fp32 partials
     float *bias_slab;   // [splits][N] fp32 column sums of B, or nullptr
     int k_per_split;    // multiple of BK
+    // > 0: A has two time-shifted parts of one source and part p's M tile j covers the
+    // same source columns as tile pair_ps * p + j (N fits one tile). Each XCD then gets
+    // whole (column chunk, split) pairs, so the two parts' reads of the same source rows
+    // meet in one L2 instead of two
+    int pair_ps;
 };
 
 template <int BM, int BN, int ST, int SCB = 0>
@@ -306,11 +311,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
         const int q = ntiles / 8, rmd = ntiles % 8, xcd = tile % 8, loc = tile / 8;
         tile = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + loc;
     }
+    int split = blockIdx.y;
+    if constexpr (WGRAD) {
+        if (G.pair_ps > 0) {
+            const int total = gridDim.x * gridDim.y, L = blockIdx.x + blockIdx.y * gridDim.x;
+            const int q = total / 8, rmd = total % 8, xcd = L % 8, loc = L / 8;
+            const int w = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + loc;
+            const int unit = w >> 1, chunk = unit / gridDim.y;
+            split = unit - chunk * gridDim.y;
+            tile = (w & 1) * G.pair_ps + chunk;  // n_ntiles == 1
+        }
+    }
     const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
     const int m0 = mt * BM, n0 = nt * BN;
     int kbeg = 0, kend = K;
     if constexpr (WGRAD) {
-        kbeg = blockIdx.y * G.k_per_split;
+        kbeg = split * G.k_per_split;
         kend = min(K, kbeg + G.k_per_split);
     }
     const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
@@ -412,7 +428,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     }
 
     if constexpr (WGRAD) {
-        float *slab = G.slab + (long long)blockIdx.y * M * N;
+        float *slab = G.slab + (long long)split * M * N;
         static_for<TM>([&](auto I) {
             static_for<TN>([&](auto J) {
                 const int n = n0 + wn * WTN + J * 16 + (lane & 15);
@@ -423,7 +439,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
             });
         });
         if (do_bsum && tid < BN && n0 + tid < N)
-            G.bias_slab[(long long)blockIdx.y * N + n0 + tid] = bsum;
+            G.bias_slab[(long long)split * N + n0 + tid] = bsum;
     } else {
         fused_epilogue<BM, BN, WM, WN>(acc, smem, E, M, N, m0, n0, tid, lane, wave);
     }
@@ -1120,7 +1136,7 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         kf_set_error("kf_gemm_fused: out8 needs N and ldo8 multiples of 32 and scale8");
         return -1;
     }
-    WgradArgs G{nullptr, nullptr, 0};
+    WgradArgs G{nullptr, nullptr, 0, 0};
     const int am = op_mode(a), bm = op_mode(b);
     const bool f8 = A->fmt == KF_FMT_MXFP8;
     if (f8 != (B->fmt == KF_FMT_MXFP8)) {
@@ -1276,9 +1292,14 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         return -1;
     }
     WgradArgs G{(float *)ws,
-                bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255)) : nullptr, kps};
+                bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255)) : nullptr, kps, 0};
     KfEpilogue E{};
     const int am = op_mode(a), bm = op_mode(b);
+    // the TDNN-F linear's [x(t - s) | x(t)]: pair the parts' tiles per XCD (KF_WG_PAIR=0: off)
+    static const int wpair = getenv("KF_WG_PAIR") ? atoi(getenv("KF_WG_PAIR")) : 1;
+    if (wpair && am == OP_P2 && A->nparts == 2 && N <= BNc && A->part_width % BMc == 0 &&
+        M == 2 * A->part_width)
+        G.pair_ps = A->part_width / BMc;
     int rc;
 #define KF_WG(AM_, BM_)                                                                          \
     do {                                                                                         \
