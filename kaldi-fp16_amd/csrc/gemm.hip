@@ -320,6 +320,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
             const int unit = w >> 1, chunk = unit / gridDim.y;
             split = unit - chunk * gridDim.y;
             tile = (w & 1) * G.pair_ps + chunk;  // n_ntiles == 1
+        } else if (G.pair_ps < 0) {  // split-major: the tiles of one split share an XCD
+            const int total = gridDim.x * gridDim.y, L = blockIdx.x + blockIdx.y * gridDim.x;
+            const int q = total / 8, rmd = total % 8, xcd = L % 8, loc = L / 8;
+            const int w = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + loc;
+            split = w / gridDim.x;
+            tile = w - split * gridDim.x;
         }
     }
     const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
@@ -1300,6 +1306,8 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     if (wpair && am == OP_P2 && A->nparts == 2 && N <= BNc && A->part_width % BMc == 0 &&
         M == 2 * A->part_width)
         G.pair_ps = A->part_width / BMc;
+    static const int wsm = getenv("KF_WG_SPLITMAJOR") ? atoi(getenv("KF_WG_SPLITMAJOR")) : 0;
+    if (wsm && G.pair_ps == 0) G.pair_ps = -1;
     int rc;
 #define KF_WG(AM_, BM_)                                                                          \
     do {                                                                                         \
