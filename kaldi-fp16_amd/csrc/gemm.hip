@@ -1263,7 +1263,7 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     static const int wbig = getenv("KF_GEMM_WBIG") ? atoi(getenv("KF_GEMM_WBIG")) : 1;
     static const int w160 = getenv("KF_GEMM_W160") ? atoi(getenv("KF_GEMM_W160")) : 1;
     int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
-    if (BNc == 160 && w160) BMc = 384;
+    if (BNc == 160 && w160) BMc = w160 == 2 ? 192 : 384;  // 2: 8-wave 192 x 160 (half the splits)
     if (BNc == 64) BMc = 256;
     if (wbig && BNc == 128) BMc = 256, BNc = N > 128 ? 256 : 128;
     // tile rows: the candidate wasting the fewest padded rows of M (ties: the larger)
@@ -1323,6 +1323,8 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
             rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BMc == 256 && BNc == 128)                                                       \
             rc = launch<256, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 192 && BNc == 160)                                                       \
+            rc = launch<192, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BMc == 384 && BNc == 160)                                                       \
             rc = launch<384, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 160)                                                                     \
