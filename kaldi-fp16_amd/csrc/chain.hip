@@ -554,7 +554,7 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 }
 
 struct DenX {
-    float *buf;     // [nseq][2][G][blk]; blk = ns*spg*64 + 64 (tail: lane s = partial sum of s)
+    float *buf;     // [nseq][2][G][blk]; blk = ns*spg*64 + 64 (tail: [q * DEN_WAVES + wave] = that wave's partial sum of sequence q)
     unsigned *cnt;  // [nseq] arrivals (zeroed before each launch)
     unsigned *tmo;  // per-launch timeout word (zeroed before each launch)
     unsigned *sticky;  // timed-out blocks since the last read (never zeroed by a launch)
@@ -575,22 +575,19 @@ __device__ __forceinline__ void den_map(const DenX &X, int &seq, int &gi) {
     gi = w & (X.G - 1);
 }
 
-// publish: the payload's sc1 stores are drained by every wave; wave 0 stores the
-// tail {psum of each of the NS sequences} and one lane adds the arrival
+// publish: every wave stores its partial sums of the NS sequences (lane 0, tail slot
+// q * DEN_WAVES + wave) beside its payload, all sc1; every wave drains vmcnt, the
+// workgroup barriers, one lane adds the arrival (one store drain per frame)
 template <int NS>
-__device__ __forceinline__ void den_publish(const DenX &X, float *tail, const float *red, int unit) {
-    const int tid = threadIdx.x, lane = tid & 63;
+__device__ __forceinline__ void den_publish(const DenX &X, float *tail, const float (&wsum)[NS], int unit) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) st_sc1(tail + q * DEN_WAVES + wave, wsum[q]);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid < 64) {
-        float ps = 0.f;
-        const int s = lane < NS ? lane : 0;
-#pragma unroll
-        for (int w2 = 0; w2 < DEN_WAVES; ++w2) ps += red[s * DEN_WAVES + w2];
-        st_sc1(tail + lane, lane < NS ? ps : 0.0f);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[unit], 1u, RLX_AGENT);
-    }
+    if (tid == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[unit], 1u, RLX_AGENT);
 }
 // wait for `target` arrivals (one lane polls); false on timeout, uniform
 __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target, int *lds_flag) {
@@ -616,28 +613,27 @@ __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     return *lds_flag != 0;
 }
-// the G partial sums of sequence s in buffer `buf`, in block order (every lane: same value)
-__device__ __forceinline__ float den_gather_psum(const DenX &X, int unit, int buf, int s) {
-    const int lane = threadIdx.x & 63;
-    float v = 0.0f;
-    if (lane < X.G)
-        v = ld_sc1(X.buf + (((size_t)unit * 2 + buf) * X.G + lane) * X.blk + X.ns * X.spg * 64 + s);
-    float sum = 0.0f;
-    for (int g2 = 0; g2 < X.G; ++g2) sum += __shfl(v, g2, 64);
-    return sum;
-}
 // all exchanged slices of buffer `buf` for the NS sequences, scattered to their
-// states: f(s, state, value, initp, owner, slot); all loads in flight at once
-template <int NS, class F>
+// states: first sum(q, total of the G x DEN_WAVES partial sums, fixed order, equal in
+// every lane), then f(q, state, value, initp, owner, slot) per slot. The partial sums
+// load with the first sequence's slices, so one round trip serves both.
+template <int NS, class FS, class F>
 __device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, int nsl,
-                                            const int *perm, const float *initp, F f) {
+                                            const int *perm, const float *initp, FS sum, F f) {
     int tid = threadIdx.x;
     // opaque to the optimiser: the per-slot addresses below are rebuilt every frame
     // instead of being hoisted out of the frame loop as 64-bit values (16 of them
     // for NS = 2 spill at the 128-VGPR budget of a 1024-thread block)
     asm volatile("" : "+v"(tid));
-    const int n = nsl * 64;
+    const int n = nsl * 64, lane = tid & 63;
     const float *xb = X.buf + ((size_t)unit * 2 + buf) * X.G * X.blk;
+    float pv[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        pv[q] = 0.0f;
+        for (int i = lane; i < X.G * DEN_WAVES; i += 64)
+            pv[q] += ld_sc1(xb + (size_t)(i / DEN_WAVES) * X.blk + X.ns * X.spg * 64 + q * DEN_WAVES + i % DEN_WAVES);
+    }
 #pragma unroll
     for (int q = 0; q < NS; ++q) {  // one sequence at a time: DEN_MAXS values live
         float v[DEN_MAXS];
@@ -647,6 +643,7 @@ __device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, in
             v[m] = ld_sc1(xb + (size_t)(j & (X.G - 1)) * X.blk + (size_t)q * X.spg * 64 +
                           (j >> X.lgG) * 64 + (c & 63));
         }
+        sum(q, wave_sum(pv[q]));
 #pragma unroll
         for (int m = 0; m < DEN_MAXS; ++m) {
             const int c = tid + m * DEN_THREADS;
@@ -861,12 +858,10 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
             }
         }
         DEN_TP(1);
+        float wsum[NS];
 #pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            const float w = wave_sum(pq[q]);
-            if (lane == 0) red[q * DEN_WAVES + wave] = w;
-        }
-        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, red, unit);
+        for (int q = 0; q < NS; ++q) wsum[q] = wave_sum(pq[q]);
+        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, wsum, unit);
         DEN_TP(2);
         if (!early) {
 #pragma unroll
@@ -877,10 +872,8 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         if (!den_wait(X, unit, (unsigned)(G * (t + 1)), flag)) return;
         DEN_TP(4);
         float as1[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) as1[q] = den_gather_psum(X, unit, buf, q);
         DEN_TP(5);
-        den_consume<NS>(X, unit, buf, nsl, F.perm, F.initp,
+        den_consume<NS>(X, unit, buf, nsl, F.perm, F.initp, [&](int q, float v) { as1[q] = v; },
                         [&](int q, int st, float v, float ip, int owner, int c) {
                             if (!live[q]) return;
                             const float a = v + as1[q] * leaky * ip;
@@ -1045,12 +1038,10 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
                 pq[q] += ipj * bd;
             }
         }
+        float wsum[NS];
 #pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            const float w = wave_sum(pq[q]);
-            if (lane == 0) red[q * DEN_WAVES + wave] = w;
-        }
-        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, red, unit);
+        for (int q = 0; q < NS; ++q) wsum[q] = wave_sum(pq[q]);
+        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, wsum, unit);
         if (!early) {
 #pragma unroll
             for (int q = 0; q < NS; ++q)
@@ -1058,12 +1049,11 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
         }
         if (!den_wait(X, unit, (unsigned)(G * (it + 1)), flag)) return;
         float tb[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            if (live[q]) nrm[q] = den_gather_psum(X, unit, buf, q);  // <init, beta'[t]>: next factor
-            tb[q] = leaky * nrm[q];
-        }
         den_consume<NS>(X, unit, buf, nsl, B.perm, B.initp,
+                        [&](int q, float v) {
+                            if (live[q]) nrm[q] = v;  // <init, beta'[t]>: the next factor
+                            tb[q] = leaky * nrm[q];
+                        },
                         [&](int q, int st, float v, float, int owner, int c) {
                             if (!live[q]) return;
                             const float b = v + tb[q];
