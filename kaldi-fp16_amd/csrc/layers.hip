@@ -73,33 +73,52 @@ __global__ __launch_bounds__(256) void k_conv_c1_fwd(ConvC1 c, const h16 *x, con
         sf[e] = scale ? shift[8 * g + e] : 0.f;
     }
     const int total = c.T * c.hout * groups;  // < 2^31, checked on the host
-    for (int it = first; it < total; it += gridDim.x * blockDim.x) {
-        const int row = it / groups;
-        const int t = row / c.hout, h = row - t * c.hout;
-        float v[8];
+    // U items per thread per iteration: their 9 x U tap loads are in flight together
+    // (one item per iteration left the kernel latency-bound at ~1.3 TB/s)
+    constexpr int U = 4;
+    const int stride = gridDim.x * blockDim.x;
+    for (int it0 = first; it0 < total; it0 += U * stride) {
+        float xv[U][9];
+        int rowu[U];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = b[e];
+        for (int u = 0; u < U; ++u) {
+            const int it = it0 + u * stride;
+            const int row = (it < total ? it : first) / groups;  // dead items: any valid row
+            rowu[u] = row;
+            const int t = row / c.hout, h = row - t * c.hout;
 #pragma unroll
-        for (int o = 0; o < 9; ++o) {
-            const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
-            const bool ok = o < c.noff && ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin;
-            const float xv = ok ? h2f(x[ok ? ts * c.hin + hs : 0]) : 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaf(xv, w[o][e], v[e]);
+            for (int o = 0; o < 9; ++o) {
+                const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
+                const bool ok = o < c.noff && ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin;
+                const float v = h2f(x[ok ? ts * c.hin + hs : 0]);
+                xv[u][o] = ok ? v : 0.f;
+            }
         }
-        unsigned bits = 0;
-        half8 out;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float a = v[e];
-            if (a > 0.f) bits |= 1u << e;
-            else a = 0.f;
-            if (scale) a = fmaf(a, sc[e], sf[e]);
-            out[e] = f2h(a);
+        for (int u = 0; u < U; ++u) {
+            const int it = it0 + u * stride;
+            if (it >= total) break;
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = b[e];
+#pragma unroll
+            for (int o = 0; o < 9; ++o)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = fmaf(xv[u][o], w[o][e], v[e]);
+            unsigned bits = 0;
+            half8 out;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float a = v[e];
+                if (a > 0.f) bits |= 1u << e;
+                else a = 0.f;
+                if (scale) a = fmaf(a, sc[e], sf[e]);
+                out[e] = f2h(a);
+            }
+            const long long idx = (long long)rowu[u] * c.fout + 8 * g;
+            store_h8(y + idx, out);
+            if (mask) mask[idx >> 3] = (uint8_t)bits;  // (a dword per 4 lanes via shuffles: slower)
         }
-        const long long idx = (long long)row * c.fout + 8 * g;
-        store_h8(y + idx, out);
-        if (mask) mask[idx >> 3] = (uint8_t)bits;
     }
 }
 
