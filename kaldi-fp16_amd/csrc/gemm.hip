@@ -167,10 +167,31 @@ __device__ __forceinline__ int mx_exponent(float amax) {
 // consecutive columns of a row (16-byte global I/O). `smem` must hold
 // 4*BN + 32*(BN/WN + 4)*WM*WN floats; every LDS-DMA into it must have landed.
 // ---------------------------------------------------------------------------
+// the epilogue's per-column parameters of column n0 + tid, loaded before the K loop so
+// their latency hides under it (KF_EPI_EARLY=0: loaded in the epilogue)
+struct EpiPre {
+    float b, s, sh, s2;
+};
+template <int BN, int NTH>
+__device__ __forceinline__ EpiPre epi_params(const KfEpilogue &E, int N, int n0, int tid) {
+    static_assert(BN <= NTH, "one column per thread");
+    EpiPre p{0.f, 0.f, 0.f, 1.f};
+    const int n = n0 + tid;
+    if (tid < BN && n < N) {
+        if (E.bias) p.b = (float)((const h16 *)E.bias)[n];
+        if (E.scale) {
+            p.s = E.scale[n];
+            p.sh = E.shift[n];
+        }
+        if (E.scale2) p.s2 = E.scale2[n];
+    }
+    return p;
+}
+
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN / WN / 16], char *smem,
                                                const KfEpilogue &E, int M, int N, int m0, int n0,
-                                               int tid, int lane, int wave) {
+                                               int tid, int lane, int wave, const EpiPre *pre = nullptr) {
     constexpr int NW = WM * WN, NTH = 64 * NW;
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -178,13 +199,14 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
     wait_vmcnt<0>();
     __syncthreads();
     float *prm = reinterpret_cast<float *>(smem);
-    for (int c = tid; c < BN; c += NTH) {
-        const int n = n0 + c;
-        const bool in = n < N;
-        prm[c] = (E.bias && in) ? (float)((const h16 *)E.bias)[n] : 0.f;
-        prm[BN + c] = (E.scale && in) ? E.scale[n] : 0.f;
-        prm[2 * BN + c] = (E.scale && in) ? E.shift[n] : 0.f;
-        prm[3 * BN + c] = (E.scale2 && in) ? E.scale2[n] : 1.f;
+    {
+        const EpiPre p = pre ? *pre : epi_params<BN, NTH>(E, N, n0, tid);
+        if (tid < BN) {
+            prm[tid] = p.b;
+            prm[BN + tid] = p.s;
+            prm[2 * BN + tid] = p.sh;
+            prm[3 * BN + tid] = p.s2;
+        }
     }
     __syncthreads();
     const EpiCols P{prm, prm + BN, prm + 2 * BN, prm + 3 * BN};
@@ -368,6 +390,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     // the counted wait retires only stage kt (never vmcnt(0) in steady state)
     // (plain statements: a lambda around `issue` makes the stager's offset arrays
     // address-taken and sends them to scratch)
+    EpiPre epre{0.f, 0.f, 0.f, 1.f};
+    if constexpr (!WGRAD) epre = epi_params<BN, 64 * NW>(E, N, n0, tid);
     if (nk > 0) issue(0, kbeg);
     if (ST >= 3 && nk > 1) issue(1, kbeg + BK);
     if (ST >= 4 && nk > 2) issue(2, kbeg + 2 * BK);
@@ -447,7 +471,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
         if (do_bsum && tid < BN && n0 + tid < N)
             G.bias_slab[(long long)split * N + n0 + tid] = bsum;
     } else {
-        fused_epilogue<BM, BN, WM, WN>(acc, smem, E, M, N, m0, n0, tid, lane, wave);
+        fused_epilogue<BM, BN, WM, WN>(acc, smem, E, M, N, m0, n0, tid, lane, wave, &epre);
     }
 }
 
@@ -483,6 +507,7 @@ struct HaloArgs {
     int nbuf;               // halo images (2 when nch > 1)
     int ctap[KF_MAX_PARTS];
     int bshift[KF_MAX_PARTS];  // BROW: row shift of tap p's weight block (op_wrows)
+    unsigned long long *trace;  // diagnostics (kf_halo_trace): block 300 wave 0 stamps, else null
 };
 
 // s_waitcnt vmcnt(n) for a wave-uniform run-time n <= 15
@@ -598,6 +623,11 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         const int q0 = ps * H.slice, q1 = min(H.npieces, q0 + H.slice);
         return q1 - q0 > wave ? (q1 - q0 - wave + NW - 1) / NW : 0;
     };
+    const bool tr = H.trace && blockIdx.x == 300 && tid == 0;
+#define HALO_TP(slot) \
+    if (tr && (slot) < 128) H.trace[slot] = wall_clock64();
+    HALO_TP(0);
+    const EpiPre epre = epi_params<BN, 64 * NW>(E, N, n0, tid);
     halo_issue(0, 0, 0, H.npieces);
     static_for<ST - 1>([&](auto I) {
         constexpr int i = decltype(I)::value;
@@ -620,6 +650,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        HALO_TP(1 + 2 * st);
         if (H.nbuf == 1 && c > 0 && p == 0) {
             // one halo image (two do not fit beside the B ring): every wave is past the
             // previous chunk's last fragment reads, so reload it in place and wait
@@ -661,8 +692,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
             });
         });
         __builtin_amdgcn_sched_barrier(0);
+        HALO_TP(2 + 2 * st);
     }
-    fused_epilogue<BM, BN, WM, WN>(acc, dsm, E, M, N, m0, n0, tid, lane, wave);
+    HALO_TP(126);
+    fused_epilogue<BM, BN, WM, WN>(acc, dsm, E, M, N, m0, n0, tid, lane, wave, &epre);
+    HALO_TP(127);
+#undef HALO_TP
 }
 
 // split-K reduction: dst[m][n] (+)= sum_s slab[s][m][n], summed in split order (the
@@ -970,9 +1005,19 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
 // 1 when launched, 0 when not applicable (the caller runs the im2col GEMM), -1 on error.
 // KF_CONV_HALO=0 disables it (A/B).
 // ---------------------------------------------------------------------------
+static unsigned long long *g_halo_trace = nullptr;
+static int g_halo_trace_at = -1, g_halo_launches = 0;
+// diagnostics: stamp block 300 of the conv-halo launch number `at` (counted from this call)
+extern "C" void kf_halo_trace(unsigned long long *buf, int at) {
+    g_halo_trace = buf;
+    g_halo_trace_at = at;
+    g_halo_launches = 0;
+}
 template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW, int ST>
-static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const HaloArgs &H, size_t lds) {
+static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const HaloArgs &H0, size_t lds) {
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
+    HaloArgs H = H0;
+    H.trace = g_halo_trace && g_halo_launches++ == g_halo_trace_at ? g_halo_trace : nullptr;
     ProfRec rec{};
     if (g_prof) {
         rec.a = prof_event();
