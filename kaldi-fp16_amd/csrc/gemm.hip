@@ -1134,8 +1134,12 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
                 lds = lds4;
             }
         }
+        // KF_HALO_W2=1: 64-column tiles on two 128x64-tile waves (more MACs per LDS byte)
+        static const int w2 = getenv("KF_HALO_W2") ? atoi(getenv("KF_HALO_W2")) : 0;
 #define KF_HALO(BKC_, BMODE_, BROW_)                                                                     \
         do {                                                                                      \
+            if (BN_ == 64 && BM_ == 256 && w2)                                                    \
+                return launch_halo<256, 64, 2, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds);   \
             if (BN_ == 64)                                                                        \
                 return BM_ == 128 ? launch_halo<128, 64, 4, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds)  \
                        : ST_ == 4 ? launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_, 4>(M, N, bp, E, H, lds)  \
