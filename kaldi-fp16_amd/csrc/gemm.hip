@@ -704,14 +704,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
 // result does not depend on the launch shape). Each thread owns 4 consecutive columns
 // and keeps 8 slab loads in flight; the scalar form (one dependent load chain per
 // element) ran at ~1.2 TB/s.
-__global__ __launch_bounds__(256) void k_slab_reduce(const float *slab, int splits, int M, int N,
-                                                     float *dst, long long ldw, int accumulate) {
+__device__ __forceinline__ void slab_reduce_body(const float *slab, int splits, int M, int N, float *dst,
+                                                 long long ldw, int accumulate, int bid, int nblk) {
     const long long total = (long long)M * N;
-    const long long step = (long long)gridDim.x * blockDim.x;
+    const long long step = (long long)nblk * blockDim.x;
     if ((N & 3) == 0) {
         const long long t4 = total >> 2;
         const float4v *s4 = reinterpret_cast<const float4v *>(slab);
-        for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < t4; i += step) {
+        for (long long i = (long long)bid * blockDim.x + threadIdx.x; i < t4; i += step) {
             float4v acc = {0.f, 0.f, 0.f, 0.f};
             int k = 0;
             for (; k + 8 <= splits; k += 8) {
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float *slab, int spli
         }
         return;
     }
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += step) {
+    for (long long i = (long long)bid * blockDim.x + threadIdx.x; i < total; i += step) {
         float s = 0.f;
         for (int k = 0; k < splits; ++k) s += slab[k * total + i];
         const long long m = i / N, n = i - m * N;
@@ -740,10 +740,10 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float *slab, int spli
 
 // bias column sums over the splits: 4 waves split the slabs of 64 columns, fixed-order
 // combine (the one-thread-per-column form was latency bound: 27 us for 86 splits)
-__global__ __launch_bounds__(256) void k_slab_reduce_cols(const float *slab, int splits, int N,
-                                                          float *dst, int accumulate) {
+__device__ __forceinline__ void slab_reduce_cols_body(const float *slab, int splits, int N, float *dst,
+                                                      int accumulate, int bid) {
     __shared__ float part[4][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    const int c = bid * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
     float s = 0.f;
     if (c < N)
         for (int k = g; k < splits; k += 4) s += slab[(long long)k * N + c];
@@ -754,6 +754,21 @@ __global__ __launch_bounds__(256) void k_slab_reduce_cols(const float *slab, int
         const float t = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
         dst[c] = accumulate ? dst[c] + t : t;
     }
+}
+
+__global__ __launch_bounds__(256) void k_slab_reduce(const float *slab, int splits, int M, int N,
+                                                     float *dst, long long ldw, int accumulate) {
+    slab_reduce_body(slab, splits, M, N, dst, ldw, accumulate, blockIdx.x, gridDim.x);
+}
+// both reduces in one launch: the first ncb blocks sum the bias columns, the rest the
+// dW slabs (the column job alone is a few latency-bound blocks: 9.5 us per launch)
+__global__ __launch_bounds__(256) void k_slab_reduce_both(const float *slab, int splits, int M, int N,
+                                                          float *dst, long long ldw, int accumulate,
+                                                          const float *bias_slab, float *bias_dst, int ncb) {
+    if ((int)blockIdx.x < ncb)
+        slab_reduce_cols_body(bias_slab, splits, N, bias_dst, accumulate, blockIdx.x);
+    else
+        slab_reduce_body(slab, splits, M, N, dst, ldw, accumulate, blockIdx.x - ncb, gridDim.x - ncb);
 }
 
 __global__ void k_rows_sum(h16 *edge, const h16 *src, long long ld, int r0, int r1, int cols) {
@@ -1288,10 +1303,14 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
 // split-K reduce of kf_gemm_wgrad's slabs (also used by conv_wgrad.hip)
 void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int M, int N, float *dW,
                      long long ldw, float *bias_grad, int accumulate) {
-    k_slab_reduce<<<kf_blocks((long long)M * N / 4 + 1, 256, 4096), 256, 0, kf_stream()>>>(
-        slab, splits, M, N, dW, ldw, accumulate);
-    if (bias_grad)
-        k_slab_reduce_cols<<<(N + 63) / 64, 256, 0, kf_stream()>>>(bias_slab, splits, N, bias_grad, accumulate);
+    const int nb = kf_blocks((long long)M * N / 4 + 1, 256, 4096);
+    if (bias_grad) {
+        const int ncb = (N + 63) / 64;
+        k_slab_reduce_both<<<ncb + nb, 256, 0, kf_stream()>>>(slab, splits, M, N, dW, ldw, accumulate, bias_slab,
+                                                             bias_grad, ncb);
+    } else {
+        k_slab_reduce<<<nb, 256, 0, kf_stream()>>>(slab, splits, M, N, dW, ldw, accumulate);
+    }
 }
 
 int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
