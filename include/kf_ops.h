@@ -239,6 +239,10 @@ void kf_gemm_debug_panel(int mode);
  * (diagnostics, scripts/rp_trace.py); NULL turns them off. */
 void kf_gemm_debug_rowpanel(int mode);
 void kf_rowpanel_trace(unsigned long long *buf);
+/* n <= KF_TRANSPOSE_MAX fp16 transposes in one launch: dst[j] [N[j] x M[j]] = src[j]^T
+ * (src[j] [M[j] x N[j]] row-major); the network's transposed weight copies */
+#define KF_TRANSPOSE_MAX 48
+int kf_transpose_batch(int n, const void *const *src, void *const *dst, const int *M, const int *N);
 /* diagnostics: wall-clock stamps (100 MHz) of block 300, wave 0 of the conv-halo launch
  * number `at` counted from this call: [0] start, [1 + 2s] after step s's wait and barrier,
  * [2 + 2s] after its MFMAs, [126] before the epilogue, [127] end; buf NULL disarms */

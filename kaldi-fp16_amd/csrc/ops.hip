@@ -446,6 +446,60 @@ int ops_tanh_backward(const void *out, void *grad, int count) {
                                                                     (h16 *)grad, count, ACT_TANH);
     return ops_check("tanh_backward");
 }
+// several transposes in one launch (the network's transposed weight copies after an
+// update): block b belongs to the job whose tile range [blk0[j], blk0[j + 1]) holds it
+struct TransposeJobs {
+    const h16 *src[KF_TRANSPOSE_MAX];
+    h16 *dst[KF_TRANSPOSE_MAX];
+    int M[KF_TRANSPOSE_MAX], N[KF_TRANSPOSE_MAX], gx[KF_TRANSPOSE_MAX];
+    int blk0[KF_TRANSPOSE_MAX + 1];
+    int n;
+};
+__global__ void k_transpose_batch(TransposeJobs J) {
+    __shared__ h16 tile[64][65];
+    int j = 0;
+    while (j + 1 < J.n && (int)blockIdx.x >= J.blk0[j + 1]) ++j;
+    const int b = blockIdx.x - J.blk0[j];
+    const int bx = (b % J.gx[j]) * 64, by = (b / J.gx[j]) * 64, M = J.M[j], N = J.N[j];
+    const h16 *src = J.src[j];
+    h16 *dst = J.dst[j];
+    for (int r = threadIdx.y; r < 64; r += blockDim.y) {
+        const int m = by + r, n = bx + threadIdx.x;
+        if (m < M && n < N) tile[r][threadIdx.x] = src[(long long)m * N + n];
+    }
+    __syncthreads();
+    for (int r = threadIdx.y; r < 64; r += blockDim.y) {
+        const int n = bx + r, m = by + threadIdx.x;
+        if (m < M && n < N) dst[(long long)n * M + m] = tile[threadIdx.x][r];
+    }
+}
+extern "C" int kf_transpose_batch(int n, const void *const *src, void *const *dst, const int *M, const int *N) {
+    if (n < 0 || n > KF_TRANSPOSE_MAX) {
+        kf_report_error("kf_transpose_batch: %d jobs (at most %d)", n, KF_TRANSPOSE_MAX);
+        return -1;
+    }
+    TransposeJobs J{};
+    int tot = 0;
+    for (int i = 0; i < n; ++i) {
+        if (M[i] <= 0 || N[i] <= 0) {
+            kf_report_error("kf_transpose_batch: job %d is %d x %d", i, M[i], N[i]);
+            return -1;
+        }
+        J.src[i] = (const h16 *)src[i];
+        J.dst[i] = (h16 *)dst[i];
+        J.M[i] = M[i];
+        J.N[i] = N[i];
+        J.gx[i] = (N[i] + 63) / 64;
+        J.blk0[i] = tot;
+        tot += J.gx[i] * ((M[i] + 63) / 64);
+    }
+    J.blk0[n] = tot;
+    J.n = n;
+    if (!tot) return 0;
+    k_transpose_batch<<<tot, dim3(64, 4), 0, kf_stream()>>>(J);
+    return ops_check("transpose_batch");
+}
+
 int ops_transpose(const void *src, void *dst, int M, int N) {
     if (M <= 0 || N <= 0) return 0;
     dim3 grid((N + 63) / 64, (M + 63) / 64);
