@@ -311,6 +311,25 @@ def test_transpose(gpu, ab, M, N):
     np.testing.assert_array_equal(bits(back.read().reshape(M, N)), bits(x))
 
 
+def test_transpose_batch(gpu):
+    """kf_transpose_batch (kf_ops.h): several ragged transposes in one launch, each equal to
+    ops_transpose's; more jobs than the limit is an error"""
+    shapes = [(320, 1536), (1, 1), (65, 130), (1500, 40), (160, 3072)]
+    xs = [f16(rng_for("trb", M, N).random((M, N)) * 2 - 1) for M, N in shapes]
+    src = [Slot(gpu, x) for x in xs]
+    dst = [Slot(gpu, np.zeros((N, M))) for M, N in shapes]
+    n = len(shapes)
+    arr = lambda t, v: (t * n)(*v)
+    gpu.core.kf_transpose_batch.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    rc = gpu.core.kf_transpose_batch(n, arr(C.c_void_p, [s.ptr for s in src]), arr(C.c_void_p, [d.ptr for d in dst]),
+                                     arr(C.c_int, [M for M, _ in shapes]), arr(C.c_int, [N for _, N in shapes]))
+    assert rc == 0
+    for x, d, (M, N) in zip(xs, dst, shapes):
+        np.testing.assert_array_equal(bits(d.read().reshape(N, M)), bits(x.T))
+    big = 49
+    assert gpu.core.kf_transpose_batch(big, arr(C.c_void_p, [src[0].ptr] * n), None, None, None) == -1
+
+
 # ----------------------------------------------------------------- backward element-wise
 @pytest.mark.parametrize("count", COUNTS)
 def test_relu_backward_exact(gpu, ab, count):
