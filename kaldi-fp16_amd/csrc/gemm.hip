@@ -51,6 +51,7 @@ struct WgradArgs {
     // whole (column chunk, split) pairs, so the two parts' reads of the same source rows
     // meet in one L2 instead of two
     int pair_ps;
+    int kil;            // fused: 1 = alternate the K-steps of a two-part A (KF_GEMM_KIL, default 1)
 };
 
 template <int BM, int BN, int ST, int SCB = 0>
@@ -392,15 +393,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     // address-taken and sends them to scratch)
     EpiPre epre{0.f, 0.f, 0.f, 1.f};
     if constexpr (!WGRAD) epre = epi_params<BN, 64 * NW>(E, N, n0, tid);
-    if (nk > 0) issue(0, kbeg);
-    if (ST >= 3 && nk > 1) issue(1, kbeg + BK);
-    if (ST >= 4 && nk > 2) issue(2, kbeg + 2 * BK);
+    // a two-part k-contiguous A ([x(t + d0) | x(t + d1)], K = 2 x part width): the K-steps
+    // alternate between the parts, so each 64-column chunk of the source rows is fetched
+    // for both parts while it is still in L2 (in part order the second pass misses)
+    int kil = 0;
+    if constexpr (!WGRAD && !F8 && AKC && AM == OP_P2)
+        kil = (A.nparts == 2 && A.pw % BK == 0 && K == 2 * A.pw && G.kil) ? A.pw : 0;
+    auto kofs = [&](int kt) { return kil ? (kt & 1) * kil + (kt >> 1) * BK : kbeg + kt * BK; };
+    if (nk > 0) issue(0, kofs(0));
+    if (ST >= 3 && nk > 1) issue(1, kofs(1));
+    if (ST >= 4 && nk > 2) issue(2, kofs(2));
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + ST - 2 < nk) wait_vmcnt<LPT * (ST - 2)>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        if (kt + ST - 1 < nk) issue((kt + ST - 1) % ST, kbeg + (kt + ST - 1) * BK);
+        if (kt + ST - 1 < nk) issue((kt + ST - 1) % ST, kofs(kt + ST - 1));
         const char *ta = smem + (kt % ST) * STAGE;
         const char *tb = ta + A_STAGE;
         if constexpr (F8) {
@@ -1209,7 +1217,8 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         kf_set_error("kf_gemm_fused: out8 needs N and ldo8 multiples of 32 and scale8");
         return -1;
     }
-    WgradArgs G{nullptr, nullptr, 0, 0};
+    static const int kil = getenv("KF_GEMM_KIL") ? atoi(getenv("KF_GEMM_KIL")) : 1;
+    WgradArgs G{nullptr, nullptr, 0, 0, kil};
     const int am = op_mode(a), bm = op_mode(b);
     const bool f8 = A->fmt == KF_FMT_MXFP8;
     if (f8 != (B->fmt == KF_FMT_MXFP8)) {
@@ -1369,7 +1378,7 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         return -1;
     }
     WgradArgs G{(float *)ws,
-                bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255)) : nullptr, kps, 0};
+                bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255)) : nullptr, kps, 0, 0};
     KfEpilogue E{};
     const int am = op_mode(a), bm = op_mode(b);
     // the TDNN-F linear's [x(t - s) | x(t)]: pair the parts' tiles per XCD (KF_WG_PAIR=0: off)
