@@ -398,7 +398,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     // for both parts while it is still in L2 (in part order the second pass misses)
     int kil = 0;
     if constexpr (!WGRAD && !F8 && AKC && AM == OP_P2)
-        kil = (A.nparts == 2 && A.pw % BK == 0 && K == 2 * A.pw && G.kil) ? A.pw : 0;
+        // (wide parts only: a narrow part's second pass is a few K-steps away and still hits)
+        kil = (A.nparts == 2 && A.pw % BK == 0 && A.pw >= 8 * BK && K == 2 * A.pw && G.kil) ? A.pw : 0;
     auto kofs = [&](int kt) { return kil ? (kt & 1) * kil + (kt >> 1) * BK : kbeg + kt * BK; };
     if (nk > 0) issue(0, kofs(0));
     if (ST >= 3 && nk > 1) issue(1, kofs(1));
