@@ -56,6 +56,22 @@ int kf_dp_allreduce_sum_f64(KfDp *dp, double *buf, size_t count);
 /* number of all-reduce launches and fp32 values exchanged since kf_dp_create */
 int kf_dp_stats(const KfDp *dp, long long *launches, long long *values);
 
+/* Test hooks (one GPU can then check what N ranks depend on). Each bucket issued by
+ * kf_dp_allreduce_mean_async whose address lies at or above grad_base also does, on the
+ * communication stream:
+ *   KF_DP_DEBUG_SNAPSHOT:  before the all-reduce, copies the bucket to the same offset
+ *                          of aux_base: the values the exchange started from, so a test
+ *                          can compare them with the finished gradient (a bucket issued
+ *                          before its producers finished differs);
+ *   KF_DP_DEBUG_PEER_MEAN: after the all-reduce, buf = (buf + aux) * 0.5 at the same
+ *                          offset: a two-rank average whose other rank's gradient is
+ *                          aux_base (a test supplies a second shard's gradient), so the
+ *                          gates, the bucket coverage and kf_dp_join all change results.
+ * mode 0 turns them off. The two modes are exclusive. -1: bad arguments. */
+#define KF_DP_DEBUG_SNAPSHOT 1
+#define KF_DP_DEBUG_PEER_MEAN 2
+int kf_dp_debug(KfDp *dp, int mode, const float *grad_base, float *aux_base);
+
 /* Bucket plan of a flat gradient buffer (host only, no device work).
  * steps: the backward visits nsteps parameter groups in order; group i occupies
  * [lo[i], hi[i]) of the flat buffer (lo = hi: no parameters). total: buffer length.
@@ -64,8 +80,10 @@ int kf_dp_stats(const KfDp *dp, long long *launches, long long *values);
  * Writes after_step[j], begin[j], end[j] for each bucket j (after_step = nsteps for
  * the final one) and returns the number of buckets. Groups that are not in
  * descending buffer order (a group reaching above the exchanged boundary) make the
- * plan one bucket [0, total) after the backward. -1: bad arguments (a group outside
- * [0, total], or max_buckets too small). */
+ * plan one bucket [0, total) after the backward. At most max_buckets buckets are
+ * written: when the limit is reached, everything not yet exchanged goes into the final
+ * bucket (after the last group). -1: bad arguments (a group outside [0, total],
+ * max_buckets < 1). */
 int kf_dp_plan(int nsteps, const long long *lo, const long long *hi, long long total,
                long long bucket_elems, int max_buckets, int *after_step, long long *begin,
                long long *end);

@@ -84,7 +84,14 @@ float *nnet_grad_buffer(KfNet *net);   /* device fp32 [num_params] */
 /* use caller-owned device memory (>= num_params fp32) as the gradient buffer */
 int nnet_bind_grad_buffer(KfNet *net, float *dev);
 float *nnet_master_buffer(KfNet *net); /* device fp32 [num_params] */
-void *nnet_weight_buffer(KfNet *net);  /* device fp16 [num_params] */
+/* device fp16 [num_params]. A host that writes weights through this pointer (a
+ * checkpoint restore, a weight broadcast) calls nnet_weights_changed afterwards, at
+ * every such write: the forward of the TDNN-F affine and prefinal big layers reads
+ * transposed copies and the fp8 mode MXFP8 copies, both derived from these weights. */
+void *nnet_weight_buffer(KfNet *net);
+/* the fp16 weights were written from outside: refresh the derived copies (transposed
+ * copies at the next forward, MXFP8 copies now) */
+int nnet_weights_changed(KfNet *net);
 int nnet_sgd(KfNet *net, float lr, float momentum);
 /* MXFP8 forward (BASELINE configs[4]): 1 = every TDNN-F / linear / prefinal / output
  * GEMM whose input has an MXFP8 copy runs on the fp8 MFMA (kf_ops.h MXFP8 operands);
@@ -102,6 +109,10 @@ typedef struct KfDp KfDp;
 int nnet_bind_dp(KfNet *net, KfDp *dp, long long bucket_bytes);
 int nnet_dp_plan(const KfNet *net, long long bucket_bytes, int max_buckets, int *after_step,
                  long long *begin, long long *end);
+/* nnet_bind_dp plans at most 256 buckets (the rest merges into the final one).
+ * Test hook: on != 0 issues every bucket at the start of nnet_backward, before any
+ * gradient exists: the negative control of the overlap tests (kf_dp_debug). */
+int nnet_dp_debug_early(KfNet *net, int on);
 
 /* diagnostics (tests): back-propagate through the top n layers only; device
  * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott", "aux", "mask",

@@ -24,6 +24,8 @@
 #include "../../include/kf_dp.h"
 
 hipStream_t kf_stream();
+// ops.hip: buf[i] = (buf[i] + peer[i]) * 0.5f on `s` (the KF_DP_DEBUG_PEER_MEAN exchange)
+int kf_dp_debug_mean_launch(float *buf, const float *peer, size_t n, hipStream_t s);
 
 namespace {
 __thread char g_err[512];
@@ -89,6 +91,10 @@ struct KfDp {
     hipEvent_t done = nullptr;      // recorded on the comm stream by kf_dp_join
     int rank = 0, world = 1, device = 0;
     long long launches = 0, values = 0;
+    // kf_dp_debug: test hooks on the communication stream (0: off)
+    int debug = 0;
+    const float *dbg_base = nullptr;  // the gradient buffer the buckets lie in
+    float *dbg_aux = nullptr;         // snapshot / peer buffer, same layout
 };
 
 extern "C" const char *kf_dp_last_error(void) { return g_err[0] ? g_err : nullptr; }
@@ -161,12 +167,35 @@ extern "C" int kf_dp_allreduce_mean_async(KfDp *dp, float *buf, size_t count) {
     if (!hip_ok(hipEventRecord(gate, kf_stream()), "hipEventRecord") ||
         !hip_ok(hipStreamWaitEvent(dp->comm_stream, gate, 0), "hipStreamWaitEvent"))
         return -1;
+    const bool dbg = dp->debug && buf >= dp->dbg_base;
+    float *aux = dbg ? dp->dbg_aux + (buf - dp->dbg_base) : nullptr;
+    // what the exchange would send, captured at the moment it starts
+    if (dbg && (dp->debug & KF_DP_DEBUG_SNAPSHOT) &&
+        !hip_ok(hipMemcpyAsync(aux, buf, count * 4, hipMemcpyDeviceToDevice, dp->comm_stream), "snapshot"))
+        return -1;
     // also at world 1 (identity), so a one-GPU run exercises the same path
     if (!nccl_ok(rccl()->all_reduce(buf, buf, count, ncclFloat32, ncclAvg, dp->comm, dp->comm_stream),
                  "ncclAllReduce"))
         return -1;
+    if (dbg && (dp->debug & KF_DP_DEBUG_PEER_MEAN) && kf_dp_debug_mean_launch(buf, aux, count, dp->comm_stream) != 0) {
+        set_err("peer mean: %s", hipGetErrorString(hipGetLastError()));
+        return -1;
+    }
     dp->launches++;
     dp->values += (long long)count;
+    return 0;
+}
+
+extern "C" int kf_dp_debug(KfDp *dp, int mode, const float *grad_base, float *aux_base) {
+    if (!dp || (mode & ~(KF_DP_DEBUG_SNAPSHOT | KF_DP_DEBUG_PEER_MEAN)) ||
+        (mode && (!grad_base || !aux_base)) ||
+        ((mode & KF_DP_DEBUG_SNAPSHOT) && (mode & KF_DP_DEBUG_PEER_MEAN))) {
+        set_err("kf_dp_debug: bad arguments");
+        return -1;
+    }
+    dp->debug = mode;
+    dp->dbg_base = mode ? grad_base : nullptr;
+    dp->dbg_aux = mode ? aux_base : nullptr;
     return 0;
 }
 

@@ -226,6 +226,19 @@ __global__ void k_transpose(const h16 *src, h16 *dst, int M, int N) {
 
 __global__ void k_h2f(const h16 *s, float *d, long long n) { GRID_STRIDE(i, n) d[i] = h2f(s[i]); }
 
+// kf_dp_debug KF_DP_DEBUG_PEER_MEAN (csrc/dp.cpp): a two-rank average whose other rank's
+// bucket is `peer`, on the communication stream
+__global__ void k_dp_peer_mean(float *buf, const float *peer, long long n) {
+    GRID_STRIDE(i, n) buf[i] = (buf[i] + peer[i]) * 0.5f;
+}
+int kf_dp_debug_mean_launch(float *buf, const float *peer, size_t n, hipStream_t s) {
+    if (!n) return 0;
+    const long long blocks = ((long long)n + 255) / 256;
+    hipLaunchKernelGGL(k_dp_peer_mean, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, buf, peer,
+                       (long long)n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 __global__ void k_sgd(float *w32, h16 *w16, const h16 *g, float *v, float lr, float mom,
                       long long n) {
     GRID_STRIDE(i, n) {

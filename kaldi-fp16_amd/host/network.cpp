@@ -211,6 +211,7 @@ struct KfNet {
     KfDp *dp = nullptr;
     std::vector<int> dp_after;  // bucket j is issued after backward step dp_after[j]
     std::vector<long long> dp_begin, dp_end;
+    bool dp_early = false;  // nnet_dp_debug_early: every bucket issued before the backward (tests)
     std::vector<void *> allocs;
 
     void *dalloc(size_t bytes) {
@@ -1427,6 +1428,8 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     size_t dp_next = 0;
     for (const auto &r : net->offpath) bridge_gpu_memset(net->grad + r.first, 0, (size_t)r.second * 4);
     (void)n;
+    // negative control of the data-parallel tests: exchanging before any producer ran
+    if (net->dp && net->dp_early && !dp_issue(net, dp_next, INT_MAX)) return -1;
     for (int li = net->chain_out; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
         NetLayer &nl = net->layers[li];
         const Layer &L = nl.L;
@@ -1740,6 +1743,12 @@ extern "C" void *nnet_weight_buffer(KfNet *net) {
     return net->w16;
 }
 
+extern "C" int nnet_weights_changed(KfNet *net) {
+    if (!on_device(net, "weights_changed")) return -1;
+    net->wt_dirty = true;  // the transposed copies are refreshed at the next forward
+    return net->fp8 && !quantise_weights(net, false) ? -1 : 0;
+}
+
 extern "C" int nnet_sgd(KfNet *net, float lr, float momentum) {
     if (!on_device(net, "sgd")) return -1;
     if (!ck(kf_sgd_flat(net->master, net->w16, net->grad, net->vel, lr, momentum, net->nparams), "sgd"))
@@ -1863,6 +1872,12 @@ extern "C" int nnet_bind_dp(KfNet *net, KfDp *dp, long long bucket_bytes) {
     net->dp_begin.assign(b.begin(), b.begin() + nb);
     net->dp_end.assign(e.begin(), e.begin() + nb);
     net->dp = dp;
+    return 0;
+}
+
+extern "C" int nnet_dp_debug_early(KfNet *net, int on) {
+    if (!net) return -1;
+    net->dp_early = on != 0;
     return 0;
 }
 

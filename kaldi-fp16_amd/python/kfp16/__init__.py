@@ -97,6 +97,8 @@ _sig(nnet, "nnet_debug_tensor", _vp, _vp, C.c_char_p, _i)
 _sig(nnet, "nnet_create_layout", _vp, C.c_char_p, _i)
 _sig(nnet, "nnet_bind_dp", _i, _vp, _vp, _ll)
 _sig(nnet, "nnet_dp_plan", _i, _vp, _ll, _i, C.POINTER(_i), C.POINTER(_ll), C.POINTER(_ll))
+_sig(nnet, "nnet_dp_debug_early", _i, _vp, _i)
+_sig(nnet, "nnet_weights_changed", _i, _vp)
 # kf_dp.h (RCCL data parallel)
 _sig(core, "kf_dp_last_error", C.c_char_p)
 _sig(core, "kf_dp_unique_id", _i, C.c_char_p)
@@ -109,6 +111,7 @@ _sig(core, "kf_dp_join", _i, _vp)
 _sig(core, "kf_dp_allreduce_mean", _i, _vp, _vp, _sz)
 _sig(core, "kf_dp_allreduce_sum_f64", _i, _vp, _vp, _sz)
 _sig(core, "kf_dp_stats", _i, _vp, C.POINTER(_ll), C.POINTER(_ll))
+_sig(core, "kf_dp_debug", _i, _vp, _i, _vp, _vp)
 _sig(core, "kf_dp_plan", _i, _i, C.POINTER(_ll), C.POINTER(_ll), _ll, _ll, _i, C.POINTER(_i),
      C.POINTER(_ll), C.POINTER(_ll))
 _sig(core, "kf_prof_enable", None, _i)
@@ -349,6 +352,15 @@ class Network:
         if n < 0:
             raise KfError("nnet_dp_plan: " + _err(nnet.nnet_last_error))
         return [(a[i], b[i], e[i]) for i in range(n)]
+
+    def weights_changed(self):
+        """The fp16 weights were written through nnet_weight_buffer (kf_nnet.h)."""
+        check(nnet.nnet_weights_changed(self.h), "nnet_weights_changed")
+
+    def dp_debug_early(self, on: bool):
+        """Test hook: issue every gradient bucket before the backward runs (the
+        negative control of the overlap tests)."""
+        check(nnet.nnet_dp_debug_early(self.h, int(on)), "nnet_dp_debug_early")
 
     def bind_dp(self, comm, bucket_bytes: int):
         """Exchange the gradient over `comm` (kfp16.dp.Communicator) in buckets during

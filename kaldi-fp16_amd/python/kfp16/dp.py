@@ -94,6 +94,16 @@ class Communicator:
         if core.kf_dp_allreduce_sum_f64(self.h, ptr, int(count)) != 0:
             raise RuntimeError("kf_dp_allreduce_sum_f64: " + _dp_err(core))
 
+    DEBUG_SNAPSHOT, DEBUG_PEER_MEAN = 1, 2
+
+    def debug(self, mode: int, grad_base=None, aux_base=None):
+        """kf_dp_debug test hooks: DEBUG_SNAPSHOT copies each bucket to aux (same offset
+        from grad_base) as its exchange starts; DEBUG_PEER_MEAN averages each exchanged
+        bucket with aux, a second rank's gradient. 0 turns them off."""
+        core = _core()
+        if core.kf_dp_debug(self.h, int(mode), grad_base, aux_base) != 0:
+            raise RuntimeError("kf_dp_debug: " + _dp_err(core))
+
     def stats(self):
         """(all-reduce launches, fp32 values exchanged) since creation."""
         n, v = C.c_longlong(), C.c_longlong()
