@@ -224,21 +224,11 @@ int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
 int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes);
 void kf_prof_reset(void);
 
-/* the panel GEMM for short-reduction wide-output fused products (K = 64 / 128 / 160 / 256 / 320,
- * csrc/panel.hip): 1 when enabled (KF_PANEL=1; off by default: measured slower than the
- * tiled GEMM on the MI355X). kf_gemm_debug_panel:
- * 0 off, 1 on, -1 back to the environment's choice (tests: bit-identical A/B). */
-int kf_panel_enabled(void);
-void kf_gemm_debug_panel(int mode);
-
-/* the row-panel GEMM for the same shapes with K = 160 / 256 / 320 and N % 32 == 0
- * (csrc/rowpanel.hip: A rows in registers, weights and epilogue row operands streamed by
- * LDS-DMA per 32-column block). Off by default (KF_ROWPANEL=1 turns it on): slower than
- * the tiled GEMM on the MI355X. kf_gemm_debug_rowpanel: 0 off, 1 on, -1
- * back to the environment's choice. kf_rowpanel_trace: phase timestamps of one block
- * (diagnostics, scripts/rp_trace.py); NULL turns them off. */
-void kf_gemm_debug_rowpanel(int mode);
-void kf_rowpanel_trace(unsigned long long *buf);
+/* test hook: the fused GEMM's K-step interleave of a two-part spliced A with parts of
+ * >= 512 columns (the TDNN-F linear forward / affine input gradient). 1 (default):
+ * the K-steps alternate between the parts; 0: part order. Only the fp32 accumulation
+ * order differs. */
+void kf_gemm_debug_kil(int on);
 /* n <= KF_TRANSPOSE_MAX fp16 transposes in one launch: dst[j] [N[j] x M[j]] = src[j]^T
  * (src[j] [M[j] x N[j]] row-major); the network's transposed weight copies */
 #define KF_TRANSPOSE_MAX 48

@@ -259,20 +259,16 @@ int kf_prof_start2(int cls, double flops, double bytes);
 void kf_prof_stop(int idx);
 
 // Returns 1 when launched, 0 when the operands are not a 3x3 conv im2col pair this
-// kernel covers (the caller runs the im2col GEMM), -1 on error. KF_CONV_WHALO=0
-// disables it (A/B).
+// kernel covers (the caller runs the im2col GEMM), -1 on error.
 int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
                            float *bias_grad, int accumulate) {
-    static const int on = getenv("KF_CONV_WHALO") ? atoi(getenv("KF_CONV_WHALO")) : 1;
-    if (!on || a.nparts != WTAPS || a.pw % 64 || a.simple || a.edges || a.tclamp || a.hshift ||
+    if (a.nparts != WTAPS || a.pw % 64 || a.simple || a.edges || a.tclamp || a.hshift ||
         a.hmul < 1 || a.hmul > 2 || a.hout < 2 || a.ncols != WTAPS * a.pw || M != a.ncols ||
         a.nrows != K || !b.simple || b.nrows != K || b.ncols != N || N % 64)
         return 0;
     // 64-column tiles on 4-wave workgroups, two per CU, measured faster than 128-column
-    // tiles on 8 waves for every layer (cnn6 1330 -> 1238 us, cnn4 690 -> 640 us);
-    // KF_WHALO_BN=128 selects the 8-wave form (A/B)
-    static const int bn_env = getenv("KF_WHALO_BN") ? atoi(getenv("KF_WHALO_BN")) : 64;
-    int BN = bn_env == 128 && N % 128 == 0 ? 128 : 64;
+    // tiles on 8 waves for every layer (cnn6 1330 -> 1238 us, cnn4 690 -> 640 us)
+    int BN = 64;
     int dtmin = 1 << 20, dtmax = -(1 << 20), dhmin = 1 << 20, dhmax = -(1 << 20);
     for (int p = 0; p < WTAPS; ++p) {
         dtmin = std::min(dtmin, a.dt[p]);
@@ -308,18 +304,16 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     }
     H.mout = K;
     // BN = 64: 4-wave workgroups, two per CU; BN = 128: 8 waves, one per CU.
-    // Stages: 3 where they fit in LDS (KF_WHALO_NS overrides), else 2.
+    // Stages: 3 where they fit in LDS, else 2.
     // a halo too large for 4 waves' registers (cnn3: 37 pieces) takes the 8-wave form
     if (BN == 64 && (H.npieces + 3) / 4 > HPW_MAX && N % 128 == 0) BN = 128;
     const int nw = BN == 64 ? 4 : 8;
     H.hpw = (H.npieces + nw - 1) / nw;
     if (H.hpw > HPW_MAX || H.nf >= 2048 || (long long)a.hsrc * a.pw * 2 >= (1 << 20)) return 0;
-    static const int ns_env = getenv("KF_WHALO_NS") ? atoi(getenv("KF_WHALO_NS")) : 0;
     const size_t stage = (size_t)H.halo_bytes + (size_t)BN * BK * 2;
     const size_t cap = BN == 64 ? 80 * 1024 : 160 * 1024;  // BN = 64: leave room for 2 per CU
     // (8-wave tiles: 2 stages, measured faster than 3)
-    int ns = ns_env ? ns_env : (BN == 64 && 3 * stage + 1024 <= cap ? 3 : 2);
-    if (ns < 2 || ns > 3) ns = 2;
+    const int ns = BN == 64 && 3 * stage + 1024 <= cap ? 3 : 2;
     const size_t lds = ns * stage + 1024;
     if (lds > 160 * 1024 || (ns - 2) * (H.hpw + BN / 8 / nw) > 15) return 0;
     if (((long long)a.T * a.ld + (long long)a.hsrc * a.pw) * 2 >= (1LL << 32) - 64) return 0;
@@ -328,8 +322,7 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     const int tiles = H.ctiles * H.ntiles;
     const int nks = (K + BK - 1) / BK;
     // one workgroup per CU: split the reduction so the grid is about one full wave of CUs
-    static const int target_env = getenv("KF_WHALO_WG") ? atoi(getenv("KF_WHALO_WG")) : 0;
-    const int target = target_env ? target_env : (nw == 4 && lds <= 80 * 1024 ? 512 : 256);
+    const int target = nw == 4 && lds <= 80 * 1024 ? 512 : 256;
     int splits = std::max(1, (target + tiles - 1) / tiles);
     splits = std::min(splits, std::max(1, nks / 8));
     H.kps = (nks + splits - 1) / splits;

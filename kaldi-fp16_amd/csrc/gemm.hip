@@ -343,12 +343,6 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
             const int unit = w >> 1, chunk = unit / gridDim.y;
             split = unit - chunk * gridDim.y;
             tile = (w & 1) * G.pair_ps + chunk;  // n_ntiles == 1
-        } else if (G.pair_ps < 0) {  // split-major: the tiles of one split share an XCD
-            const int total = gridDim.x * gridDim.y, L = blockIdx.x + blockIdx.y * gridDim.x;
-            const int q = total / 8, rmd = total % 8, xcd = L % 8, loc = L / 8;
-            const int w = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + loc;
-            split = w / gridDim.x;
-            tile = w - split * gridDim.x;
         }
     }
     const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
@@ -400,7 +394,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     if constexpr (!WGRAD && !F8 && AKC && AM == OP_P2)
         // (wide parts only: a narrow part's second pass is a few K-steps away and still hits)
         kil = (A.nparts == 2 && A.pw % BK == 0 && A.pw >= 8 * BK && K == 2 * A.pw && G.kil) ? A.pw : 0;
-    auto kofs = [&](int kt) { return kil ? (kt & 1) * kil + (kt >> 1) * BK : kbeg + kt * BK; };
+    auto kofs = [&](int kt) { return kbeg + (kil ? (kt & 1) * kil + (kt >> 1) * BK : kt * BK); };
     if (nk > 0) issue(0, kofs(0));
     if (ST >= 3 && nk > 1) issue(1, kofs(1));
     if (ST >= 4 && nk > 2) issue(2, kofs(2));
@@ -1030,7 +1024,6 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
 // conv_halo_kernel dispatch: A must be a conv im2col / col2im operand (k-contiguous,
 // 64-channel parts, zero time padding, no edge rows, hdiv 1, hmul 1 or 2). Returns
 // 1 when launched, 0 when not applicable (the caller runs the im2col GEMM), -1 on error.
-// KF_CONV_HALO=0 disables it (A/B).
 // ---------------------------------------------------------------------------
 static unsigned long long *g_halo_trace = nullptr;
 static int g_halo_trace_at = -1, g_halo_launches = 0;
@@ -1070,8 +1063,7 @@ static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const Ha
 
 static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm, bool bkc,
                          const KfEpilogue &E) {
-    static const int on = getenv("KF_CONV_HALO") ? atoi(getenv("KF_CONV_HALO")) : 1;
-    if (!on || op_mode(a) != OP_GEN || !a.p64 || a.edges || a.tclamp || a.hshift ||
+    if (op_mode(a) != OP_GEN || !a.p64 || a.edges || a.tclamp || a.hshift ||
         a.hmul < 1 || a.hmul > 2 || a.hout < 2 || a.ncols != K || a.nparts * a.pw != K)
         return 0;
     if (bkc ? bm != OP_GEN : bm != OP_SIMPLE) return 0;
@@ -1121,78 +1113,50 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     }
     // 32-bit source offsets: the largest byte offset the halo can form
     if (((long long)a.T * a.ld + (long long)a.hsrc * a.pw) * 2 >= (1LL << 32) - 64) return 0;
-    static const int bn_max = getenv("KF_HALO_BNMAX") ? atoi(getenv("KF_HALO_BNMAX")) : 256;
-    static const int bm_env = getenv("KF_HALO_BM") ? atoi(getenv("KF_HALO_BM")) : 256;
-    const int BN_ = (N <= 64 || bn_max <= 64) ? 64 : (N <= 128 || bn_max <= 128) ? 128 : 256;
-    // 256-row tiles only: where the two halo images do not fit beside a 256-column B ring
-    // (cnn5's stride-2 forward) the 128-row halo tile measured slower than im2col
-    // 128-row tiles for the strided convs' per-residue input gradients (3 or 6 taps; two
-    // workgroups per CU): cnn3 461 -> 332 and 588 -> 460 us, cnn5 370 -> 317 and
-    // 536 -> 468 us; 256-row tiles for everything else (KF_HALO_BM=128 forces 128)
+    const int BN_ = N <= 64 ? 64 : N <= 128 ? 128 : 256;
+    // 256-row tiles, except 128-row tiles for the strided convs' per-residue input
+    // gradients (3 or 6 taps; two workgroups per CU): cnn3 461 -> 332 and 588 -> 460 us,
+    // cnn5 370 -> 317 and 536 -> 468 us
     const bool residue = brow && a.nparts < 9;
-    for (int BM_ : {bm_env == 128 || residue ? 128 : 256}) {
-        H.nf = (BM_ - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
-        H.rows = H.nf * H.hpos;
-        H.npieces = (H.rows + 7) / 8;
-        H.slice = (H.npieces + H.ntaps - 1) / H.ntaps;
-        H.halo_bytes = H.npieces * 1024;
-        const int nw = BN_ == 64 ? 4 : 8, wtn = BN_ == 64 ? 64 : BN_ == 128 ? 64 : 64;
-        const size_t epi = 16 * BN_ + 32 * (wtn + 4) * 4 * nw;
-        size_t lds = std::max((size_t)H.nbuf * H.halo_bytes + 2 * BN_ * BK * 2, epi);
-        // two halo images too large (cnn5's stride-2 forward: 80 KB each beside a 64 KB
-        // B ring): one image, reloaded between channel chunks (KF_HALO_ONE=0: im2col GEMM)
-        static const int one = getenv("KF_HALO_ONE") ? atoi(getenv("KF_HALO_ONE")) : 1;
-        if (lds > 160 * 1024 && H.nbuf == 2 && one) {
-            H.nbuf = 1;
-            lds = std::max((size_t)H.halo_bytes + 2 * BN_ * BK * 2, epi);
-        }
-        if (lds > 160 * 1024) continue;
-        // KF_HALO_ST=4: a 4-stage B ring on 256-row tiles where it fits (two weight stages
-        // in flight across each barrier). Off: measured slower (cnn2 fwd / dgrad 517 / 521
-        // -> 884 / 986 us at one workgroup per CU instead of two, no layer faster)
-        static const int st_env = getenv("KF_HALO_ST") ? atoi(getenv("KF_HALO_ST")) : 2;
-        int ST_ = 2;
-        {
-            const int nw_ = BN_ == 64 ? 4 : 8, nc = BN_ / 8 / nw_;
-            const int hpw = (H.nbuf > 1 ? (H.slice + nw_ - 1) / nw_ : 0);
-            const size_t lds4 = std::max((size_t)H.nbuf * H.halo_bytes + 4 * BN_ * BK * 2, epi);
-            if (st_env >= 4 && BM_ == 256 && lds4 <= 160 * 1024 && 2 * (hpw + nc) <= 15) {
-                ST_ = 4;
-                lds = lds4;
-            }
-        }
-        // KF_HALO_W2=1: 64-column tiles on two 128x64-tile waves (more MACs per LDS byte)
-        static const int w2 = getenv("KF_HALO_W2") ? atoi(getenv("KF_HALO_W2")) : 0;
-#define KF_HALO(BKC_, BMODE_, BROW_)                                                                     \
-        do {                                                                                      \
-            if (BN_ == 64 && BM_ == 256 && w2)                                                    \
-                return launch_halo<256, 64, 2, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds);   \
-            if (BN_ == 64)                                                                        \
-                return BM_ == 128 ? launch_halo<128, 64, 4, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds)  \
-                       : ST_ == 4 ? launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_, 4>(M, N, bp, E, H, lds)  \
-                                  : launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds); \
-            if (BN_ == 128)                                                                       \
-                return BM_ == 128 ? launch_halo<128, 128, 4, 2, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds) \
-                       : ST_ == 4 ? launch_halo<256, 128, 4, 2, BKC_, BMODE_, BROW_, 4>(M, N, bp, E, H, lds) \
-                                  : launch_halo<256, 128, 4, 2, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds); \
-            return BM_ == 128 ? launch_halo<128, 256, 2, 4, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds)     \
-                   : ST_ == 4 ? launch_halo<256, 256, 2, 4, BKC_, BMODE_, BROW_, 4>(M, N, bp, E, H, lds)     \
-                              : launch_halo<256, 256, 2, 4, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds);    \
-        } while (0)
-        if (bkc) KF_HALO(true, OP_SIMPLE, true);
-        KF_HALO(false, OP_SIMPLE, false);
-#undef KF_HALO
+    const int BM_ = residue ? 128 : 256;
+    H.nf = (BM_ - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
+    H.rows = H.nf * H.hpos;
+    H.npieces = (H.rows + 7) / 8;
+    H.slice = (H.npieces + H.ntaps - 1) / H.ntaps;
+    H.halo_bytes = H.npieces * 1024;
+    const int nw = BN_ == 64 ? 4 : 8;
+    const size_t epi = 16 * BN_ + 32 * (64 + 4) * 4 * nw;
+    size_t lds = std::max((size_t)H.nbuf * H.halo_bytes + 2 * BN_ * BK * 2, epi);
+    // two halo images too large (cnn5's stride-2 forward: 80 KB each beside a 64 KB
+    // B ring): one image, reloaded between channel chunks
+    if (lds > 160 * 1024 && H.nbuf == 2) {
+        H.nbuf = 1;
+        lds = std::max((size_t)H.halo_bytes + 2 * BN_ * BK * 2, epi);
     }
+    if (lds > 160 * 1024) return 0;
+    // (measured and dropped: a 4-stage weight ring at one workgroup per CU, cnn2 517 ->
+    // 884 us; 64-column tiles on two 128x64-tile waves, cnn2 529 -> 781 us)
+#define KF_HALO(BKC_, BMODE_, BROW_)                                                                     \
+    do {                                                                                                 \
+        if (BN_ == 64)                                                                                   \
+            return BM_ == 128 ? launch_halo<128, 64, 4, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds)  \
+                              : launch_halo<256, 64, 4, 1, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds); \
+        if (BN_ == 128)                                                                                  \
+            return BM_ == 128 ? launch_halo<128, 128, 4, 2, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds) \
+                              : launch_halo<256, 128, 4, 2, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds); \
+        return BM_ == 128 ? launch_halo<128, 256, 2, 4, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds)     \
+                          : launch_halo<256, 256, 2, 4, BKC_, BMODE_, BROW_, 2>(M, N, bp, E, H, lds);    \
+    } while (0)
+    if (bkc) KF_HALO(true, OP_SIMPLE, true);
+    KF_HALO(false, OP_SIMPLE, false);
+#undef KF_HALO
     return 0;
 }
 
-static int gemm_big() {
-    const char *e = getenv("KF_GEMM_BIG");
-    return e ? atoi(e) : 1;
-}
-
-int kf_rowpanel_try(int M, int N, int K, const OpD &a, const OpD &b, int am, int bm, bool bkc,
-                    const KfEpilogue &E);
+// K-step interleave of two-part spliced A operands (WgradArgs::kil): 1 = on (default),
+// 0 = part order. Test hook: kf_gemm_debug_kil (kf_ops.h) compares the two orders.
+static int g_kil = 1;
+extern "C" void kf_gemm_debug_kil(int on) { g_kil = on != 0; }
 
 extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              const KfEpilogue *epi) {
@@ -1218,8 +1182,7 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         kf_set_error("kf_gemm_fused: out8 needs N and ldo8 multiples of 32 and scale8");
         return -1;
     }
-    static const int kil = getenv("KF_GEMM_KIL") ? atoi(getenv("KF_GEMM_KIL")) : 1;
-    WgradArgs G{nullptr, nullptr, 0, 0, kil};
+    WgradArgs G{nullptr, nullptr, 0, 0, g_kil};
     const int am = op_mode(a), bm = op_mode(b);
     const bool f8 = A->fmt == KF_FMT_MXFP8;
     if (f8 != (B->fmt == KF_FMT_MXFP8)) {
@@ -1242,55 +1205,23 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
             return launch<128, 128, 2, 2, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
         return launch<128, 128, 2, 2, true, true, false, 2, OP_P2, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
     }
-    PanelB pb;
-    if (kf_panel_ok(M, N, K, a, b, B->kcontig != 0, E, &pb)) {
-        ProfRec rec{};
-        if (g_prof) {
-            rec.a = prof_event();
-            rec.b = prof_event();
-            rec.cls = KF_PROF_FUSED;
-            rec.flops = 2.0 * M * N * (double)K;
-            rec.bytes = op_src_bytes(a, 0) + op_src_bytes(b, 0) + epi_bytes(E, M, N);
-            hipEventRecord(rec.a, kf_stream());
-        }
-        const int rc = kf_panel_launch(M, N, K, a, pb, E);
-        if (g_prof) {
-            hipEventRecord(rec.b, kf_stream());
-            g_prof_recs.push_back(rec);
-        }
-        return rc;
-    }
-    {
-        const int hr = kf_rowpanel_try(M, N, K, a, b, am, bm, B->kcontig != 0, E);
-        if (hr != 0) return hr < 0 ? -1 : 0;
-    }
     if (!E.out8) {
         const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);
         if (hr != 0) return hr < 0 ? -1 : 0;
     }
-    // 8-wave 256-row tiles halve the staged bytes per MFMA flop against the 4-wave
-    // 128-row ones; KF_GEMM_BIG=0 selects the 4-wave family for A/B.
-    static const int big = gemm_big();
-    static const int b128 = getenv("KF_GEMM_B128") ? atoi(getenv("KF_GEMM_B128")) : 0;
-    static const int b160 = getenv("KF_GEMM_B160") ? atoi(getenv("KF_GEMM_B160")) : 1;
-    int tile = (N % 160 == 0 && N <= 320) ? 1 : (N <= 64 ? 2 : (big && N >= 256 ? 3 : 0));
-    if (tile == 0 && b128 && N <= 128) tile = 4;
-    if (E.out8 && tile == 1) tile = 0;  // out8 needs 32-column blocks inside one wave's tile
-    if (tile == 1 && b160) tile = 5;    // 8-wave 384x160: 1.5x the flops per staged byte
-    // Wide fused GEMMs spend much of a tile in the epilogue's HBM traffic (the TDNN-F
-    // affine forward and linear input gradient, K = 320, write 2-3 full-width fp16
-    // tensors). 192x128 tiles stage 80 KB of LDS, so two workgroups share a CU and one's
-    // epilogue overlaps the other's MFMA loop: 293 -> 266 us and 244 -> 228 us per
-    // launch against 256x256, step 47.2 -> 46.2 ms. KF_GEMM_T6=0 restores 256x256,
-    // 1 limits 192x128 to K <= 640.
-    static const int t6 = getenv("KF_GEMM_T6") ? atoi(getenv("KF_GEMM_T6")) : 2;
-    if (t6 && tile == 3 && (K <= 640 || t6 == 2) && !E.out8) tile = 6;
+    // Tiles: 384x160 8-wave for N = 160 / 320; 256x64 for N <= 64; for
+    // N >= 256 192x128 8-wave tiles (80 KB of LDS: two workgroups share a CU and one's
+    // epilogue overlaps the other's MFMA loop; the wide K = 320 products write 2-3
+    // full-width fp16 tensors), 256x256 when the epilogue writes an MXFP8 copy (32-column
+    // blocks inside one wave's tile); 128x128 otherwise.
+    int tile = 0;
+    if (N % 160 == 0 && N <= 320 && !E.out8) tile = 5;
+    else if (N <= 64) tile = 2;
+    else if (N >= 256) tile = E.out8 ? 3 : 6;
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
         if (tile == 3) return launch<256, 256, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 6) return launch<192, 128, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
-        if (tile == 4) return launch<256, 128, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
-        if (tile == 1) return launch<128, 160, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 5) return launch<384, 160, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 2) return launch<256, 64, 4, 1, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);  \
         return launch<128, 128, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);               \
@@ -1341,29 +1272,24 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         const int hr = kf_conv_wgrad_halo_try(M, N, K, a, b, dW, ldw, bias_grad, accumulate);
         if (hr != 0) return hr < 0 ? -1 : 0;
     }
-    static const int wbig = getenv("KF_GEMM_WBIG") ? atoi(getenv("KF_GEMM_WBIG")) : 1;
-    static const int w160 = getenv("KF_GEMM_W160") ? atoi(getenv("KF_GEMM_W160")) : 1;
-    int BMc = 128, BNc = (N % 160 == 0 && N <= 320) ? 160 : (N <= 64 ? 64 : 128);
-    if (BNc == 160 && w160) BMc = w160 == 2 ? 192 : 384;  // 2: 8-wave 192 x 160 (half the splits)
-    if (BNc == 64) BMc = 256;
-    if (wbig && BNc == 128) BMc = 256, BNc = N > 128 ? 256 : 128;
-    // tile rows: the candidate wasting the fewest padded rows of M (ties: the larger)
-    static const int wfit = getenv("KF_GEMM_WFIT") ? atoi(getenv("KF_GEMM_WFIT")) : 1;
-    if (wfit && BMc == 256 && BNc != 160) {
+    // tiles: 384x160 for N = 160 / 320 (TDNN-F linear); otherwise 64-, 128- or 256-column
+    // tiles whose row count (192, 256 or 320) wastes the fewest padded rows of M
+    int BMc = 256, BNc = (N % 160 == 0 && N <= 320) ? 160 : N <= 64 ? 64 : N <= 128 ? 128 : 256;
+    if (BNc == 160) {
+        BMc = 384;
+    } else {
         const int cands[3] = {256, BNc == 256 ? 320 : 256, 192};
-        int best = 256;
         long long bw = (long long)(M + 255) / 256 * 256;
         for (int c : cands) {
             const long long w = (long long)(M + c - 1) / c * c;
-            if (w < bw) bw = w, best = c;
+            if (w < bw) bw = w, BMc = c;
         }
-        BMc = best;
     }
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
     // workgroups per launch: every split writes an M x N fp32 slab that the reduce
     // reads back, so the target trades CU fill against slab traffic
-    static const int wg_target = getenv("KF_WG_TARGET") ? atoi(getenv("KF_WG_TARGET")) : 512;
-    int splits = (wg_target + tiles - 1) / tiles;
+    // (targets of 256 / 384 / 768 / 1024 measured slower)
+    int splits = (512 + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
     if (splits > maxsplit) splits = maxsplit;
     if (splits < 1) splits = 1;
@@ -1382,13 +1308,10 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
                 bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255)) : nullptr, kps, 0, 0};
     KfEpilogue E{};
     const int am = op_mode(a), bm = op_mode(b);
-    // the TDNN-F linear's [x(t - s) | x(t)]: pair the parts' tiles per XCD (KF_WG_PAIR=0: off)
-    static const int wpair = getenv("KF_WG_PAIR") ? atoi(getenv("KF_WG_PAIR")) : 1;
-    if (wpair && am == OP_P2 && A->nparts == 2 && N <= BNc && A->part_width % BMc == 0 &&
+    // the TDNN-F linear's [x(t - s) | x(t)]: pair the parts' tiles per XCD
+    if (am == OP_P2 && A->nparts == 2 && N <= BNc && A->part_width % BMc == 0 &&
         M == 2 * A->part_width)
         G.pair_ps = A->part_width / BMc;
-    static const int wsm = getenv("KF_WG_SPLITMAJOR") ? atoi(getenv("KF_WG_SPLITMAJOR")) : 0;
-    if (wsm && G.pair_ps == 0) G.pair_ps = -1;
     int rc;
 #define KF_WG(AM_, BM_)                                                                          \
     do {                                                                                         \
@@ -1404,16 +1327,10 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
             rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BMc == 256 && BNc == 128)                                                       \
             rc = launch<256, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
-        else if (BMc == 192 && BNc == 160)                                                       \
-            rc = launch<192, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
-        else if (BMc == 384 && BNc == 160)                                                       \
-            rc = launch<384, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 160)                                                                     \
-            rc = launch<128, 160, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
-        else if (BNc == 64)                                                                      \
-            rc = launch<256, 64, 4, 1, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+            rc = launch<384, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else                                                                                     \
-            rc = launch<128, 128, 2, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+            rc = launch<256, 64, 4, 1, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
     } while (0)
     if (bm == OP_SIMPLE && am == OP_SIMPLE) KF_WG(OP_SIMPLE, OP_SIMPLE);
     else if (bm == OP_SIMPLE && am == OP_P2) KF_WG(OP_P2, OP_SIMPLE);

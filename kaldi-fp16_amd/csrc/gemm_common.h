@@ -1,4 +1,4 @@
-// gemm_common.h — device pieces shared by the MFMA GEMM kernels (gemm.hip, panel.hip):
+// gemm_common.h — device pieces shared by the MFMA GEMM kernels (gemm.hip, conv_wgrad.hip):
 // operand addressing (the device form of KfOperand), the LDS images and fragment
 // loads of v_mfma_f32_16x16x32_f16, the LDS-DMA operand stager and the 8-column
 // epilogue. gfx950 only.
@@ -348,18 +348,3 @@ __device__ __forceinline__ void epilogue8(const KfEpilogue &E, const EpiCols &P,
         store_h8((h16 *)E.out2 + (long long)m * E.ldo2 + n, o);
     }
 }
-
-
-// ---------------------------------------------------------------------------
-// panel kernel (panel.hip): short-reduction, wide-output fused GEMMs
-// ---------------------------------------------------------------------------
-struct PanelB {  // B^T rows: element (n, k) of part p = k / pw at base[(n + roff[p]) * ld + k % pw]
-    const h16 *base;
-    long long ld;
-    int pw, nparts;
-    int roff[2];
-};
-// applicable: K = 64, 128, 160, 256 or 320, N % 32 == 0, a plain or time-spliced A,
-// a k-contiguous plain or row-part (op_wrows) B, no beta / MXFP8 output
-bool kf_panel_ok(int M, int N, int K, const OpD &a, const OpD &b, bool bkc, const KfEpilogue &E, PanelB *pb);
-int kf_panel_launch(int M, int N, int K, const OpD &a, const PanelB &pb, const KfEpilogue &E);

@@ -122,93 +122,6 @@ __global__ __launch_bounds__(256) void k_conv_c1_fwd(ConvC1 c, const h16 *x, con
     }
 }
 
-// 64-filter form: one thread per output row (t, h) with all 64 filters, so each input
-// tap is loaded once per row instead of once per 8-filter group (the per-group form is
-// bound by its 9 scattered 2-byte tap loads per 16 output bytes). Weights, bias and BN
-// sit in LDS and are read as wave-uniform broadcasts; the arithmetic per output (bias,
-// then taps in order, ReLU, BN) is the per-group kernel's, so the outputs are identical.
-__global__ __launch_bounds__(256) void k_conv_c1_fwd64(ConvC1 c, const h16 *x, const h16 *W, const h16 *bias,
-                                                       const float *scale, const float *shift, h16 *y,
-                                                       uint8_t *mask) {
-    __shared__ float4 ws[9][16];
-    __shared__ float4 bs[16], scs[16], sfs[16];
-    // output staging: a wave's 64 rows x 128 B, row stride 136 B (2-way bank conflicts),
-    // written per row by its lane, read back as 1 KiB contiguous stores
-    __shared__ __attribute__((aligned(16))) char stage[4][64 * 136];
-    for (int i = threadIdx.x; i < 9 * 64; i += blockDim.x) {
-        const int o = i / 64, f = i % 64;
-        reinterpret_cast<float *>(ws[o])[f] = o < c.noff ? h2f(W[o * 64 + f]) : 0.f;
-    }
-    for (int f = threadIdx.x; f < 64; f += blockDim.x) {
-        reinterpret_cast<float *>(bs)[f] = bias ? h2f(bias[f]) : 0.f;
-        reinterpret_cast<float *>(scs)[f] = scale ? scale[f] : 1.f;
-        reinterpret_cast<float *>(sfs)[f] = scale ? shift[f] : 0.f;
-    }
-    __syncthreads();
-    const int rows = c.T * c.hout;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    char *stg = stage[wave];
-    // the loop runs while any lane of the wave has a row (wave-uniform trip count)
-    for (int row0 = blockIdx.x * blockDim.x + wave * 64; row0 < rows; row0 += gridDim.x * blockDim.x) {
-        const int row = min(row0 + lane, rows - 1);
-        const int t = row / c.hout, h = row - t * c.hout;
-        float xv[9];
-#pragma unroll
-        for (int o = 0; o < 9; ++o) {
-            const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
-            const bool ok = o < c.noff && ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin;
-            const float v = h2f(x[ok ? ts * c.hin + hs : 0]);
-            xv[o] = ok ? v : 0.f;
-        }
-        unsigned long long bits = 0;
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {  // 8 filters at a time: 8 accumulators live
-            float v[8];
-            const float4 b0 = bs[2 * g], b1 = bs[2 * g + 1];
-            v[0] = b0.x, v[1] = b0.y, v[2] = b0.z, v[3] = b0.w;
-            v[4] = b1.x, v[5] = b1.y, v[6] = b1.z, v[7] = b1.w;
-#pragma unroll
-            for (int o = 0; o < 9; ++o) {
-                const float4 w0 = ws[o][2 * g], w1 = ws[o][2 * g + 1];
-                v[0] = fmaf(xv[o], w0.x, v[0]);
-                v[1] = fmaf(xv[o], w0.y, v[1]);
-                v[2] = fmaf(xv[o], w0.z, v[2]);
-                v[3] = fmaf(xv[o], w0.w, v[3]);
-                v[4] = fmaf(xv[o], w1.x, v[4]);
-                v[5] = fmaf(xv[o], w1.y, v[5]);
-                v[6] = fmaf(xv[o], w1.z, v[6]);
-                v[7] = fmaf(xv[o], w1.w, v[7]);
-            }
-            const float *sc = reinterpret_cast<const float *>(scs) + 8 * g;
-            const float *sf = reinterpret_cast<const float *>(sfs) + 8 * g;
-            half8 out;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                float a = v[e];
-                if (a > 0.f) bits |= 1ull << (8 * g + e);
-                else a = 0.f;
-                if (scale) a = fmaf(a, sc[e], sf[e]);
-                out[e] = f2h(a);
-            }
-            *reinterpret_cast<half8 *>(stg + lane * 136 + 16 * g) = out;
-        }
-        if (mask && row0 + lane < rows) *reinterpret_cast<unsigned long long *>(mask + (long long)row * 8) = bits;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {  // chunk q = 64k + lane: row q / 8, 16-byte piece q % 8
-            const int q = 64 * k + lane, r = q >> 3, pc = q & 7;
-            if (row0 + r < rows)
-                store_h8(y + (long long)(row0 + r) * 64 + 8 * pc,
-                         *reinterpret_cast<const half8 *>(stg + r * 136 + 16 * pc));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-}
-
 // partial dW / db of the 1-filter conv. Thread = (row group, 8 consecutive
 // filters): 16-byte dz loads, the <= 9 input taps per row read through L1.
 // Each block reduces a contiguous range of rows in a fixed order into
@@ -376,14 +289,7 @@ int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, co
         c.dt[i] = dt[i];
         c.dh[i] = dh[i];
     }
-    // KF_C1_ROWS=1: the row-per-thread form (measured slower: 359 -> 740 us with LDS-staged
-    // stores, 2177 us with per-row stores); off
-    static const int rows64 = getenv("KF_C1_ROWS") ? atoi(getenv("KF_C1_ROWS")) : 0;
-    if (fout == 64 && rows64) {
-        k_conv_c1_fwd64<<<kf_blocks((long long)T * hout, 256, 4096), 256, 0, kf_stream()>>>(
-            c, (const h16 *)x, (const h16 *)W, (const h16 *)bias, scale, shift, (h16 *)y, mask);
-        return lay_check("conv_c1_forward");
-    }
+    // (a row-per-thread form with all 64 filters measured slower: 359 -> 740 us)
     const long long total = (long long)T * hout * (fout / 8);
     k_conv_c1_fwd<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
         c, (const h16 *)x, (const h16 *)W, (const h16 *)bias, scale, shift, (h16 *)y, mask);

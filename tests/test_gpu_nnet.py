@@ -45,7 +45,11 @@ def test_ops_gemm_matches_fp32(gpu):
         kfp16.check(kfp16.core.ops_gemm(h, M, N, K, alpha, dA.ptr, K, dB.ptr, N, beta, dC.ptr, N), "gemm")
         got = kfp16.read_fp16(dC.ptr, (M, N)).astype(np.float64)
         ref = alpha * (A.astype(np.float64) @ B.astype(np.float64)) + beta * C0.astype(np.float64)
-        tol = 2 * np.abs(ref) * 2 ** -11 + 1e-6 * K * np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64) + 1e-3
+        # fp32 accumulation K * 2^-23 * sum|ab| (scaled by alpha), beta * C in fp32,
+        # one fp16 rounding of the result (<= |ref| * 2^-11, doubled for the shifted value)
+        mag = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
+        tol = (abs(alpha) * K * 2 ** -23 * mag + 2 ** -23 * abs(beta) * np.abs(C0.astype(np.float64))
+               + np.abs(ref) * 2 ** -10 + 2 ** -24)
         assert np.all(np.abs(got - ref) <= tol), (M, N, K, float(np.max(np.abs(got - ref) - tol)))
     kfp16.core.ops_cublas_destroy(h)
 
