@@ -436,6 +436,16 @@ struct SellDev {  // sliced ELL, 64 rows per slice, rows sorted by degree
     // (value row at byte 256, exp row after it), so the gathers need no address VALU
     const uint2 *arc_s;
     const float *initp;   // init[perm[c]] in slice order (0 for padding rows), f and b only
+    // Slice ownership for G = 1, 2, 4, 8 blocks per sequence (index log2 G): the slices
+    // are spread over the G x DEN_WAVES (block, wave) pairs by length, longest first onto
+    // the least loaded pair, so the slowest wave of a frame carries about the mean share
+    // (round-robin ownership left it 1.3-1.4x the mean on the den graph's degree-sorted
+    // slices). slot[lgG][gi * spg + k]: the slice in slot k of block gi, processed by
+    // wave k % DEN_WAVES (-1: empty); own[lgG][j] = gi << 16 | k. The q table keeps only
+    // its G = 1 lists (the posterior kernel's waves).
+    const int *slot[4];
+    const int *own[4];
+    int spg[4];
 };
 struct DenDev {
     int S, P;
@@ -466,9 +476,6 @@ struct DenRun {
     h16 *out_grad;
     long long ldg;
     KfChainOpts opts;
-    int early;              // bit 0: fetch the next frame's output row at frame start; bit 1:
-                            // also write its exp(x) before the exchange wait (KF_DEN_EARLY=3:
-                            // measured neutral, 7081 vs 7080 us)
 };
 
 enum { DEN_ABI = 0, DEN_PRODUCT = 1 };
@@ -523,12 +530,11 @@ struct StatePre {  // alpha' row prefetch (S <= DEN_MAXS * DEN_THREADS)
     }
 };
 
-// fwd / bwd: fixed part (va or vb, xe, len/off/coff); the rest of the 160 KiB LDS
-// holds resident arc records
+// fwd / bwd LDS: reduction scratch, the state row (va or vb), the exp row (xe), and
+// the table's slice metadata (len / off / perm / initp / ownership / this block's slots)
 #define DEN_LDS_TOTAL (160 * 1024)
-static size_t den_rec_fixed_bytes(int S, int P, int nsl, int ns = 1) {
-    return (size_t)4 * (64 + (size_t)ns * (S + P + (P & 1)) + 2 * (size_t)nsl + 128 * (size_t)nsl +
-                        nsl + 2) + 64;
+static size_t den_rec_fixed_bytes(int S, int P, int nsl, int spg) {
+    return (size_t)4 * (64 + (size_t)S + P + (P & 1) + 2 * (size_t)nsl + 128 * (size_t)nsl + nsl + spg) + 64;
 }
 static size_t den_post_lds_bytes(int S, int P, int nslq, int pair = 1) {
     return (size_t)4 * (64 + 2 * (size_t)pair * S + (size_t)pair * P + (size_t)nslq * 66);
@@ -556,15 +562,13 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 }
 
 struct DenX {
-    float *buf;     // [nseq][2][G][blk]; blk = ns*spg*64 + 64 (tail: [q * DEN_WAVES + wave] = that wave's partial sum of sequence q)
+    float *buf;     // [nseq][2][G][blk]; blk = spg*64 + 64 (tail: [wave] = that wave's partial sum)
     unsigned *cnt;  // [nseq] arrivals (zeroed before each launch)
     unsigned *tmo;  // per-launch timeout word (zeroed before each launch)
     unsigned *sticky;  // timed-out blocks since the last read (never zeroed by a launch)
     unsigned spin_limit;  // polls before a wait gives up (kf_chain_debug_spin_limit)
-    int G, lgG, spg, blk, nseq;  // nseq: exchange units (groups of ns sequences)
-    int ns, nseqs;               // sequences per unit, sequences in all
-    unsigned cache_f, cache_b;  // LDS bytes for resident arc records (fwd / bwd kernels)
-    unsigned lds_f, lds_b;      // dynamic LDS of the fwd / bwd kernels
+    int G, lgG, spg, blk, nseq;  // spg: exchange slots per block (the table's at this G)
+    unsigned lds_f, lds_b;       // dynamic LDS of the fwd / bwd kernels
 };
 
 // seq / slice-owner of this block; the G blocks of a sequence share an XCD when
@@ -577,19 +581,15 @@ __device__ __forceinline__ void den_map(const DenX &X, int &seq, int &gi) {
     gi = w & (X.G - 1);
 }
 
-// publish: every wave stores its partial sums of the NS sequences (lane 0, tail slot
-// q * DEN_WAVES + wave) beside its payload, all sc1; every wave drains vmcnt, the
-// workgroup barriers, one lane adds the arrival (one store drain per frame)
-template <int NS>
-__device__ __forceinline__ void den_publish(const DenX &X, float *tail, const float (&wsum)[NS], int unit) {
+// publish: every wave stores its partial sum (lane 0, tail slot `wave`) beside its
+// payload, all sc1; every wave drains vmcnt, the workgroup barriers, one lane adds
+// the arrival (one store drain per frame)
+__device__ __forceinline__ void den_publish(const DenX &X, float *tail, float wsum, int seq) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < NS; ++q) st_sc1(tail + q * DEN_WAVES + wave, wsum[q]);
-    }
+    if (lane == 0) st_sc1(tail + wave, wsum);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[unit], 1u, RLX_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[seq], 1u, RLX_AGENT);
 }
 // wait for `target` arrivals (one lane polls); false on timeout, uniform
 __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target, int *lds_flag) {
@@ -615,44 +615,38 @@ __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     return *lds_flag != 0;
 }
-// all exchanged slices of buffer `buf` for the NS sequences, scattered to their
-// states: first sum(q, total of the G x DEN_WAVES partial sums, fixed order, equal in
-// every lane), then f(q, state, value, initp, owner, slot) per slot. The partial sums
-// load with the first sequence's slices, so one round trip serves both.
-template <int NS, class FS, class F>
-__device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, int nsl,
+// all exchanged slices of buffer `buf`, scattered to their states: first sum(total of
+// the G x DEN_WAVES partial sums, fixed order, equal in every lane), then
+// f(state, value, initp, owner, slot) per slot. Slice j lives in slot own[j] & 0xFFFF
+// of block own[j] >> 16. The partial sums load with the slices, so one round trip
+// serves both.
+template <class FS, class F>
+__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, int nsl, const int *own,
                                             const int *perm, const float *initp, FS sum, F f) {
     int tid = threadIdx.x;
     // opaque to the optimiser: the per-slot addresses below are rebuilt every frame
-    // instead of being hoisted out of the frame loop as 64-bit values (16 of them
-    // for NS = 2 spill at the 128-VGPR budget of a 1024-thread block)
+    // instead of being hoisted out of the frame loop as 64-bit values
     asm volatile("" : "+v"(tid));
     const int n = nsl * 64, lane = tid & 63;
-    const float *xb = X.buf + ((size_t)unit * 2 + buf) * X.G * X.blk;
-    float pv[NS];
+    const float *xb = X.buf + ((size_t)seq * 2 + buf) * X.G * X.blk;
+    float pv = 0.0f;
+    for (int i = lane; i < X.G * DEN_WAVES; i += 64)
+        pv += ld_sc1(xb + (size_t)(i / DEN_WAVES) * X.blk + X.spg * 64 + i % DEN_WAVES);
+    float v[DEN_MAXS];
+    int o[DEN_MAXS];
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        pv[q] = 0.0f;
-        for (int i = lane; i < X.G * DEN_WAVES; i += 64)
-            pv[q] += ld_sc1(xb + (size_t)(i / DEN_WAVES) * X.blk + X.ns * X.spg * 64 + q * DEN_WAVES + i % DEN_WAVES);
+    for (int m = 0; m < DEN_MAXS; ++m) {  // unconditional loads (index clamped)
+        const int c = min(tid + m * DEN_THREADS, n - 1);
+        o[m] = own[c >> 6];
+        v[m] = ld_sc1(xb + (size_t)(o[m] >> 16) * X.blk + (o[m] & 0xFFFF) * 64 + (c & 63));
     }
+    sum(wave_sum(pv));
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {  // one sequence at a time: DEN_MAXS values live
-        float v[DEN_MAXS];
-#pragma unroll
-        for (int m = 0; m < DEN_MAXS; ++m) {  // unconditional loads (index clamped)
-            const int c = min(tid + m * DEN_THREADS, n - 1), j = c >> 6;
-            v[m] = ld_sc1(xb + (size_t)(j & (X.G - 1)) * X.blk + (size_t)q * X.spg * 64 +
-                          (j >> X.lgG) * 64 + (c & 63));
-        }
-        sum(q, wave_sum(pv[q]));
-#pragma unroll
-        for (int m = 0; m < DEN_MAXS; ++m) {
-            const int c = tid + m * DEN_THREADS;
-            if (c < n) {
-                const int st = perm[c];
-                if (st >= 0) f(q, st, v[m], initp[c], (c >> 6) & (X.G - 1), c);
-            }
+    for (int m = 0; m < DEN_MAXS; ++m) {
+        const int c = tid + m * DEN_THREADS;
+        if (c < n) {
+            const int st = perm[c];
+            if (st >= 0) f(st, v[m], initp[c], o[m] >> 16, c);
         }
     }
 }
@@ -662,277 +656,174 @@ __device__ __forceinline__ float lds_at(const unsigned char *smem, int a) {
     return *reinterpret_cast<const float *>(smem + a);
 }
 
-// gather-sum over one slice of a SELL table (fixed arc order); arcs may be a
-// global table or the LDS cache (callers branch, so each call's space is static)
+// gather-sum over one slice of a SELL table (fixed arc order)
 template <class Term>
 __device__ __forceinline__ float sell_slice(const uint2 *arcs, int len, int off, int lane, Term term) {
     const uint2 *e = arcs + (size_t)off * 64 + lane;
     float acc = 0.f;
-    int k = 0;
-    for (; k < len; k += 8) {  // 8 records in flight per lane (len is a multiple of 8)
-        uint2 rr[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            acc += term(rr[i].x & 0xFFFF, rr[i].x >> 16, __uint_as_float(rr[i].y));
-    }
-    return acc;
-}
-
-// the same pass for NS sequences sharing the records: acc[q] += term(q, f1, f2, tp)
-template <int NS, class Term>
-__device__ __forceinline__ void sell_slice_ns(const uint2 *arcs, int len, int off, int lane,
-                                              float (&acc)[NS], Term term) {
-    const uint2 *e = arcs + (size_t)off * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) acc[q] = 0.f;
     for (int k = 0; k < len; k += 8) {  // 8 records in flight per lane (len is a multiple of 8)
         uint2 rr[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int q = 0; q < NS; ++q)
-                acc[q] += term(q, rr[i].x & 0xFFFF, rr[i].x >> 16, __uint_as_float(rr[i].y));
+        for (int i = 0; i < 8; ++i) acc += term(rr[i].x & 0xFFFF, rr[i].x >> 16, __uint_as_float(rr[i].y));
     }
+    return acc;
 }
 
-// Per-block SELL state in LDS: len/off of every slice, and the arc records of this
-// block's first `kc` owned slices (slices gi, gi+G, ...), which then never leave
-// LDS for the whole launch (the rest are streamed from L2 every frame).
+// Per-block SELL state in LDS: len / off / perm / initp of every slice, the slice
+// ownership (own[j] = block << 16 | slot) and this block's slot list (slot k is
+// processed by wave k % DEN_WAVES; -1 = empty).
 struct SellLds {
     const int *len, *off;  // [nsl] each
     const int *perm;       // [nsl*64]
     const float *initp;    // [nsl*64]
-    const int *coff;       // [nk] record offset of owned slice k in the cache
-    const uint2 *cache;
-    int kc;
+    const int *own;        // [nsl]
+    const int *slot;       // [spg]
 };
-__device__ __forceinline__ SellLds stage_sell(const SellDev &T, int gi, int G, int nk,
-                                              unsigned char *base, size_t cache_bytes) {
+__device__ __forceinline__ SellLds stage_sell(const SellDev &T, int lgG, int gi, int spg, unsigned char *base) {
     int *lenl = reinterpret_cast<int *>(base), *offl = lenl + T.nsl;
     int *perml = offl + T.nsl;
     float *initl = reinterpret_cast<float *>(perml + T.nsl * 64);
-    int *coff = reinterpret_cast<int *>(initl + T.nsl * 64);
-    uint2 *cache = reinterpret_cast<uint2 *>(coff + ((nk + 1) & ~1));
+    int *ownl = reinterpret_cast<int *>(initl + T.nsl * 64);
+    int *slotl = ownl + T.nsl;
     for (int i = threadIdx.x; i < T.nsl; i += DEN_THREADS) {
         lenl[i] = T.len[i];
         offl[i] = T.off[i];
+        ownl[i] = T.own[lgG][i];
     }
     for (int i = threadIdx.x; i < T.nsl * 64; i += DEN_THREADS) {
         perml[i] = T.perm[i];
         initl[i] = T.initp[i];
     }
-    int kc = 0;
-    size_t used = 0;
-    for (int k = 0; k < nk; ++k) {  // every thread, same answer
-        const size_t rec = (size_t)T.len[gi + G * k] * 64;
-        if ((used + rec) * 8 > cache_bytes) break;
-        if (threadIdx.x == 0) coff[k] = (int)(used / 64);  // in 64-record rows, like T.off
-        used += rec;
-        kc = k + 1;
-    }
-    for (int k = 0, o = 0; k < kc; ++k) {
-        const int j = gi + G * k, n = T.len[j] * 64;
-        const uint2 *src = T.arc + (size_t)T.off[j] * 64;
-        for (int i = threadIdx.x; i < n; i += DEN_THREADS) cache[o + i] = src[i];
-        o += n;
-    }
-    SellLds L{lenl, offl, perml, initl, coff, cache, kc};
+    for (int i = threadIdx.x; i < spg; i += DEN_THREADS) slotl[i] = T.slot[lgG][gi * spg + i];
+    SellLds L{lenl, offl, perml, initl, ownl, slotl};
     return L;
 }
 
-// Forward pass (chain_den.cu:583-620), G blocks per exchange unit of NS sequences:
-// block gi computes alpha[t+1] for the destination rows of slices gi, gi+G, ... of
-// every sequence of its unit (the NS sequences share each arc record read), and all
-// blocks rebuild the full alpha'[t+1] in LDS from the exchanged slices. alpha' of
-// every frame goes to HBM for the posterior kernel. Ragged units: a sequence past
-// its last frame stops updating (its alpha'[T] stays in LDS for the total).
-template <typename XT, int NS>
+// Forward pass (chain_den.cu:583-620), G blocks per sequence: block gi computes
+// alpha[t+1] for the destination rows of its slices (a load-balanced share, SellDev::
+// slot), and all blocks rebuild the full alpha'[t+1] in LDS from the exchanged slices.
+// alpha' of every frame goes to HBM for the posterior kernel.
+template <typename XT>
 __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
-                                             unsigned char *smem, int unit, int gi) {
+                                             unsigned char *smem, int seq, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int G = X.G, nsl = g.f.nsl;
+    const int G = X.G, nsl = g.f.nsl, spg = X.spg;
     const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);          // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;        // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;      // [NS][S] alpha'[t]
-    float *xe = va + NS * S;                               // [NS][PP] exp(clamp(x))
-    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
-    const int nk = (nsl - gi + G - 1) / G;                 // slices owned by this block
+    float *va = reinterpret_cast<float *>(smem) + 64;      // [S] alpha'[t]
+    float *xe = va + S;                                    // [PP] exp(clamp(x))
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + PP);
 
-    int Ts[NS];
-    long long r0[NS];
-    int Tmax = 0;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        const int sq = unit * NS + q;
-        Ts[q] = sq < X.nseqs ? r.frames[sq] : 0;
-        r0[q] = sq < X.nseqs ? r.row0[sq] : 0;
-        Tmax = max(Tmax, Ts[q]);
-    }
+    const int T = seq < X.nseq ? r.frames[seq] : 0;
+    const long long r0 = seq < X.nseq ? r.row0[seq] : 0;
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const int rs = nsl * 64;  // stored rows are in slice order: contiguous, whole lines
     const float leaky = r.leaky;
-    auto astore = [&](int q) { return r.alpha_store + (size_t)(unit * NS + q) * (r.max_frames + 1) * rs; };
-    auto asum = [&](int q) { return r.asum_store + (size_t)(unit * NS + q) * (r.max_frames + 1); };
+    float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rs;
+    float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
 
-    const bool scaled = NS == 1 && g.f.arc_s != nullptr;
-    SellDev tf = g.f;
-    if (scaled) tf.arc = g.f.arc_s;
-    const SellLds F = stage_sell(tf, gi, G, nk, sbase, X.cache_f);
+    const bool scaled = g.f.arc_s != nullptr;
+    const uint2 *arcs = scaled ? g.f.arc_s : g.f.arc;
+    const SellLds F = stage_sell(g.f, X.lgG, gi, spg, sbase);
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
     const float as0 = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
-    float as[NS];
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        as[q] = as0;
-        for (int s = tid; s < S; s += DEN_THREADS) va[q * S + s] = g.init[s] + as0 * leaky * g.init[s];
-        if (gi == 0 && unit * NS + q < X.nseqs) {
-            float *a0 = astore(q);
-            for (int c = tid; c < rs; c += DEN_THREADS)
-                __builtin_nontemporal_store(F.initp[c] + as0 * leaky * F.initp[c], a0 + c);
-            if (tid == 0) {
-                asum(q)[0] = as0;
-                r.stats[(size_t)(unit * NS + q) * 8 + 3] = 0.0f;  // accumulated by k_den_post
-                r.stats[(size_t)(unit * NS + q) * 8 + 6] = 0.0f;
-            }
+    float as = as0;
+    for (int s = tid; s < S; s += DEN_THREADS) va[s] = g.init[s] + as0 * leaky * g.init[s];
+    if (gi == 0 && seq < X.nseq) {
+        for (int c = tid; c < rs; c += DEN_THREADS)
+            __builtin_nontemporal_store(F.initp[c] + as0 * leaky * F.initp[c], astore + c);
+        if (tid == 0) {
+            asum[0] = as0;
+            r.stats[(size_t)seq * 8 + 3] = 0.0f;  // accumulated by k_den_post
+            r.stats[(size_t)seq * 8 + 6] = 0.0f;
         }
     }
-    RowPre<XT> pre[NS];
+    RowPre<XT> pre;
+    if (T > 0) {
+        pre.fetch(nnet + r0 * r.ld, P);
 #pragma unroll
-    for (int q = 0; q < NS; ++q)
-        if (Ts[q] > 0) {
-            pre[q].fetch(nnet + r0[q] * r.ld, P);
+        for (int i = 0; i < DEN_MAXPT; ++i) {
+            int p = tid + i * DEN_THREADS;
+            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));  // kernel_apply_exp
+        }
+    }
+    __syncthreads();
+    const bool tr = r.trace && seq == 0 && gi == 0 && tid == 0;
+#define DEN_TP(i) \
+    if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
+    for (int t = 0; t < T; ++t) {
+        DEN_TP(0);
+        const int buf = (t + 1) & 1;
+        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        const float inv = as > 0.0f ? 1.0f / as : 1.0f;
+        float pq = 0.f;
+        auto term = [&](int src, int pdf, float tp) { return va[src] * tp * xe[pdf]; };
+        auto term_s = [&](int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
+        for (int k = wave; k < spg; k += DEN_WAVES) {
+            const int j = F.slot[k];
+            if (j < 0) continue;
+            const int st = F.perm[j * 64 + lane];
+            const float acc = scaled ? sell_slice(arcs, F.len[j], F.off[j], lane, term_s)
+                                     : sell_slice(arcs, F.len[j], F.off[j], lane, term);
+            const float v = st >= 0 ? acc * inv : 0.0f;
+            st_sc1(blk + k * 64 + lane, v);
+            pq += v;
+        }
+        DEN_TP(1);
+        den_publish(X, blk + spg * 64, wave_sum(pq), seq);
+        DEN_TP(2);
+        // the next frame's output row: fetched after the publish, so its latency hides under
+        // the exchange wait (fetched at the frame start, the record loads' in-order vmcnt
+        // waits queue behind it: frame 13.3 -> 15.3 us)
+        if (t + 1 < T) pre.fetch(nnet + (r0 + (long long)(t + 1) * r.stride) * r.ld, P);
+        DEN_TP(3);
+        if (!den_wait(X, seq, (unsigned)(G * (t + 1)), flag)) return;
+        DEN_TP(4);
+        float as1 = 0.f;
+        DEN_TP(5);
+        den_consume(X, seq, buf, nsl, F.own, F.perm, F.initp, [&](float v) { as1 = v; },
+                    [&](int st, float v, float ip, int owner, int c) {
+                        const float a = v + as1 * leaky * ip;
+                        va[st] = a;
+                        if (owner == gi)  // keep L2 for the arcs
+                            __builtin_nontemporal_store(a, astore + (size_t)(t + 1) * rs + c);
+                    });
+        DEN_TP(6);
+        // past the publish barrier nothing reads this frame's xe
+        if (t + 1 < T) {
 #pragma unroll
             for (int i = 0; i < DEN_MAXPT; ++i) {
                 int p = tid + i * DEN_THREADS;
-                if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));  // kernel_apply_exp
+                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
             }
         }
-    __syncthreads();
-    const bool tr = r.trace && unit == 0 && gi == 0 && tid == 0;
-#define DEN_TP(i) \
-    if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
-    // the next frame's output row is fetched at the start of each frame, so its latency
-    // hides under the arc phase (the first slices come from the LDS record cache, so the
-    // record loads' vmcnt waits do not queue behind it); KF_DEN_EARLY=0: after publish
-    const bool early = (r.early & 1) != 0, xe_early = early && (r.early & 2);
-    for (int t = 0; t < Tmax; ++t) {
-        DEN_TP(0);
-        if (early) {
-#pragma unroll
-            for (int q = 0; q < NS; ++q)
-                if (t + 1 < Ts[q]) pre[q].fetch(nnet + (r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
-        }
-        const int buf = (t + 1) & 1;
-        float *blk = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
-        float inv[NS], pq[NS];
-        bool live[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            live[q] = t < Ts[q];
-            inv[q] = as[q] > 0.0f ? 1.0f / as[q] : 1.0f;
-            pq[q] = 0.f;
-        }
-        auto term = [&](int q, int src, int pdf, float tp) { return va[q * S + src] * tp * xe[q * PP + pdf]; };
-        auto term_s = [&](int, int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
-        for (int k = wave; k < nk; k += DEN_WAVES) {
-            const int j = gi + G * k;
-            const int st = F.perm[j * 64 + lane];
-            float acc[NS];
-            if (scaled) {
-                if (k < F.kc) sell_slice_ns<NS>(F.cache, F.len[j], F.coff[k], lane, acc, term_s);
-                else sell_slice_ns<NS>(tf.arc, F.len[j], F.off[j], lane, acc, term_s);
-            } else if (k < F.kc) {
-                sell_slice_ns<NS>(F.cache, F.len[j], F.coff[k], lane, acc, term);
-            } else {
-                sell_slice_ns<NS>(g.f.arc, F.len[j], F.off[j], lane, acc, term);
-            }
-#pragma unroll
-            for (int q = 0; q < NS; ++q) {
-                const float v = (st >= 0 && live[q]) ? acc[q] * inv[q] : 0.0f;
-                st_sc1(blk + (size_t)q * X.spg * 64 + k * 64 + lane, v);
-                pq[q] += v;
-            }
-        }
-        DEN_TP(1);
-        float wsum[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) wsum[q] = wave_sum(pq[q]);
-        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, wsum, unit);
-        DEN_TP(2);
-        // past the publish barrier nothing reads this frame's xe: with the row fetched at the
-        // frame start, the next frame's exp(x) is written while the partner's slices travel
-        auto next_xe = [&]() {
-#pragma unroll
-            for (int q = 0; q < NS; ++q)
-                if (t + 1 < Ts[q]) {
-#pragma unroll
-                    for (int i = 0; i < DEN_MAXPT; ++i) {
-                        int p = tid + i * DEN_THREADS;
-                        if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));
-                    }
-                }
-        };
-        if (xe_early) next_xe();
-        if (!early) {
-#pragma unroll
-            for (int q = 0; q < NS; ++q)
-                if (t + 1 < Ts[q]) pre[q].fetch(nnet + (r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
-        }
-        DEN_TP(3);
-        if (!den_wait(X, unit, (unsigned)(G * (t + 1)), flag)) return;
-        DEN_TP(4);
-        float as1[NS];
-        DEN_TP(5);
-        den_consume<NS>(X, unit, buf, nsl, F.perm, F.initp, [&](int q, float v) { as1[q] = v; },
-                        [&](int q, int st, float v, float ip, int owner, int c) {
-                            if (!live[q]) return;
-                            const float a = v + as1[q] * leaky * ip;
-                            va[q * S + st] = a;
-                            if (owner == gi)  // keep L2 for the arcs
-                                __builtin_nontemporal_store(a, astore(q) + (size_t)(t + 1) * rs + c);
-                        });
-        DEN_TP(6);
-        if (!xe_early) next_xe();
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            if (live[q]) {
-                if (gi == 0 && tid == 0) asum(q)[t + 1] = as1[q];
-                as[q] = as1[q];
-            }
-        }
+        if (gi == 0 && tid == 0) asum[t + 1] = as1;
+        as = as1;
         __syncthreads();
         DEN_TP(7);
     }
 #undef DEN_TP
-    if (gi != 0) return;
+    if (gi != 0 || seq >= X.nseq) return;
     // total_prob = sum(alpha'[T]); log_correction = sum_{t<T} log(alpha_sum[t])
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        const int sq = unit * NS + q;
-        if (sq >= X.nseqs) break;
-        part = 0.f;
-        for (int s = tid; s < S; s += DEN_THREADS) part += va[q * S + s];
-        const float total = block_sum<DEN_WAVES>(part, red);
-        double lc = 0.0;
-        for (int t = tid; t < Ts[q]; t += DEN_THREADS) {
-            float a = asum(q)[t];
-            if (a > 0.0f) lc += log((double)a);
-        }
-        double *redd = reinterpret_cast<double *>(smem) + 8;  // red[16..31]
-        __syncthreads();
-        lc = block_sum_d<DEN_WAVES>(lc, redd);
-        if (tid == 0) {
-            r.den_out[sq * 2 + 0] = total;
-            r.den_out[sq * 2 + 1] = (float)(log((double)total) + lc);
-            r.stats[(size_t)sq * 8 + 1] = r.den_out[sq * 2 + 1];
-        }
-        __syncthreads();
+    part = 0.f;
+    for (int s = tid; s < S; s += DEN_THREADS) part += va[s];
+    const float total = block_sum<DEN_WAVES>(part, red);
+    double lc = 0.0;
+    for (int t = tid; t < T; t += DEN_THREADS) {
+        float a = asum[t];
+        if (a > 0.0f) lc += log((double)a);
+    }
+    double *redd = reinterpret_cast<double *>(smem) + 8;  // red[16..31]
+    __syncthreads();
+    lc = block_sum_d<DEN_WAVES>(lc, redd);
+    if (tid == 0) {
+        r.den_out[seq * 2 + 0] = total;
+        r.den_out[seq * 2 + 1] = (float)(log((double)total) + lc);
+        r.stats[(size_t)seq * 8 + 1] = r.den_out[seq * 2 + 1];
     }
 }
 template <typename XT>
@@ -940,151 +831,97 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int seq, gi;
     den_map(X, seq, gi);
-    den_fwd_body<XT, 1>(g, r, X, smem, seq, gi);
+    den_fwd_body<XT>(g, r, X, smem, seq, gi);
 }
 
 // Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per
-// unit: beta'[t] over the source rows of this block's slices (exchanged),
+// sequence: beta'[t] over the source rows of this block's slices (exchanged),
 // beta[t] = beta'[t] + leaky*<init, beta'[t]>; beta[t] for t >= 1 goes to HBM for
 // k_den_post. The reference scales beta'[t] by 1/sum(alpha[t]) and starts from
 // 1/total_prob; any positive per-frame factor gives the same posteriors once
 // k_den_post normalises each frame (the den posteriors of a frame sum to one:
 // they are d log p / d x_t), so this pass scales by 1/<init, beta'[t+1]> and
 // starts from ones — it needs nothing from the forward pass and runs beside it.
-// Ragged units run from the longest sequence's last frame; a shorter sequence
-// joins at its own last frame.
-template <typename XT, int NS>
+template <typename XT>
 __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, const DenX &X,
-                                             unsigned char *smem, int unit, int gi) {
+                                             unsigned char *smem, int seq, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int G = X.G, nsl = g.b.nsl;
+    const int G = X.G, nsl = g.b.nsl, spg = X.spg;
     const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);      // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;    // [32]
-    float *vb = reinterpret_cast<float *>(smem) + 64;  // [NS][S] beta[t+1]
-    float *xe = vb + NS * S;                           // [NS][PP] exp(clamp(x))
-    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
-    const int nk = (nsl - gi + G - 1) / G;
+    float *vb = reinterpret_cast<float *>(smem) + 64;  // [S] beta[t+1]
+    float *xe = vb + S;                                // [PP] exp(clamp(x))
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + PP);
 
-    int Ts[NS];
-    long long r0[NS];
-    int Tmax = 0;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        const int sq = unit * NS + q;
-        Ts[q] = sq < X.nseqs ? r.frames[sq] : 0;
-        r0[q] = sq < X.nseqs ? r.row0[sq] : 0;
-        Tmax = max(Tmax, Ts[q]);
-    }
+    const int T = seq < X.nseq ? r.frames[seq] : 0;
+    const long long r0 = seq < X.nseq ? r.row0[seq] : 0;
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const int rs = nsl * 64;
-    auto bstore = [&](int q) { return r.beta_store + (size_t)(unit * NS + q) * (r.max_frames + 1) * rs; };
+    float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rs;
     const float leaky = r.leaky;
 
-    const bool scaled = NS == 1 && g.b.arc_s != nullptr;
-    SellDev tbl = g.b;
-    if (scaled) tbl.arc = g.b.arc_s;
-    const SellLds B = stage_sell(tbl, gi, G, nk, sbase, X.cache_b);
+    const bool scaled = g.b.arc_s != nullptr;
+    const uint2 *arcs = scaled ? g.b.arc_s : g.b.arc;
+    const SellLds B = stage_sell(g.b, X.lgG, gi, spg, sbase);
     // BetaDashLastFrame up to the per-frame factor: beta'[T] = 1, <init, 1> = sum(init)
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
     const float n0 = block_sum<DEN_WAVES>(part, red);
-    float nrm[NS];
-    RowPre<XT> pre[NS];
+    float nrm = n0;
+    RowPre<XT> pre;
+    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = 1.0f + leaky * n0;
+    if (gi == 0 && seq < X.nseq) {
+        float *bT = bstore + (size_t)T * rs;
+        for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(1.0f + leaky * n0, bT + c);
+    }
+    if (T > 0) {
+        pre.fetch(nnet + (r0 + (long long)(T - 1) * r.stride) * r.ld, P);
 #pragma unroll
-    for (int q = 0; q < NS; ++q) {
-        nrm[q] = n0;
-        for (int s = tid; s < S; s += DEN_THREADS) vb[q * S + s] = 1.0f + leaky * n0;
-        if (gi == 0 && unit * NS + q < X.nseqs) {
-            float *bT = bstore(q) + (size_t)Ts[q] * rs;
-            for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(1.0f + leaky * n0, bT + c);
-        }
-        if (Ts[q] > 0) {
-            pre[q].fetch(nnet + (r0[q] + (long long)(Ts[q] - 1) * r.stride) * r.ld, P);
-#pragma unroll
-            for (int i = 0; i < DEN_MAXPT; ++i) {
-                int p = tid + i * DEN_THREADS;
-                if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));
-            }
+        for (int i = 0; i < DEN_MAXPT; ++i) {
+            int p = tid + i * DEN_THREADS;
+            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
         }
     }
     __syncthreads();
-    const bool early = (r.early & 1) != 0, xe_early = early && (r.early & 2);  // as den_fwd_body
-    for (int t = Tmax - 1, it = 0; t >= 0; --t, ++it) {
-        if (early) {
-#pragma unroll
-            for (int q = 0; q < NS; ++q)
-                if (t < Ts[q] && t > 0) pre[q].fetch(nnet + (r0[q] + (long long)(t - 1) * r.stride) * r.ld, P);
-        }
+    for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
         const int buf = t & 1;
-        float *blk = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
-        float inv[NS], pq[NS];
-        bool live[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            live[q] = t < Ts[q];
-            inv[q] = nrm[q] > 0.0f ? 1.0f / nrm[q] : 1.0f;
-            pq[q] = 0.f;
-        }
-        auto term = [&](int q, int dst, int pdf, float tp) { return vb[q * S + dst] * tp * xe[q * PP + pdf]; };
-        auto term_s = [&](int, int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
-        for (int k = wave; k < nk; k += DEN_WAVES) {  // kernel_den_backward_transitions
-            const int j = gi + G * k;
+        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        const float inv = nrm > 0.0f ? 1.0f / nrm : 1.0f;
+        float pq = 0.f;
+        auto term = [&](int dst, int pdf, float tp) { return vb[dst] * tp * xe[pdf]; };
+        auto term_s = [&](int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
+        for (int k = wave; k < spg; k += DEN_WAVES) {  // kernel_den_backward_transitions
+            const int j = B.slot[k];
+            if (j < 0) continue;
             const int st = B.perm[j * 64 + lane];
-            float acc[NS];
-            if (scaled) {
-                if (k < B.kc) sell_slice_ns<NS>(B.cache, B.len[j], B.coff[k], lane, acc, term_s);
-                else sell_slice_ns<NS>(tbl.arc, B.len[j], B.off[j], lane, acc, term_s);
-            } else if (k < B.kc) {
-                sell_slice_ns<NS>(B.cache, B.len[j], B.coff[k], lane, acc, term);
-            } else {
-                sell_slice_ns<NS>(g.b.arc, B.len[j], B.off[j], lane, acc, term);
-            }
-            const float ipj = B.initp[j * 64 + lane];
+            const float acc = scaled ? sell_slice(arcs, B.len[j], B.off[j], lane, term_s)
+                                     : sell_slice(arcs, B.len[j], B.off[j], lane, term);
+            const float bd = st >= 0 ? acc * inv : 0.0f;
+            st_sc1(blk + k * 64 + lane, bd);
+            pq += B.initp[j * 64 + lane] * bd;
+        }
+        den_publish(X, blk + spg * 64, wave_sum(pq), seq);
+        if (t > 0) pre.fetch(nnet + (r0 + (long long)(t - 1) * r.stride) * r.ld, P);  // as den_fwd_body
+        if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
+        float tb = 0.f;
+        den_consume(X, seq, buf, nsl, B.own, B.perm, B.initp,
+                    [&](float v) {
+                        nrm = v;  // <init, beta'[t]>: the next factor
+                        tb = leaky * nrm;
+                    },
+                    [&](int st, float v, float, int owner, int c) {
+                        const float b = v + tb;
+                        vb[st] = b;
+                        if (t > 0 && owner == gi) __builtin_nontemporal_store(b, bstore + (size_t)t * rs + c);
+                    });
+        if (t > 0) {
 #pragma unroll
-            for (int q = 0; q < NS; ++q) {
-                const float bd = (st >= 0 && live[q]) ? acc[q] * inv[q] : 0.0f;
-                st_sc1(blk + (size_t)q * X.spg * 64 + k * 64 + lane, bd);
-                pq[q] += ipj * bd;
+            for (int i = 0; i < DEN_MAXPT; ++i) {
+                int p = tid + i * DEN_THREADS;
+                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
             }
         }
-        float wsum[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) wsum[q] = wave_sum(pq[q]);
-        den_publish<NS>(X, blk + (size_t)NS * X.spg * 64, wsum, unit);
-        auto next_xe = [&]() {  // as den_fwd_body
-#pragma unroll
-            for (int q = 0; q < NS; ++q) {
-                if (live[q] && t > 0) {
-#pragma unroll
-                    for (int i = 0; i < DEN_MAXPT; ++i) {
-                        int p = tid + i * DEN_THREADS;
-                        if (p < P) xe[q * PP + p] = expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i))));
-                    }
-                }
-            }
-        };
-        if (xe_early) next_xe();
-        if (!early) {
-#pragma unroll
-            for (int q = 0; q < NS; ++q)
-                if (live[q] && t > 0) pre[q].fetch(nnet + (r0[q] + (long long)(t - 1) * r.stride) * r.ld, P);
-        }
-        if (!den_wait(X, unit, (unsigned)(G * (it + 1)), flag)) return;
-        float tb[NS];
-        den_consume<NS>(X, unit, buf, nsl, B.perm, B.initp,
-                        [&](int q, float v) {
-                            if (live[q]) nrm[q] = v;  // <init, beta'[t]>: the next factor
-                            tb[q] = leaky * nrm[q];
-                        },
-                        [&](int q, int st, float v, float, int owner, int c) {
-                            if (!live[q]) return;
-                            const float b = v + tb[q];
-                            vb[q * S + st] = b;
-                            if (t > 0 && owner == gi)
-                                __builtin_nontemporal_store(b, bstore(q) + (size_t)t * rs + c);
-                        });
-        if (!xe_early) next_xe();
         __syncthreads();
     }
 }
@@ -1094,7 +931,7 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
 // passes are independent, see den_bwd_body). One launch keeps all 2*nseq*G blocks
 // co-resident, which the bounded exchange polls rely on; the XCD grouping of
 // den_map is kept (G consecutive ids share an XCD).
-template <typename XT, int NS>
+template <typename XT>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const DenRun r, const DenX XF,
                                                         const DenX XB) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1103,9 +940,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
     if (nb % 8 == 0 && (nb / 8) % XF.G == 0) w = (b % 8) * (nb / 8) + b / 8;
     const bool bwd = w >= half;
     const int inner = bwd ? w - half : w;
-    const int unit = inner >> XF.lgG, gi = inner & (XF.G - 1);
-    if (bwd) den_bwd_body<XT, NS>(g, r, XB, smem, unit, gi);
-    else den_fwd_body<XT, NS>(g, r, XF, smem, unit, gi);
+    const int seq = inner >> XF.lgG, gi = inner & (XF.G - 1);
+    if (bwd) den_bwd_body<XT>(g, r, XB, smem, seq, gi);
+    else den_fwd_body<XT>(g, r, XF, smem, seq, gi);
 }
 
 // Posteriors (kernel_den_posteriors, chain_den.cu:253-280) for every (sequence,
@@ -1210,7 +1047,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
         float gpart[PAIR];
 #pragma unroll
         for (int f = 0; f < PAIR; ++f) gpart[f] = 0.f;
-        for (int j = wave; j < nslq; j += DEN_WAVES) {
+        for (int k = wave; k < g.q.spg[0]; k += DEN_WAVES) {
+            const int j = g.q.slot[0][k];
+            if (j < 0) continue;
             const int pdf = permq[j * 64 + lane];
             float acc[PAIR];
             post_slice<PAIR>(g.q.arc, lenq[j], offq[j], lane, va, vb, S, acc);
@@ -1341,8 +1180,7 @@ Sell build_sell(int nrows, int A, const int32_t *key, const int32_t *f1, const i
     // 32-lane half-wave, the two LDS gathers (f1 and f2 indices) fall in distinct
     // banks ((index) mod 32 for ds_read_b32) as far as possible; padding records
     // (tp = 0) take indices of free banks. Summation order per row changes, but
-    // stays fixed. KF_SELL_PLAIN=1 keeps plain arc order.
-    const bool plain = getenv("KF_SELL_PLAIN") && atoi(getenv("KF_SELL_PLAIN"));
+    // stays fixed.
     for (int j = 0; j < nsl; ++j) {
         for (int half = 0; half < 2; ++half) {
             std::vector<std::vector<int>> rem(32);
@@ -1363,8 +1201,7 @@ Sell build_sell(int nrows, int A, const int32_t *key, const int32_t *f1, const i
                     if (!rem[l].empty()) {
                         size_t best = 0;
                         int bestc = 3;
-                        if (!plain)
-                            for (size_t q = 0; q < rem[l].size() && bestc > 0; ++q) {
+                        for (size_t q = 0; q < rem[l].size() && bestc > 0; ++q) {
                                 const int a = rem[l][q];
                                 int c = (used1[f1[a] & 31] ? 1 : 0) + (used2[f2[a] & 31] ? 1 : 0);
                                 if (c < bestc) {
@@ -1378,7 +1215,7 @@ Sell build_sell(int nrows, int A, const int32_t *key, const int32_t *f1, const i
                         uint32_t tpu;
                         memcpy(&tpu, &tp[a], 4);
                         rec = make_uint2((uint32_t)f1[a] | ((uint32_t)f2[a] << 16), tpu);
-                    } else if (!plain) {  // padding: valid indices on free banks
+                    } else {  // padding: valid indices on free banks
                         const int m1 = std::min(32, n1) - 1, m2 = std::min(32, n2) - 1;
                         int b1 = 0, b2 = 0;
                         while (b1 < m1 && used1[b1]) ++b1;
@@ -1404,9 +1241,37 @@ T *dev_upload(const std::vector<T> &v, std::vector<void *> &owned) {
     return (T *)p;
 }
 
-static int den_early() {
-    static const int v = getenv("KF_DEN_EARLY") ? atoi(getenv("KF_DEN_EARLY")) : 1;
-    return v;
+// Slice ownership of SellDev::slot / own for G blocks of DEN_WAVES waves: longest
+// slice first onto the least loaded (block, wave) pair (a slice costs its rows plus a
+// fixed 4 for its per-slice work); bin b is block b % G, wave b / G, so the largest
+// slices also spread over the blocks.
+void den_balance(const std::vector<int> &len, int G, std::vector<int> &slot, std::vector<int> &own, int &spg) {
+    const int nsl = (int)len.size(), bins = G * DEN_WAVES;
+    std::vector<int> order(nsl);
+    for (int j = 0; j < nsl; ++j) order[j] = j;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return len[a] > len[b]; });
+    std::vector<long long> load(bins, 0);
+    std::vector<std::vector<int>> lists(bins);
+    for (int j : order) {
+        int b = 0;
+        for (int i = 1; i < bins; ++i)
+            if (load[i] < load[b]) b = i;
+        lists[b].push_back(j);
+        load[b] += len[j] + 4;
+    }
+    size_t maxc = 1;
+    for (auto &l : lists) maxc = std::max(maxc, l.size());
+    spg = (int)maxc * DEN_WAVES;
+    slot.assign((size_t)G * spg, -1);
+    own.assign(nsl, 0);
+    for (int b = 0; b < bins; ++b) {
+        const int gi = b % G, w = b / G;
+        for (size_t i = 0; i < lists[b].size(); ++i) {
+            const int k = w + DEN_WAVES * (int)i, j = lists[b][i];
+            slot[(size_t)gi * spg + k] = j;
+            own[j] = (gi << 16) | k;
+        }
+    }
 }
 
 struct DenTables {
@@ -1432,7 +1297,7 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         return nullptr;
     }
     if (den_post_lds_bytes(S, P, (P + 63) / 64) > DEN_LDS_TOTAL ||
-        den_rec_fixed_bytes(S, P, (S + 63) / 64) > DEN_LDS_TOTAL || S > DEN_MAXS * DEN_THREADS) {
+        den_rec_fixed_bytes(S, P, (S + 63) / 64, (S + 63) / 64) > DEN_LDS_TOTAL || S > DEN_MAXS * DEN_THREADS) {
         *why = "den graph too large for the LDS-resident kernels (S <= 8192, ~12*S + 14*P B)";
         return nullptr;
     }
@@ -1450,21 +1315,36 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
     d.S = S;
     d.P = P;
     bool ok = true;
-    auto put = [&](SellDev &o, const Sell &h) {
+    auto put = [&](SellDev &o, const Sell &h, int ngs) {
         o.nsl = (int)h.len.size();
         o.perm = dev_upload(h.perm, t->owned);
         o.len = dev_upload(h.len, t->owned);
         o.off = dev_upload(h.off, t->owned);
         o.arc = dev_upload(h.arcs, t->owned);
         ok = ok && o.perm && o.len && o.off && o.arc;
+        for (int lg = 0; lg < 4; ++lg) {
+            o.slot[lg] = o.own[lg] = nullptr;
+            o.spg[lg] = 0;
+            if (lg >= ngs) continue;
+            std::vector<int> slot, own;
+            den_balance(h.len, 1 << lg, slot, own, o.spg[lg]);
+            o.slot[lg] = dev_upload(slot, t->owned);
+            o.own[lg] = dev_upload(own, t->owned);
+            ok = ok && o.slot[lg] && o.own[lg];
+        }
     };
-    put(d.f, sf);
-    put(d.b, sb);
-    put(d.q, sq);
+    put(d.f, sf, 4);
+    put(d.b, sb, 4);
+    put(d.q, sq, 1);
+    for (int lg = 0; lg < 4 && ok; ++lg)
+        if (den_rec_fixed_bytes(S, P, d.f.nsl, std::max(d.f.spg[lg], d.b.spg[lg])) > DEN_LDS_TOTAL) {
+            delete t;
+            *why = "den graph too large for the LDS-resident kernels (slice lists)";
+            return nullptr;
+        }
     // pre-scaled copies for the NS = 1 recursions: value row at byte 256 (64 floats of
     // reduction scratch before it), exp row at 256 + 4 S (den_fwd_body / den_bwd_body)
     const bool fit16 = 256 + 4 * ((size_t)S + P + 1) < 65536;
-    const bool want_s = !getenv("KF_DEN_SCALED") || atoi(getenv("KF_DEN_SCALED"));
     auto scaled = [&](const Sell &h) {
         std::vector<uint2> a(h.arcs);
         for (auto &r : a) {
@@ -1473,7 +1353,7 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         }
         return a;
     };
-    if (fit16 && want_s) {
+    if (fit16) {
         d.f.arc_s = dev_upload(scaled(sf), t->owned);
         d.b.arc_s = dev_upload(scaled(sb), t->owned);
         ok = ok && d.f.arc_s && d.b.arc_s;
@@ -1529,10 +1409,6 @@ int den_pick_G(int nseq) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 1;
     }
-    if (const char *e = getenv("KF_DEN_G")) {
-        int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4 || v == 8) return (nseq * v <= cus) ? v : 1;
-    }
     for (int G = 4; G > 1; G /= 2)
         if (nseq * G <= cus) return G;
     return 1;
@@ -1547,28 +1423,16 @@ struct DenXBuf {
         if (buf) hipFree(buf);
         if (cnt) hipFree(cnt);
     }
-    // nseq sequences in units of ns (ns = 1 or 2 sequences per block)
-    bool make(const DenDev &g, int nseq, int G, DenX &X, int ns = 1) {
+    // nseq sequences, G blocks each, over table `tb` (the f table for the forward
+    // recursion, b for the backward)
+    bool make(const DenDev &g, const SellDev &tb, int nseq, int G, DenX &X) {
         X.G = G;
-        X.ns = ns;
-        X.nseqs = nseq;
-        X.nseq = (nseq + ns - 1) / ns;
+        X.nseq = nseq;
         X.lgG = G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
-        X.spg = (g.f.nsl + G - 1) / G;
-        X.blk = ns * X.spg * 64 + 64;
-        const size_t fixed_f = den_rec_fixed_bytes(g.S, g.P, g.f.nsl, ns);
-        const size_t fixed_b = den_rec_fixed_bytes(g.S, g.P, g.b.nsl, ns);
-        // resident arc records are opt-in (KF_DEN_CACHE=1): measured on MI355X they do not
-        // shorten the recursion (it is bound by the LDS gathers, not the L2 stream) and the
-        // full-LDS request keeps the numerator kernel off those CUs
-        X.cache_f = X.cache_b = 0;
-        if (const char *e = getenv("KF_DEN_CACHE"))
-            if (atoi(e)) {
-                X.cache_f = fixed_f < DEN_LDS_TOTAL ? (unsigned)(DEN_LDS_TOTAL - fixed_f) : 0u;
-                X.cache_b = fixed_b < DEN_LDS_TOTAL ? (unsigned)(DEN_LDS_TOTAL - fixed_b) : 0u;
-            }
-        X.lds_f = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_f + X.cache_f);
-        X.lds_b = (unsigned)std::min<size_t>(DEN_LDS_TOTAL, fixed_b + X.cache_b);
+        X.spg = tb.spg[X.lgG];
+        X.blk = X.spg * 64 + 64;
+        X.lds_f = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.f.nsl, g.f.spg[X.lgG]);
+        X.lds_b = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.b.nsl, g.b.spg[X.lgG]);
         size_t nb = (size_t)X.nseq * 2 * G * X.blk * 4;
         size_t nc = (((size_t)X.nseq + 2) * 4 + 15) / 16 * 16;  // sticky, timeout, counters
         if (nb > buf_cap) {
@@ -1632,20 +1496,13 @@ void launch_den_fb(const DenDev &g, const DenRun &r, const DenX &XF, DenXBuf &xf
     xbb.zero(st);
     dim3 grid(2 * XF.nseq * XF.G);
     const size_t lds = std::max(XF.lds_f, XB.lds_b);
-#define KF_FB(XT_, NS_) hipLaunchKernelGGL((k_den_fb<XT_, NS_>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB)
-    if (XF.ns == 2) {
-        if (fp32_in) KF_FB(float, 2);
-        else KF_FB(h16, 2);
-    } else {
-        if (fp32_in) KF_FB(float, 1);
-        else KF_FB(h16, 1);
-    }
-#undef KF_FB
+    if (fp32_in) hipLaunchKernelGGL((k_den_fb<float>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
+    else hipLaunchKernelGGL((k_den_fb<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
 }
 void launch_den_post(const DenDev &g, const DenRun &r, const DenX &X, bool fp32_in, int mode) {
     hipStream_t st = kf_stream();
     const int nfb = (r.max_frames + POST_FRAMES - 1) / POST_FRAMES;
-    dim3 pgrid(X.nseqs * nfb);
+    dim3 pgrid(X.nseq * nfb);
     // frame pairs share the arc stream when both frames' alpha/beta fit in LDS
     const bool pair = den_post_lds_bytes(g.S, g.P, g.q.nsl, 2) <= DEN_LDS_TOTAL;
     size_t plds = den_post_lds_bytes(g.S, g.P, g.q.nsl, pair ? 2 : 1);
@@ -2326,7 +2183,7 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     DenX X{}, XB{};
     DenXBuf xbuf, xbuf2;
     const int G = h_post ? den_pick_G(2) : den_pick_G(1);
-    if (!xbuf.make(g, 1, G, X) || (h_post && !xbuf2.make(g, 1, G, XB))) {
+    if (!xbuf.make(g, g.f, 1, G, X) || (h_post && !xbuf2.make(g, g.b, 1, G, XB))) {
         den_set_error("den_forward: hipMalloc failed");
         return -1e30f;
     }
@@ -2692,19 +2549,10 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
     double bytes = frames * (3.0 * 8.0 * c->den->num_arcs + 8.0 * dd.S + 6.0 * dd.P);
     int pd = kf_prof_start(KF_PROF_CHAIN_DEN, bytes);
     DenX X{}, XB{};
-    // forward and backward blocks share the CUs. KF_DEN_NS=2 puts two sequences in a
-    // block (G = 4), sharing every arc record read; measured on MI355X it is slower
-    // (11.6 vs 9.3 ms for 64 sequences: the G = 4 exchange and doubled LDS gathers cost
-    // more than the halved record stream), so one sequence per block is the default
-    int ns = 1, G = den_pick_G(2 * nseq);
-    {
-        static const int want = getenv("KF_DEN_NS") ? atoi(getenv("KF_DEN_NS")) : 1;
-        const int units = (nseq + 1) / 2;
-        if (want == 2 && nseq >= 2 && den_pick_G(2 * units) == 4 &&
-            den_rec_fixed_bytes(dd.S, dd.P, dd.f.nsl, 2) <= DEN_LDS_TOTAL)
-            ns = 2, G = 4;
-    }
-    if (!c->xbuf.make(dd, nseq, G, X, ns) || !c->xbuf2.make(dd, nseq, G, XB, ns)) {
+    // forward and backward blocks share the CUs (two sequences sharing each record
+    // read, G = 4, measured slower in r02: 11.6 vs 9.3 ms for 64 sequences)
+    const int G = den_pick_G(2 * nseq);
+    if (!c->xbuf.make(dd, dd.f, nseq, G, X) || !c->xbuf2.make(dd, dd.b, nseq, G, XB)) {
         kfc_set_error("kf_chain_compute: hipMalloc failed");
         return -1;
     }

@@ -79,11 +79,17 @@ __device__ __forceinline__ long long op_off(const OpD &d, int t, int h, int kk, 
 constexpr int BK = 64;
 // k-contiguous [rows][64] halves: 16-byte chunk c of row r at slot c ^ ((r>>1)&7)
 __device__ __forceinline__ int kc_off(int r, int c) { return r * 128 + 16 * (c ^ ((r >> 1) & 7)); }
-// reduction-major [64][W] halves: 8-byte unit u of row r at u ^ swz(r)
+// reduction-major [64][W] halves: 8-byte unit u of row r at u ^ swz(r). One
+// ds_read_b64_tr_b16 reads rows {8g + q (+4)} x 4 units in each 32-lane group; the
+// swizzle spreads those 8 rows over all 64 banks for the row stride's residue:
+// W/2 dwords = 0 (mod 64) needs 8 distinct 4-unit blocks, 32 (mod 64) 4 distinct 4-unit
+// blocks per half-bank set, 16 (mod 32) one block flip (checked offline for every tile
+// width in use: 64 ... 384; the W = 192 / 320 / 384 wgrad tiles were 2-4-way conflicted
+// under the W % 32 rule, SQ_LDS_BANK_CONFLICT 0.31-0.62 of their LDS cycles)
 template <int W>
 __device__ __forceinline__ int mn_swz(int r) {
-    if constexpr (W == 64) return ((r & 2) << 1) ^ (((r >> 3) & 1) << 3);
-    else if constexpr (W == 128 || W == 256) return ((r & 3) << 2) ^ (((r >> 3) & 1) << 4);
+    if constexpr (W % 128 == 0) return ((r & 3) << 2) ^ (((r >> 3) & 1) << 4);
+    else if constexpr (W % 64 == 0) return ((r & 2) << 1) ^ (((r >> 3) & 1) << 3);
     else if constexpr (W % 32 == 0) return ((r >> 3) & 1) << 2;
     else return 0;
 }

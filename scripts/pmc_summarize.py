@@ -39,17 +39,22 @@ def load(d, counter):
     return per
 
 
-root = sys.argv[1]
-fetch = load(os.path.join(root, "fetch"), "FETCH_SIZE")
-write = load(os.path.join(root, "write"), "WRITE_SIZE")
-out = {}
-for k in sorted(set(fetch) | set(write)):
-    f, w = fetch.get(k, []), write.get(k, [])
-    n = max(len(f), len(w))
-    if not n:
-        continue
-    fb = 2.0 * 1024 * sum(f) / max(len(f), 1)
-    wb = 1024.0 * sum(w) / max(len(w), 1)
-    out[k] = {"launches": n, "read_bytes_per_launch": fb, "write_bytes_per_launch": wb,
-              "hbm_bytes_per_launch": fb + wb}
-print(json.dumps(out, indent=1))
+def main():
+    root = sys.argv[1]
+    fetch = load(os.path.join(root, "fetch"), "FETCH_SIZE")
+    write = load(os.path.join(root, "write"), "WRITE_SIZE")
+    out = {}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, []), write.get(k, [])
+        n = max(len(f), len(w))
+        if not n:
+            continue
+        fb = 2.0 * 1024 * sum(f) / max(len(f), 1)
+        wb = 1024.0 * sum(w) / max(len(w), 1)
+        out[k] = {"launches": n, "read_bytes_per_launch": fb, "write_bytes_per_launch": wb,
+                  "hbm_bytes_per_launch": fb + wb}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
