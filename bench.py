@@ -289,6 +289,54 @@ def config1_affine(threads, reps=50):
             "gpu_vs_cpu_max_rel_err": round(err, 5)}
 
 
+def dropin_forward(a, reps=3):
+    """The drop-in path timed beside the fused one: the reference's own
+    Network.Forward host sequence over the per-op C-ABI (kfp16.refpath: ops_gemm,
+    K = 1-GEMM AddBias, ops_relu, ops_batchnorm_forward, ops_copy / ops_concat_cols
+    splices, ops_add_scaled) against nnet_forward on the same layers and input. Both run
+    the TDNN-F stack of cnn_tdnn_17f (tdnnf7 ... output, fed a [T x 2560] input in place
+    of cnn6's activation: the reference's conv front end im2cols on the host,
+    forward.go:435-456, which would time the host, not the ABI) at 64 egs."""
+    import kfp16
+    from kfp16 import refpath, synth
+    text = synth.load_xconfig("cnn_tdnn_17f.xconfig").splitlines()
+    k = next(i for i, l in enumerate(text) if "name=tdnnf7" in l)
+    xcfg = "\n".join(["input name=input dim=2560"] + text[k:]) + "\n"
+    T = a.egs * FRAMES_PER_EG
+    net = kfp16.Network(xcfg, max_frames=T)
+    params, bns = synth.init_network(net, seed=42)
+    rp = refpath.RefPathForward(xcfg, params, bns, T)
+    x = (torch.randn(T, 2560, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) * 0.5).half()
+    st = torch.cuda.current_stream()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / reps
+    ms_fused = timed(lambda: net.forward(x.data_ptr(), T))
+    ms_ref = timed(lambda: rp.forward(x.data_ptr(), T))
+    got = rp.read("output").astype(np.float32)
+    ref = net.read_activation("output").astype(np.float32)
+    err = float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30))
+    n_ops = rp.ncalls
+    rp.close()
+    net.close()
+    return {"workload": f"tdnnf7 ... output of cnn_tdnn_17f, forward, {a.egs} egs x 1500 frames",
+            "dropin_per_op_abi_ms": round(ms_ref, 3), "dropin_frames_per_sec": round(T / (ms_ref * 1e-3), 1),
+            "fused_nnet_forward_ms": round(ms_fused, 3), "fused_frames_per_sec": round(T / (ms_fused * 1e-3), 1),
+            "speedup_fused_over_dropin": round(ms_ref / ms_fused, 2), "abi_calls_per_forward": n_ops,
+            "output_rel_fro_dropin_vs_fused": round(err, 5),
+            "path": "kfp16.refpath: forward.go:589-1001's ABI sequence (spliceBackward / spliceForward by "
+                    "ops_copy + ops_concat_cols, ops_gemm, AddBias as the K = 1 ops_gemm of ops.go:335, ops_relu, "
+                    "ops_batchnorm_forward, ops_add_scaled); buffers allocated once"}
+
+
 # --------------------------------------------------------------------------- selftest (CPU)
 def selftest(a, rank, world):
     """gloo: the bench's launch / argument path plus the bucketed exchange of a flat
@@ -473,6 +521,7 @@ def main():
         extra["configs[4]_forward_3072_mxfp8"] = dict(
             workload="cnn_tdnn_17f_3072 forward only, MXFP8 GEMMs",
             **describe(r, a, world, "forward", True, "", PEAK_FP8_TFLOPS))
+        extra["dropin_per_op_abi_forward"] = dropin_forward(a)
 
     if rank == 0:
         # the box's CPU share (OMP_NUM_THREADS is set to it there; nproc shows the whole host)
