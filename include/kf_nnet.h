@@ -116,7 +116,7 @@ int nnet_dp_debug_early(KfNet *net, int on);
 
 /* diagnostics (tests): back-propagate through the top n layers only; device
  * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott", "aux", "mask",
- * "bn_scale", "bn2_scale", and with fp8 on "x8q" / "x8s": the e4m3 values
+ * "bn_scale", "bn2_scale", "dproj" (attention: the gradient of its affine output), and with fp8 on "x8q" / "x8s": the e4m3 values
  * [T x pad128(in_dim)] and E8M0 scales [T x pad128(in_dim)/32] of the MXFP8 input copy
  * the layer's GEMM reads; `layer` selects the per-layer ones), NULL if unknown */
 int nnet_backward_n(KfNet *net, const void *out_grad_dev, int n);

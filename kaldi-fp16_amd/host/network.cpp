@@ -1403,6 +1403,7 @@ extern "C" const void *nnet_debug_tensor(KfNet *net, const char *what, int layer
     if (w == "dbott") return net->dbott;
     if (layer < 0 || layer >= (int)net->layers.size()) return nullptr;
     if (w == "aux") return net->layers[layer].aux;
+    if (w == "dproj") return net->layers[layer].dproj;
     if (w == "mask") return net->layers[layer].mask;
     if (w == "bn_scale") return net->layers[layer].bn_scale;
     if (w == "bn2_scale") return net->layers[layer].bn2_scale;
