@@ -237,6 +237,10 @@ int kf_transpose_batch(int n, const void *const *src, void *const *dst, const in
  * number `at` counted from this call: [0] start, [1 + 2s] after step s's wait and barrier,
  * [2 + 2s] after its MFMAs, [126] before the epilogue, [127] end; buf NULL disarms */
 void kf_halo_trace(unsigned long long *buf, int at);
+/* diagnostics: phase stamps of block `blk` and {start, end, hw id | xcc << 32} of every
+ * block of gemm_kernel launch number `at` (counted from this call), wall_clock64 ticks
+ * (100 MHz); buf holds 64 + 3 * blocks words; null = off */
+void kf_gemm_trace(unsigned long long *buf, int at, int blk);
 
 const char *kf_last_error(void);
 void kf_clear_error(void);

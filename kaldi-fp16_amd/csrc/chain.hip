@@ -467,7 +467,8 @@ struct DenRun {
     unsigned long long *trace;  // optional phase timestamps (kf_chain_trace), null = off
     float *alpha_store;     // [nseq][max_frames+1][nsl_f*64], forward-table slice order
     float *beta_store;      // [nseq][max_frames+1][nsl_b*64], backward-table slice order
-    float *asum_store;      // [nseq][max_frames+1]
+    float *asum_store;      // [nseq][max_frames+1] alpha sums (alpha'[t] = row + asum[t]*leaky*init)
+    float *bsum_store;      // [nseq][max_frames+1] <init, beta'[t]> (beta[t] = row + leaky*bsum[t])
     float *stats;           // [nseq][8]
     // ABI mode
     float *post_dense;      // [T x P] (single sequence)
@@ -562,7 +563,8 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 }
 
 struct DenX {
-    float *buf;     // [nseq][2][G][blk]; blk = spg*64 + 64 (tail: [wave] = that wave's partial sum)
+    float *buf;     // [nseq][2][G][blk]; blk = 64: [wave] = that wave's partial sum (the state
+                    // slices themselves are exchanged through the alpha / beta stores)
     unsigned *cnt;  // [nseq] arrivals (zeroed before each launch)
     unsigned *tmo;  // per-launch timeout word (zeroed before each launch)
     unsigned *sticky;  // timed-out blocks since the last read (never zeroed by a launch)
@@ -615,38 +617,32 @@ __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     return *lds_flag != 0;
 }
-// all exchanged slices of buffer `buf`, scattered to their states: first sum(total of
-// the G x DEN_WAVES partial sums, fixed order, equal in every lane), then
-// f(state, value, initp, owner, slot) per slot. Slice j lives in slot own[j] & 0xFFFF
-// of block own[j] >> 16. The partial sums load with the slices, so one round trip
-// serves both.
+// one frame's exchanged state row `row` (slice order: every slice stored sc1 by the
+// block that owns it) and the G x DEN_WAVES partial sums of buffer `buf`: first
+// sum(total, fixed order, equal in every lane), then f(state, value, initp) per row. The
+// partial sums load with the row, so one round trip serves both.
 template <class FS, class F>
-__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, int nsl, const int *own,
+__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, const float *row, int nsl,
                                             const int *perm, const float *initp, FS sum, F f) {
     int tid = threadIdx.x;
-    // opaque to the optimiser: the per-slot addresses below are rebuilt every frame
-    // instead of being hoisted out of the frame loop as 64-bit values
+    // opaque to the optimiser: the row addresses below are rebuilt every frame instead of
+    // being hoisted out of the frame loop as 64-bit values
     asm volatile("" : "+v"(tid));
     const int n = nsl * 64, lane = tid & 63;
     const float *xb = X.buf + ((size_t)seq * 2 + buf) * X.G * X.blk;
     float pv = 0.0f;
     for (int i = lane; i < X.G * DEN_WAVES; i += 64)
-        pv += ld_sc1(xb + (size_t)(i / DEN_WAVES) * X.blk + X.spg * 64 + i % DEN_WAVES);
+        pv += ld_sc1(xb + (size_t)(i / DEN_WAVES) * X.blk + i % DEN_WAVES);
     float v[DEN_MAXS];
-    int o[DEN_MAXS];
 #pragma unroll
-    for (int m = 0; m < DEN_MAXS; ++m) {  // unconditional loads (index clamped)
-        const int c = min(tid + m * DEN_THREADS, n - 1);
-        o[m] = own[c >> 6];
-        v[m] = ld_sc1(xb + (size_t)(o[m] >> 16) * X.blk + (o[m] & 0xFFFF) * 64 + (c & 63));
-    }
+    for (int m = 0; m < DEN_MAXS; ++m) v[m] = ld_sc1(row + min(tid + m * DEN_THREADS, n - 1));  // clamped
     sum(wave_sum(pv));
 #pragma unroll
     for (int m = 0; m < DEN_MAXS; ++m) {
         const int c = tid + m * DEN_THREADS;
         if (c < n) {
             const int st = perm[c];
-            if (st >= 0) f(st, v[m], initp[c], o[m] >> 16, c);
+            if (st >= 0) f(st, v[m], initp[c]);
         }
     }
 }
@@ -703,8 +699,10 @@ __device__ __forceinline__ SellLds stage_sell(const SellDev &T, int lgG, int gi,
 
 // Forward pass (chain_den.cu:583-620), G blocks per sequence: block gi computes
 // alpha[t+1] for the destination rows of its slices (a load-balanced share, SellDev::
-// slot), and all blocks rebuild the full alpha'[t+1] in LDS from the exchanged slices.
-// alpha' of every frame goes to HBM for the posterior kernel.
+// slot) and stores them (sc1) into row t+1 of the alpha store, which is also the
+// exchange: all blocks rebuild the full alpha'[t+1] in LDS from that row. The store keeps
+// the slices before the leaky term: alpha'[t] = row[t] + asum[t] * leaky * init, which
+// k_den_post applies when it loads the row (one write per frame, not two).
 template <typename XT>
 __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
                                              unsigned char *smem, int seq, int gi) {
@@ -734,8 +732,7 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     float as = as0;
     for (int s = tid; s < S; s += DEN_THREADS) va[s] = g.init[s] + as0 * leaky * g.init[s];
     if (gi == 0 && seq < X.nseq) {
-        for (int c = tid; c < rs; c += DEN_THREADS)
-            __builtin_nontemporal_store(F.initp[c] + as0 * leaky * F.initp[c], astore + c);
+        for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(F.initp[c], astore + c);
         if (tid == 0) {
             asum[0] = as0;
             r.stats[(size_t)seq * 8 + 3] = 0.0f;  // accumulated by k_den_post
@@ -758,7 +755,8 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     for (int t = 0; t < T; ++t) {
         DEN_TP(0);
         const int buf = (t + 1) & 1;
-        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        float *tail = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        float *arow = astore + (size_t)(t + 1) * rs;
         const float inv = as > 0.0f ? 1.0f / as : 1.0f;
         float pq = 0.f;
         auto term = [&](int src, int pdf, float tp) { return va[src] * tp * xe[pdf]; };
@@ -770,11 +768,11 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
             const float acc = scaled ? sell_slice(arcs, F.len[j], F.off[j], lane, term_s)
                                      : sell_slice(arcs, F.len[j], F.off[j], lane, term);
             const float v = st >= 0 ? acc * inv : 0.0f;
-            st_sc1(blk + k * 64 + lane, v);
+            st_sc1(arow + j * 64 + lane, v);
             pq += v;
         }
         DEN_TP(1);
-        den_publish(X, blk + spg * 64, wave_sum(pq), seq);
+        den_publish(X, tail, wave_sum(pq), seq);
         DEN_TP(2);
         // the next frame's output row: fetched after the publish, so its latency hides under
         // the exchange wait (fetched at the frame start, the record loads' in-order vmcnt
@@ -785,13 +783,8 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         DEN_TP(4);
         float as1 = 0.f;
         DEN_TP(5);
-        den_consume(X, seq, buf, nsl, F.own, F.perm, F.initp, [&](float v) { as1 = v; },
-                    [&](int st, float v, float ip, int owner, int c) {
-                        const float a = v + as1 * leaky * ip;
-                        va[st] = a;
-                        if (owner == gi)  // keep L2 for the arcs
-                            __builtin_nontemporal_store(a, astore + (size_t)(t + 1) * rs + c);
-                    });
+        den_consume(X, seq, buf, arow, nsl, F.perm, F.initp, [&](float v) { as1 = v; },
+                    [&](int st, float v, float ip) { va[st] = v + as1 * leaky * ip; });
         DEN_TP(6);
         // past the publish barrier nothing reads this frame's xe
         if (t + 1 < T) {
@@ -835,9 +828,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
 }
 
 // Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per
-// sequence: beta'[t] over the source rows of this block's slices (exchanged),
-// beta[t] = beta'[t] + leaky*<init, beta'[t]>; beta[t] for t >= 1 goes to HBM for
-// k_den_post. The reference scales beta'[t] by 1/sum(alpha[t]) and starts from
+// sequence: beta'[t] over the source rows of this block's slices, stored (sc1) into row t
+// of the beta store, which is also the exchange; beta[t] = beta'[t] + leaky*<init,
+// beta'[t]>, the second term kept per frame in bsum (k_den_post adds it). The reference scales beta'[t] by 1/sum(alpha[t]) and starts from
 // 1/total_prob; any positive per-frame factor gives the same posteriors once
 // k_den_post normalises each frame (the den posteriors of a frame sum to one:
 // they are d log p / d x_t), so this pass scales by 1/<init, beta'[t+1]> and
@@ -859,6 +852,7 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const int rs = nsl * 64;
     float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rs;
+    float *bsum = r.bsum_store + (size_t)seq * (r.max_frames + 1);
     const float leaky = r.leaky;
 
     const bool scaled = g.b.arc_s != nullptr;
@@ -873,7 +867,8 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
     for (int s = tid; s < S; s += DEN_THREADS) vb[s] = 1.0f + leaky * n0;
     if (gi == 0 && seq < X.nseq) {
         float *bT = bstore + (size_t)T * rs;
-        for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(1.0f + leaky * n0, bT + c);
+        for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(1.0f, bT + c);
+        if (tid == 0) bsum[T] = n0;
     }
     if (T > 0) {
         pre.fetch(nnet + (r0 + (long long)(T - 1) * r.stride) * r.ld, P);
@@ -886,7 +881,8 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
     __syncthreads();
     for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
         const int buf = t & 1;
-        float *blk = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        float *tail = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
+        float *brow = bstore + (size_t)t * rs;
         const float inv = nrm > 0.0f ? 1.0f / nrm : 1.0f;
         float pq = 0.f;
         auto term = [&](int dst, int pdf, float tp) { return vb[dst] * tp * xe[pdf]; };
@@ -898,23 +894,20 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
             const float acc = scaled ? sell_slice(arcs, B.len[j], B.off[j], lane, term_s)
                                      : sell_slice(arcs, B.len[j], B.off[j], lane, term);
             const float bd = st >= 0 ? acc * inv : 0.0f;
-            st_sc1(blk + k * 64 + lane, bd);
+            st_sc1(brow + j * 64 + lane, bd);
             pq += B.initp[j * 64 + lane] * bd;
         }
-        den_publish(X, blk + spg * 64, wave_sum(pq), seq);
+        den_publish(X, tail, wave_sum(pq), seq);
         if (t > 0) pre.fetch(nnet + (r0 + (long long)(t - 1) * r.stride) * r.ld, P);  // as den_fwd_body
         if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
         float tb = 0.f;
-        den_consume(X, seq, buf, nsl, B.own, B.perm, B.initp,
+        den_consume(X, seq, buf, brow, nsl, B.perm, B.initp,
                     [&](float v) {
                         nrm = v;  // <init, beta'[t]>: the next factor
                         tb = leaky * nrm;
                     },
-                    [&](int st, float v, float, int owner, int c) {
-                        const float b = v + tb;
-                        vb[st] = b;
-                        if (t > 0 && owner == gi) __builtin_nontemporal_store(b, bstore + (size_t)t * rs + c);
-                    });
+                    [&](int st, float v, float) { vb[st] = v + tb; });
+        if (gi == 0 && tid == 0) bsum[t] = nrm;
         if (t > 0) {
 #pragma unroll
             for (int i = 0; i < DEN_MAXPT; ++i) {
@@ -997,6 +990,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     const int rsf = g.f.nsl * 64, rsb = g.b.nsl * 64;  // slice-ordered rows (k_den_fb)
     const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rsf;
     const float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rsb;
+    const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
+    const float *bsum = r.bsum_store + (size_t)seq * (r.max_frames + 1);
+    const float leaky = r.leaky;
 
     int ok = 1;
     float w = 1.0f;
@@ -1025,22 +1021,41 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     const bool do_oor = MODE == DEN_PRODUCT && r.opts.out_of_range_regularize > 0.0f;
     const bool do_l2 = MODE == DEN_PRODUCT && r.opts.l2_regularize > 0.0f;
     float oor = 0.f, sq = 0.f;
+    // this thread's rows c = tid + m * DEN_THREADS of both stores: their state and the
+    // initial probability, once for the block's frames (rs <= DEN_MAXS * DEN_THREADS)
+    int pfw[DEN_MAXS], pbw[DEN_MAXS];
+    float ipf[DEN_MAXS];
+#pragma unroll
+    for (int m = 0; m < DEN_MAXS; ++m) {
+        const int c = tid + m * DEN_THREADS;
+        pfw[m] = c < rsf ? g.f.perm[c] : -1;
+        ipf[m] = c < rsf ? g.f.initp[c] : 0.f;
+        pbw[m] = c < rsb ? g.b.perm[c] : -1;
+    }
     for (int t = t0; t < t1; t += PAIR) {
         const int nf2 = min(PAIR, t1 - t);
-        // stage alpha'[t+f], beta[t+f+1] (a missing second frame computes zeros)
+        // stage alpha'[t+f], beta[t+f+1] (a missing second frame computes zeros); the
+        // stored rows lack the leaky terms (den_fwd_body, den_bwd_body), added here as the
+        // recursions add them
 #pragma unroll
         for (int f = 0; f < PAIR; ++f) {
             const bool live = f < nf2;
-            const float *ar = astore + (size_t)(t + f) * rsf, *br = bstore + (size_t)(t + f + 1) * rsb;
-            for (int c = tid; c < rsf; c += DEN_THREADS) {
-                const int st = g.f.perm[c];
-                const float v = live ? __builtin_nontemporal_load(ar + c) : 0.f;
-                if (st >= 0) va[f * S + st] = v;
+            // (a missing frame reads frame t's rows, which exist, and stores zeros)
+            const int tf = live ? t + f : t;
+            const float *ar = astore + (size_t)tf * rsf, *br = bstore + (size_t)(tf + 1) * rsb;
+            const float as1 = live ? asum[t + f] : 0.f;
+            const float tb = live ? leaky * bsum[t + f + 1] : 0.f;
+            float va_[DEN_MAXS], vb_[DEN_MAXS];
+#pragma unroll
+            for (int m = 0; m < DEN_MAXS; ++m) {  // unconditional loads (index clamped)
+                const int c = tid + m * DEN_THREADS;
+                va_[m] = __builtin_nontemporal_load(ar + min(c, rsf - 1));
+                vb_[m] = __builtin_nontemporal_load(br + min(c, rsb - 1));
             }
-            for (int c = tid; c < rsb; c += DEN_THREADS) {
-                const int st = g.b.perm[c];
-                const float v = live ? __builtin_nontemporal_load(br + c) : 0.f;
-                if (st >= 0) vb[f * S + st] = v;
+#pragma unroll
+            for (int m = 0; m < DEN_MAXS; ++m) {
+                if (pfw[m] >= 0) va[f * S + pfw[m]] = live ? va_[m] + as1 * leaky * ipf[m] : 0.f;
+                if (pbw[m] >= 0) vb[f * S + pbw[m]] = live ? vb_[m] + tb : 0.f;
             }
         }
         __syncthreads();
@@ -1430,7 +1445,7 @@ struct DenXBuf {
         X.nseq = nseq;
         X.lgG = G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
         X.spg = tb.spg[X.lgG];
-        X.blk = X.spg * 64 + 64;
+        X.blk = 64;  // partial sums only: the slices go through the alpha / beta stores
         X.lds_f = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.f.nsl, g.f.spg[X.lgG]);
         X.lds_b = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.b.nsl, g.b.spg[X.lgG]);
         size_t nb = (size_t)X.nseq * 2 * G * X.blk * 4;
@@ -2146,11 +2161,11 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     }
     const int S = t->dev.S, P = t->dev.P;
     const size_t TP = (size_t)T * P;
-    DevBuf x, init, as, bs, ast, stats, post, row0, frames, dout;
+    DevBuf x, init, as, bs, ast, bst, stats, post, row0, frames, dout;
     const size_t rs = (size_t)t->dev.f.nsl * 64;  // slice-ordered rows
     if (!x.alloc(TP * 4) || !init.alloc(S * 4) || !as.alloc((size_t)(T + 1) * rs * 4) ||
         (h_post && !bs.alloc((size_t)(T + 1) * rs * 4)) ||
-        !ast.alloc((T + 1) * 4) || !stats.alloc(32) || !row0.alloc(8) || !frames.alloc(4) ||
+        !ast.alloc((T + 1) * 4) || !bst.alloc((T + 1) * 4) || !stats.alloc(32) || !row0.alloc(8) || !frames.alloc(4) ||
         !dout.alloc(8) ||
         (h_post && !post.alloc(TP * 4))) {
         den_set_error("den_forward: hipMalloc failed");
@@ -2177,6 +2192,7 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     r.alpha_store = (float *)as.p;
     r.beta_store = (float *)bs.p;
     r.asum_store = (float *)ast.p;
+    r.bsum_store = (float *)bst.p;
     r.stats = (float *)stats.p;
     r.post_dense = (float *)post.p;
     r.den_out = (float *)dout.p;
@@ -2246,7 +2262,8 @@ struct KfChain {
     const KfDenGraph *den = nullptr;
     DenXBuf xbuf2;  // the backward recursion's exchange (k_den_fb)
     int max_seqs = 0, max_frames = 0;
-    float *alpha_store = nullptr, *beta_store = nullptr, *asum_store = nullptr, *stats = nullptr;
+    float *alpha_store = nullptr, *beta_store = nullptr, *asum_store = nullptr, *bsum_store = nullptr;
+    float *stats = nullptr;
     float *num_ab = nullptr;      // numerator alpha/beta
     size_t num_ab_cap = 0;
     float *num_post = nullptr;    // sparse numerator posteriors
@@ -2273,7 +2290,8 @@ struct KfChain {
         if (ev_in) hipEventDestroy(ev_in);
         if (ev_num) hipEventDestroy(ev_num);
         if (den_out) hipFree(den_out);
-        for (void *p : {(void *)alpha_store, (void *)beta_store, (void *)asum_store, (void *)stats, (void *)num_ab,
+        for (void *p : {(void *)alpha_store, (void *)beta_store, (void *)asum_store, (void *)bsum_store,
+                        (void *)stats, (void *)num_ab,
                         (void *)num_post, (void *)d_desc, (void *)d_row0, (void *)d_frames,
                         (void *)d_num_total})
             if (p) hipFree(p);
@@ -2385,6 +2403,7 @@ extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max
     bool ok = hipMalloc(&c->alpha_store, (size_t)max_seqs * (max_frames + 1) * rs * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->beta_store, (size_t)max_seqs * (max_frames + 1) * rs * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->asum_store, (size_t)max_seqs * (max_frames + 1) * 4) == hipSuccess;
+    ok = ok && hipMalloc(&c->bsum_store, (size_t)max_seqs * (max_frames + 1) * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->stats, (size_t)max_seqs * 8 * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->d_desc, (size_t)max_seqs * sizeof(LogFstDev)) == hipSuccess;
     ok = ok && hipMalloc(&c->d_row0, (size_t)max_seqs * 8) == hipSuccess;
@@ -2535,6 +2554,7 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
     r.alpha_store = c->alpha_store;
     r.beta_store = c->beta_store;
     r.asum_store = c->asum_store;
+    r.bsum_store = c->bsum_store;
     r.stats = c->stats;
     r.den_out = c->den_out;
     r.trace = c->trace;

@@ -52,6 +52,10 @@ struct WgradArgs {
     // meet in one L2 instead of two
     int pair_ps;
     int kil;            // fused: 1 = alternate the K-steps of a two-part A (KF_GEMM_KIL, default 1)
+    // diagnostics (kf_gemm_trace), null = off: [0..63] phase stamps of block trace_blk
+    // (tid 0), then per block {start, end, hw id | xcc id << 32}
+    unsigned long long *trace;
+    int trace_blk;
 };
 
 template <int BM, int BN, int ST, int SCB = 0>
@@ -325,6 +329,21 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
+    const int bid = blockIdx.x + blockIdx.y * gridDim.x;
+    const bool trb = G.trace != nullptr && tid == 0, trp = trb && bid == G.trace_blk;
+    if (trb) {
+        G.trace[64 + 3 * bid] = wall_clock64();
+        G.trace[64 + 3 * bid + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4) | (31 << 11)) |
+                                    ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (31 << 11)) << 32);
+    }
+#define GEMM_TP(slot) \
+    if (trp) G.trace[slot] = wall_clock64();
+    GEMM_TP(0);
+    if (trb && bid == 0) {
+        G.trace[60] = (unsigned long long)M | ((unsigned long long)N << 20) | ((unsigned long long)K << 40);
+        G.trace[61] = (unsigned long long)BM | ((unsigned long long)BN << 16) | ((unsigned long long)gridDim.x << 32);
+        G.trace[62] = gridDim.y;
+    }
 
     // XCD-aware tile order: consecutive tile ids (the N tiles of one M tile, which
     // share the A rows) land on one XCD, whose L2 then serves the A re-reads.
@@ -398,11 +417,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     if (nk > 0) issue(0, kofs(0));
     if (ST >= 3 && nk > 1) issue(1, kofs(1));
     if (ST >= 4 && nk > 2) issue(2, kofs(2));
+    GEMM_TP(1);
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + ST - 2 < nk) wait_vmcnt<LPT * (ST - 2)>();
         else wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        if (kt < 40) GEMM_TP(2 + kt);
         if (kt + ST - 1 < nk) issue((kt + ST - 1) % ST, kofs(kt + ST - 1));
         const char *ta = smem + (kt % ST) * STAGE;
         const char *tb = ta + A_STAGE;
@@ -474,8 +495,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
         if (do_bsum && tid < BN && n0 + tid < N)
             G.bias_slab[(long long)split * N + n0 + tid] = bsum;
     } else {
+        GEMM_TP(42);
         fused_epilogue<BM, BN, WM, WN>(acc, smem, E, M, N, m0, n0, tid, lane, wave, &epre);
     }
+    GEMM_TP(43);
+    if (trb) G.trace[64 + 3 * bid + 1] = wall_clock64();
+#undef GEMM_TP
 }
 
 // ---------------------------------------------------------------------------
@@ -988,12 +1013,30 @@ static bool mn_gen_ok(const OpD &o, const char *name) {
     return true;
 }
 
+// diagnostics: stamp the gemm_kernel launch number `at` (fused and wgrad launches, counted
+// from this call): phase stamps of block `blk` and {start, end, hw id} of every block
+// (wall_clock64 ticks, 100 MHz). buf holds 64 + 3 * blocks words; null = off
+static unsigned long long *g_gemm_trace = nullptr;
+static int g_gemm_trace_at = -1, g_gemm_trace_blk = 0, g_gemm_launches = 0;
+extern "C" void kf_gemm_trace(unsigned long long *buf, int at, int blk) {
+    g_gemm_trace = buf;
+    g_gemm_trace_at = at;
+    g_gemm_trace_blk = blk;
+    g_gemm_launches = 0;
+}
+
 template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE,
           int F8 = 0>
 static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilogue &E,
-                  const WgradArgs &G, int splits) {
+                  const WgradArgs &G0, int splits) {
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     dim3 grid(mt * nt, WGRAD ? splits : 1);
+    WgradArgs G = G0;
+    G.trace = nullptr;
+    if (g_gemm_trace && g_gemm_launches++ == g_gemm_trace_at) {
+        G.trace = g_gemm_trace;
+        G.trace_blk = g_gemm_trace_blk;
+    }
     ProfRec rec{};
     if (g_prof) {
         rec.a = prof_event();
