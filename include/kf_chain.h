@@ -109,6 +109,9 @@ void kf_chain_trace(KfChain *c, unsigned long long *dev_buf);
  * 0xFFFFFFFF restores the default). A timeout in ANY compute since the last
  * kf_chain_result makes that call fail (the count is sticky across launches). */
 void kf_chain_debug_spin_limit(KfChain *c, unsigned polls);
+/* Diagnostics (tests): force != 0 makes the den exchange use agent scope (through to
+ * memory) even where all blocks of a sequence share an XCD; 0 restores the default. */
+void kf_chain_debug_exchange_sys(KfChain *c, int force);
 
 const char *kf_chain_last_error(void);
 void kf_chain_clear_error(void);

@@ -561,11 +561,34 @@ __device__ __forceinline__ void st_sc1(float *p, float v) {
 __device__ __forceinline__ float ld_sc1(const float *p) {
     return __uint_as_float(__hip_atomic_load((gu32_t *)p, RLX_AGENT));
 }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t den_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)0xFFFFFFFF, 0x00020000);
+}
+// Exchange word access. LOC: every block of the sequence runs on one XCD, so they share
+// one L2 — plain stores (written through the CU's L1 into that L2, acknowledged there)
+// and sc0 loads (which miss the L1) hand the data over without the write-through to
+// memory that agent scope (sc1) needs across XCDs. `base` is uniform, `i` a word index.
+template <bool LOC>
+__device__ __forceinline__ void x_st(float *base, int i, float v) {
+    if constexpr (LOC)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), den_rsrc(base), i * 4, 0, 0);
+    else
+        st_sc1(base + i, v);
+}
+template <bool LOC>
+__device__ __forceinline__ float x_ld(const float *base, int i) {
+    if constexpr (LOC)
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(den_rsrc(base), i * 4, 0, 1 /* sc0 */));
+    else
+        return ld_sc1(base + i);
+}
 
 struct DenX {
     float *buf;     // [nseq][2][G][blk]; blk = 64: [wave] = that wave's partial sum (the state
                     // slices themselves are exchanged through the alpha / beta stores)
     unsigned *cnt;  // [nseq] arrivals (zeroed before each launch)
+    unsigned *xm;   // [nseq] XCD census: 4-bit arrival count per XCD (zeroed before each launch)
+    int force_sys;  // 1: agent-scope exchange even when a sequence's blocks share an XCD (tests)
     unsigned *tmo;  // per-launch timeout word (zeroed before each launch)
     unsigned *sticky;  // timed-out blocks since the last read (never zeroed by a launch)
     unsigned spin_limit;  // polls before a wait gives up (kf_chain_debug_spin_limit)
@@ -586,19 +609,24 @@ __device__ __forceinline__ void den_map(const DenX &X, int &seq, int &gi) {
 // publish: every wave stores its partial sum (lane 0, tail slot `wave`) beside its
 // payload, all sc1; every wave drains vmcnt, the workgroup barriers, one lane adds
 // the arrival (one store drain per frame)
+template <bool LOC>
 __device__ __forceinline__ void den_publish(const DenX &X, float *tail, float wsum, int seq) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (lane == 0) st_sc1(tail + wave, wsum);
+    if (lane == 0) x_st<LOC>(tail, wave, wsum);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[seq], 1u, RLX_AGENT);
 }
-// wait for `target` arrivals (one lane polls); false on timeout, uniform
-__device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target, int *lds_flag) {
+// one lane polls `word` until done(value); false on timeout, uniform. *val: the last value
+template <class Done>
+__device__ __forceinline__ bool den_poll(const DenX &X, const unsigned *word, Done done, int *lds_flag,
+                                         unsigned *val = nullptr) {
     if (threadIdx.x == 0) {
         int ok = 1;
         for (unsigned it = 0;; ++it) {
-            if (__hip_atomic_load((gu32_t *)&X.cnt[seq], RLX_AGENT) >= target) break;
+            const unsigned v = __hip_atomic_load((gu32_t *)word, RLX_AGENT);
+            if (val) *val = v;
+            if (done(v)) break;
             if ((it & 255) == 255 && __hip_atomic_load((gu32_t *)X.tmo, RLX_AGENT)) {
                 ok = 0;
                 break;
@@ -617,11 +645,38 @@ __device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     return *lds_flag != 0;
 }
+// wait for `target` arrivals; false on timeout, uniform
+__device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target, int *lds_flag) {
+    return den_poll(X, &X.cnt[seq], [&](unsigned v) { return v >= target; }, lds_flag);
+}
+// XCD census before the first exchange: 1 if all G blocks of the sequence run on one
+// XCD (the placement den_map asks the dispatcher for, not a guarantee), 0 if not or
+// forced, -1 on timeout; uniform. Each block adds 1 to its XCD's 4-bit field.
+__device__ __forceinline__ int den_xcd_local(const DenX &X, int seq, int *lds_flag) {
+    if (seq >= X.nseq) return 0;  // grid padding: no exchange
+    unsigned *word = X.xm + seq;
+    if (threadIdx.x == 0) {
+        const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (3 << 11)) & 7;  // HW_REG_XCC_ID
+        __hip_atomic_fetch_add((gu32_t *)word, 1u << (4 * xcc), RLX_AGENT);
+    }
+    auto total = [](unsigned v) {
+        unsigned n = 0;
+        for (int k = 0; k < 8; ++k) n += (v >> (4 * k)) & 15;
+        return n;
+    };
+    unsigned *vl = reinterpret_cast<unsigned *>(lds_flag) + 1;
+    if (!den_poll(X, word, [&](unsigned v) { return total(v) >= (unsigned)X.G; }, lds_flag, vl)) return -1;
+    const unsigned v = *vl;
+    bool one = false;
+    for (int k = 0; k < 8; ++k)
+        if (((v >> (4 * k)) & 15) == (unsigned)X.G) one = true;
+    return one && !X.force_sys ? 1 : 0;
+}
 // one frame's exchanged state row `row` (slice order: every slice stored sc1 by the
 // block that owns it) and the G x DEN_WAVES partial sums of buffer `buf`: first
 // sum(total, fixed order, equal in every lane), then f(state, value, initp) per row. The
 // partial sums load with the row, so one round trip serves both.
-template <class FS, class F>
+template <bool LOC, class FS, class F>
 __device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, const float *row, int nsl,
                                             const int *perm, const float *initp, FS sum, F f) {
     int tid = threadIdx.x;
@@ -632,10 +687,10 @@ __device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, con
     const float *xb = X.buf + ((size_t)seq * 2 + buf) * X.G * X.blk;
     float pv = 0.0f;
     for (int i = lane; i < X.G * DEN_WAVES; i += 64)
-        pv += ld_sc1(xb + (size_t)(i / DEN_WAVES) * X.blk + i % DEN_WAVES);
+        pv += x_ld<LOC>(xb, (i / DEN_WAVES) * X.blk + i % DEN_WAVES);
     float v[DEN_MAXS];
 #pragma unroll
-    for (int m = 0; m < DEN_MAXS; ++m) v[m] = ld_sc1(row + min(tid + m * DEN_THREADS, n - 1));  // clamped
+    for (int m = 0; m < DEN_MAXS; ++m) v[m] = x_ld<LOC>(row, min(tid + m * DEN_THREADS, n - 1));  // clamped
     sum(wave_sum(pv));
 #pragma unroll
     for (int m = 0; m < DEN_MAXS; ++m) {
@@ -703,7 +758,7 @@ __device__ __forceinline__ SellLds stage_sell(const SellDev &T, int lgG, int gi,
 // exchange: all blocks rebuild the full alpha'[t+1] in LDS from that row. The store keeps
 // the slices before the leaky term: alpha'[t] = row[t] + asum[t] * leaky * init, which
 // k_den_post applies when it loads the row (one write per frame, not two).
-template <typename XT>
+template <typename XT, bool LOC>
 __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
                                              unsigned char *smem, int seq, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -768,11 +823,11 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
             const float acc = scaled ? sell_slice(arcs, F.len[j], F.off[j], lane, term_s)
                                      : sell_slice(arcs, F.len[j], F.off[j], lane, term);
             const float v = st >= 0 ? acc * inv : 0.0f;
-            st_sc1(arow + j * 64 + lane, v);
+            x_st<LOC>(arow, j * 64 + lane, v);
             pq += v;
         }
         DEN_TP(1);
-        den_publish(X, tail, wave_sum(pq), seq);
+        den_publish<LOC>(X, tail, wave_sum(pq), seq);
         DEN_TP(2);
         // the next frame's output row: fetched after the publish, so its latency hides under
         // the exchange wait (fetched at the frame start, the record loads' in-order vmcnt
@@ -783,7 +838,7 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         DEN_TP(4);
         float as1 = 0.f;
         DEN_TP(5);
-        den_consume(X, seq, buf, arow, nsl, F.perm, F.initp, [&](float v) { as1 = v; },
+        den_consume<LOC>(X, seq, buf, arow, nsl, F.perm, F.initp, [&](float v) { as1 = v; },
                     [&](int st, float v, float ip) { va[st] = v + as1 * leaky * ip; });
         DEN_TP(6);
         // past the publish barrier nothing reads this frame's xe
@@ -824,7 +879,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int seq, gi;
     den_map(X, seq, gi);
-    den_fwd_body<XT>(g, r, X, smem, seq, gi);
+    const int loc = den_xcd_local(X, seq, reinterpret_cast<int *>(smem) + 32);
+    if (loc > 0) den_fwd_body<XT, true>(g, r, X, smem, seq, gi);
+    else if (loc == 0) den_fwd_body<XT, false>(g, r, X, smem, seq, gi);
 }
 
 // Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per
@@ -835,7 +892,7 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
 // k_den_post normalises each frame (the den posteriors of a frame sum to one:
 // they are d log p / d x_t), so this pass scales by 1/<init, beta'[t+1]> and
 // starts from ones — it needs nothing from the forward pass and runs beside it.
-template <typename XT>
+template <typename XT, bool LOC>
 __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, const DenX &X,
                                              unsigned char *smem, int seq, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -894,14 +951,14 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
             const float acc = scaled ? sell_slice(arcs, B.len[j], B.off[j], lane, term_s)
                                      : sell_slice(arcs, B.len[j], B.off[j], lane, term);
             const float bd = st >= 0 ? acc * inv : 0.0f;
-            st_sc1(brow + j * 64 + lane, bd);
+            x_st<LOC>(brow, j * 64 + lane, bd);
             pq += B.initp[j * 64 + lane] * bd;
         }
-        den_publish(X, tail, wave_sum(pq), seq);
+        den_publish<LOC>(X, tail, wave_sum(pq), seq);
         if (t > 0) pre.fetch(nnet + (r0 + (long long)(t - 1) * r.stride) * r.ld, P);  // as den_fwd_body
         if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
         float tb = 0.f;
-        den_consume(X, seq, buf, brow, nsl, B.perm, B.initp,
+        den_consume<LOC>(X, seq, buf, brow, nsl, B.perm, B.initp,
                     [&](float v) {
                         nrm = v;  // <init, beta'[t]>: the next factor
                         tb = leaky * nrm;
@@ -934,8 +991,15 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
     const bool bwd = w >= half;
     const int inner = bwd ? w - half : w;
     const int seq = inner >> XF.lgG, gi = inner & (XF.G - 1);
-    if (bwd) den_bwd_body<XT>(g, r, XB, smem, seq, gi);
-    else den_fwd_body<XT>(g, r, XF, smem, seq, gi);
+    const int loc = den_xcd_local(bwd ? XB : XF, seq, reinterpret_cast<int *>(smem) + 32);
+    if (loc < 0) return;  // timed out (reported through the timeout words)
+    if (bwd) {
+        if (loc) den_bwd_body<XT, true>(g, r, XB, smem, seq, gi);
+        else den_bwd_body<XT, false>(g, r, XB, smem, seq, gi);
+    } else {
+        if (loc) den_fwd_body<XT, true>(g, r, XF, smem, seq, gi);
+        else den_fwd_body<XT, false>(g, r, XF, smem, seq, gi);
+    }
 }
 
 // Posteriors (kernel_den_posteriors, chain_den.cu:253-280) for every (sequence,
@@ -1449,7 +1513,7 @@ struct DenXBuf {
         X.lds_f = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.f.nsl, g.f.spg[X.lgG]);
         X.lds_b = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.b.nsl, g.b.spg[X.lgG]);
         size_t nb = (size_t)X.nseq * 2 * G * X.blk * 4;
-        size_t nc = (((size_t)X.nseq + 2) * 4 + 15) / 16 * 16;  // sticky, timeout, counters
+        size_t nc = (((size_t)X.nseq * 2 + 2) * 4 + 15) / 16 * 16;  // sticky, timeout, counters, census
         if (nb > buf_cap) {
             if (buf) hipFree(buf);
             buf = nullptr;
@@ -1473,12 +1537,15 @@ struct DenXBuf {
         X.sticky = cnt;
         X.tmo = cnt + 1;
         X.cnt = cnt + 2;
+        X.xm = cnt + 2 + X.nseq;
         X.spin_limit = spin_limit;
+        X.force_sys = force_sys;
         return true;
     }
     // counters and the per-launch timeout word; never the sticky word
     void zero(hipStream_t st) { hipMemsetAsync(cnt + 1, 0, cnt_cap - 4, st); }
     unsigned spin_limit = 1u << 21;
+    int force_sys = 0;
     // blocks that timed out since the last call (stream-ordered read, then cleared)
     unsigned take_timeouts(hipStream_t st) {
         if (!cnt) return 0;
@@ -2600,6 +2667,12 @@ extern "C" void kf_chain_debug_spin_limit(KfChain *c, unsigned polls) {
     if (!c) return;
     const unsigned v = polls == 0xFFFFFFFFu ? (1u << 21) : polls;
     c->xbuf.spin_limit = c->xbuf2.spin_limit = v;
+}
+
+// diagnostics (tests): 1 makes the den exchange use agent scope (sc1 through to memory)
+// even where the blocks of a sequence share an XCD; 0 = default (L2-local when they do)
+extern "C" void kf_chain_debug_exchange_sys(KfChain *c, int force) {
+    if (c) c->xbuf.force_sys = c->xbuf2.force_sys = force ? 1 : 0;
 }
 
 extern "C" const float *kf_chain_seq_stats(const KfChain *c) { return c ? c->stats : nullptr; }

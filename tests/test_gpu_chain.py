@@ -232,6 +232,31 @@ def test_batched_objective_repeatable(gpu, den):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("negs", [16, pytest.param(64, marks=pytest.mark.slow)])
+def test_den_exchange_xcd_local_matches_agent_scope(gpu, den, negs):
+    """The den exchange between the blocks of a sequence that share an XCD (L2-local
+    stores / L1-missing loads) hands over exactly the words the agent-scope exchange
+    (through to memory) does: objective, per-sequence stats and gradient bit-identical
+    at 16 and at the bench's 64 egs, where den_map's XCD placement holds."""
+    from kfp16 import chain
+    g, init, P, row0, frames, stride, fsts, x = _batch_setup(gpu, den, negs, seed=31)
+    dx = gpu.upload_fp16(x)
+    og = gpu.DeviceBuffer(x.size * 2)
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=negs, max_frames=490)
+    nb = chain.NumBatch(fsts)
+    outs = []
+    for force in (True, False, True):
+        ch.debug_exchange_sys(force)
+        ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+        res = ch.result()
+        outs.append((res.objf, res.num_ok, ch.seq_stats(negs).copy(), gpu.read_fp16(og.ptr, x.shape)))
+    ch.debug_exchange_sys(False)
+    for o in outs[1:]:
+        assert o[0] == outs[0][0] and o[1] == outs[0][1] == negs
+        np.testing.assert_array_equal(o[2], outs[0][2])
+        np.testing.assert_array_equal(o[3], outs[0][3])
+
+
 def test_den_exchange_timeout_is_sticky(gpu, den):
     """A den exchange that gives up (forced: zero polls allowed) makes the next
     kf_chain_result fail even when a later compute succeeds; the result call that
