@@ -102,7 +102,8 @@ const float *kf_chain_seq_stats(const KfChain *c);
 int kf_chain_result(KfChain *c, KfChainResult *out);
 
 /* diagnostics: phase timestamps of the den forward kernel (sequence 0, block 0,
- * frames 16..47, 8 u64 each, 100 MHz wall clock) into a device buffer; NULL = off */
+ * frames 16..47, 8 u64 each, 100 MHz wall clock), then the arc-phase end of every wave
+ * of blocks 0 and 1 (32 x 2 x 16 u64) into a device buffer; NULL = off */
 void kf_chain_trace(KfChain *c, unsigned long long *dev_buf);
 /* diagnostics (tests): polls a den exchange wait makes before it declares the
  * partner blocks non-resident (default 2^21; 0 forces the timeout path;
@@ -112,6 +113,9 @@ void kf_chain_debug_spin_limit(KfChain *c, unsigned polls);
 /* Diagnostics (tests): force != 0 makes the den exchange use agent scope (through to
  * memory) even where all blocks of a sequence share an XCD; 0 restores the default. */
 void kf_chain_debug_exchange_sys(KfChain *c, int force);
+/* Diagnostics (tests): pairs == 0 runs the den recursions one sequence per workgroup set
+ * even where two sequences could share each record (the default, pairs == 1). */
+void kf_chain_debug_den_pairs(KfChain *c, int pairs);
 
 const char *kf_chain_last_error(void);
 void kf_chain_clear_error(void);

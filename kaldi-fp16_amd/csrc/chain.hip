@@ -431,20 +431,19 @@ struct SellDev {  // sliced ELL, 64 rows per slice, rows sorted by degree
     int nsl;
     const int *perm, *len, *off;
     const uint2 *arc;     // {f1 | f2 << 16, tp}
-    // f and b only, when 64 + S + P < 16384: the same records with f1, f2 replaced by
-    // the LDS byte addresses of their operands in the NS = 1 recursion layout
-    // (value row at byte 256, exp row after it), so the gathers need no address VALU
-    const uint2 *arc_s;
+    // f and b only: the same records with f1, f2 replaced by the LDS byte offsets of their
+    // operands in the NS-interleaved state and exp rows (4 * NS * f1, 4 * NS * f2; index
+    // NS - 1), so the gathers need one address add each
+    const uint2 *arc_p[2];
     const float *initp;   // init[perm[c]] in slice order (0 for padding rows), f and b only
     // Slice ownership for G = 1, 2, 4, 8 blocks per sequence (index log2 G): the slices
     // are spread over the G x DEN_WAVES (block, wave) pairs by length, longest first onto
     // the least loaded pair, so the slowest wave of a frame carries about the mean share
     // (round-robin ownership left it 1.3-1.4x the mean on the den graph's degree-sorted
     // slices). slot[lgG][gi * spg + k]: the slice in slot k of block gi, processed by
-    // wave k % DEN_WAVES (-1: empty); own[lgG][j] = gi << 16 | k. The q table keeps only
-    // its G = 1 lists (the posterior kernel's waves).
+    // wave k % DEN_WAVES (-1: empty). The q table keeps only its G = 1 lists (the
+    // posterior kernel's waves).
     const int *slot[4];
-    const int *own[4];
     int spg[4];
 };
 struct DenDev {
@@ -453,6 +452,7 @@ struct DenDev {
     SellDev b;  // rows = source states:      {dst, pdf0}
     SellDev q;  // rows = pdfs:               {src, dst}
     const float *init;
+    int pair_ok;  // the NS = 2 recursion fits the LDS
 };
 
 struct DenRun {
@@ -485,22 +485,21 @@ enum { DEN_ABI = 0, DEN_PRODUCT = 1 };
 #define DEN_MAXPT 4  // P <= 4096
 #define DEN_MAXS 8  // S <= 8192
 
-// Loads are unconditional (index clamped, value selected afterwards): a
-// "load or constant" select makes hipcc branch and wait vmcnt(0) per element.
-template <typename XT>
-__device__ __forceinline__ void den_fetch_row(float (&r)[DEN_MAXPT], const XT *row, int P) {
-#pragma unroll
-    for (int i = 0; i < DEN_MAXPT; ++i) {
-        int p = threadIdx.x + i * DEN_THREADS;
-        float v = (float)row[min(p, P - 1)];
-        r[i] = (p < P) ? v : 0.0f;
-    }
-}
 // Row prefetch held in registers between frames: fp16 rows stay packed (2 per VGPR).
+// Loads are unconditional (index clamped); the out-of-range select at issue makes the
+// fetch wait for its row, which measured faster than a select at use (5.87 vs 6.13 ms
+// for k_den_fb: the consume loads then no longer queue behind the HBM row in vmcnt).
 template <typename XT> struct RowPre {
     float v[DEN_MAXPT];
-    __device__ __forceinline__ void fetch(const XT *row, int P) { den_fetch_row(v, row, P); }
-    __device__ __forceinline__ float get(int i) const { return v[i]; }
+    __device__ __forceinline__ void fetch(const XT *row, int P) {
+#pragma unroll
+        for (int i = 0; i < DEN_MAXPT; ++i) {
+            int p = threadIdx.x + i * DEN_THREADS;
+            float x = (float)row[min(p, P - 1)];
+            v[i] = p < P ? x : 0.0f;
+        }
+    }
+    __device__ __forceinline__ float get(int i, int) const { return v[i]; }
 };
 template <> struct RowPre<h16> {
     uint32_t v[DEN_MAXPT / 2];
@@ -514,7 +513,7 @@ template <> struct RowPre<h16> {
             v[i] = (p0 < P ? lo : 0u) | ((p1 < P ? hi : 0u) << 16);
         }
     }
-    __device__ __forceinline__ float get(int i) const {
+    __device__ __forceinline__ float get(int i, int) const {
         unsigned short b = (unsigned short)((i & 1) ? (v[i >> 1] >> 16) : (v[i >> 1] & 0xFFFF));
         return (float)__builtin_bit_cast(h16, b);
     }
@@ -531,11 +530,11 @@ struct StatePre {  // alpha' row prefetch (S <= DEN_MAXS * DEN_THREADS)
     }
 };
 
-// fwd / bwd LDS: reduction scratch, the state row (va or vb), the exp row (xe), and
-// the table's slice metadata (len / off / perm / initp / ownership / this block's slots)
+// fwd / bwd LDS: reduction scratch, the NS-interleaved state row (va or vb) and exp row
+// (xe), and the table's slice metadata (len / off / this block's slots / 16-bit perm)
 #define DEN_LDS_TOTAL (160 * 1024)
-static size_t den_rec_fixed_bytes(int S, int P, int nsl, int spg) {
-    return (size_t)4 * (64 + (size_t)S + P + (P & 1) + 2 * (size_t)nsl + 128 * (size_t)nsl + nsl + spg) + 64;
+static size_t den_rec_fixed_bytes(int S, int P, int nsl, int spg, int ns) {
+    return (size_t)4 * (64 + (size_t)ns * ((size_t)S + P + (P & 1)) + 2 * (size_t)nsl + spg) + (size_t)2 * 64 * nsl + 64;
 }
 static size_t den_post_lds_bytes(int S, int P, int nslq, int pair = 1) {
     return (size_t)4 * (64 + 2 * (size_t)pair * S + (size_t)pair * P + (size_t)nslq * 66);
@@ -583,39 +582,49 @@ __device__ __forceinline__ float x_ld(const float *base, int i) {
         return ld_sc1(base + i);
 }
 
+// NS = 2: the blocks of a unit run two sequences at once. The LDS state is
+// interleaved (float2 per state), so one SELL record, one pair of address adds and
+// two 8-byte gathers serve both sequences (the record stream and the gather issue of
+// the arc phase halve per sequence); G doubles so the grid keeps every CU busy.
 struct DenX {
-    float *buf;     // [nseq][2][G][blk]; blk = 64: [wave] = that wave's partial sum (the state
-                    // slices themselves are exchanged through the alpha / beta stores)
+    float *buf;     // [nseq][2][G][blk]; blk = 64: [q * DEN_WAVES + wave] = that wave's partial
+                    // sum of sequence q of the unit (the state slices themselves are exchanged
+                    // through the alpha / beta stores)
     unsigned *cnt;  // [nseq] arrivals (zeroed before each launch)
     unsigned *xm;   // [nseq] XCD census: 4-bit arrival count per XCD (zeroed before each launch)
-    int force_sys;  // 1: agent-scope exchange even when a sequence's blocks share an XCD (tests)
+    int force_sys;  // 1: agent-scope exchange even when a unit's blocks share an XCD (tests)
     unsigned *tmo;  // per-launch timeout word (zeroed before each launch)
     unsigned *sticky;  // timed-out blocks since the last read (never zeroed by a launch)
     unsigned spin_limit;  // polls before a wait gives up (kf_chain_debug_spin_limit)
-    int G, lgG, spg, blk, nseq;  // spg: exchange slots per block (the table's at this G)
-    unsigned lds_f, lds_b;       // dynamic LDS of the fwd / bwd kernels
+    int G, lgG, spg, blk;  // spg: exchange slots per block (the table's at this G)
+    int nseq;              // exchange units (NS sequences each: 2u, 2u+1 for NS = 2)
+    int nseqs, ns;         // sequences, sequences per unit
+    unsigned lds_f, lds_b; // dynamic LDS of the fwd / bwd kernels
 };
 
-// seq / slice-owner of this block; the G blocks of a sequence share an XCD when
-// the grid allows it (blocks b and b+8 share one, MI355X_MICROARCH.md) — speed only
-__device__ __forceinline__ void den_map(const DenX &X, int &seq, int &gi) {
+// unit / slice-owner of this block; the G blocks of a unit share an XCD when the grid
+// allows it (blocks b and b+8 share one, MI355X_MICROARCH.md)
+__device__ __forceinline__ void den_map(const DenX &X, int &unit, int &gi) {
     const int nb = X.nseq * X.G, b = blockIdx.x;
     int w = b;
     if (nb % 8 == 0 && (nb / 8) % X.G == 0) w = (b % 8) * (nb / 8) + b / 8;
-    seq = w >> X.lgG;
+    unit = w >> X.lgG;
     gi = w & (X.G - 1);
 }
 
-// publish: every wave stores its partial sum (lane 0, tail slot `wave`) beside its
-// payload, all sc1; every wave drains vmcnt, the workgroup barriers, one lane adds
-// the arrival (one store drain per frame)
-template <bool LOC>
-__device__ __forceinline__ void den_publish(const DenX &X, float *tail, float wsum, int seq) {
+// publish: every wave stores its NS partial sums (lane 0, tail slots q * DEN_WAVES +
+// wave); every wave drains vmcnt, the workgroup barriers, one lane adds the arrival
+// (one store drain per frame)
+template <bool LOC, int NS>
+__device__ __forceinline__ void den_publish(const DenX &X, float *tail, const float (&wsum)[NS], int unit) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (lane == 0) x_st<LOC>(tail, wave, wsum);
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) x_st<LOC>(tail, q * DEN_WAVES + wave, wsum[q]);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[seq], 1u, RLX_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add((gu32_t *)&X.cnt[unit], 1u, RLX_AGENT);
 }
 // one lane polls `word` until done(value); false on timeout, uniform. *val: the last value
 template <class Done>
@@ -646,15 +655,15 @@ __device__ __forceinline__ bool den_poll(const DenX &X, const unsigned *word, Do
     return *lds_flag != 0;
 }
 // wait for `target` arrivals; false on timeout, uniform
-__device__ __forceinline__ bool den_wait(const DenX &X, int seq, unsigned target, int *lds_flag) {
-    return den_poll(X, &X.cnt[seq], [&](unsigned v) { return v >= target; }, lds_flag);
+__device__ __forceinline__ bool den_wait(const DenX &X, int unit, unsigned target, int *lds_flag) {
+    return den_poll(X, &X.cnt[unit], [&](unsigned v) { return v >= target; }, lds_flag);
 }
-// XCD census before the first exchange: 1 if all G blocks of the sequence run on one
-// XCD (the placement den_map asks the dispatcher for, not a guarantee), 0 if not or
+// XCD census before the first exchange: 1 if all G blocks of the unit run on one XCD
+// (the placement den_map asks the dispatcher for, not a guarantee), 0 if not or
 // forced, -1 on timeout; uniform. Each block adds 1 to its XCD's 4-bit field.
-__device__ __forceinline__ int den_xcd_local(const DenX &X, int seq, int *lds_flag) {
-    if (seq >= X.nseq) return 0;  // grid padding: no exchange
-    unsigned *word = X.xm + seq;
+__device__ __forceinline__ int den_xcd_local(const DenX &X, int unit, int *lds_flag) {
+    if (unit >= X.nseq) return 0;  // grid padding: no exchange
+    unsigned *word = X.xm + unit;
     if (threadIdx.x == 0) {
         const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (3 << 11)) & 7;  // HW_REG_XCC_ID
         __hip_atomic_fetch_add((gu32_t *)word, 1u << (4 * xcc), RLX_AGENT);
@@ -672,316 +681,488 @@ __device__ __forceinline__ int den_xcd_local(const DenX &X, int seq, int *lds_fl
         if (((v >> (4 * k)) & 15) == (unsigned)X.G) one = true;
     return one && !X.force_sys ? 1 : 0;
 }
-// one frame's exchanged state row `row` (slice order: every slice stored sc1 by the
-// block that owns it) and the G x DEN_WAVES partial sums of buffer `buf`: first
-// sum(total, fixed order, equal in every lane), then f(state, value, initp) per row. The
-// partial sums load with the row, so one round trip serves both.
-template <bool LOC, class FS, class F>
-__device__ __forceinline__ void den_consume(const DenX &X, int seq, int buf, const float *row, int nsl,
-                                            const int *perm, const float *initp, FS sum, F f) {
+// NS values per state: the LDS state row is NS-interleaved (one 4 * NS-byte word per state)
+template <int NS> struct DenV {
+    float x[NS];
+};
+template <int NS>
+__device__ __forceinline__ DenV<NS> lds_v(const unsigned char *base, unsigned off) {
+    DenV<NS> r;
+    if constexpr (NS == 2) {
+        const float2 t = *reinterpret_cast<const float2 *>(base + off);
+        r.x[0] = t.x;
+        r.x[1] = t.y;
+    } else {
+        r.x[0] = *reinterpret_cast<const float *>(base + off);
+    }
+    return r;
+}
+
+// Exchanged state rows of the NS sequences of a unit (rows[q], slice order: every slice
+// stored by the block that owns it) and the G x DEN_WAVES partial sums of buffer `buf`:
+// first sum(q, total) for every live q (fixed order, equal in every lane), then
+// f(state, values, initp) per row. Only live sequences are loaded (rows[q] of a sequence
+// past its last frame is never read); their values are 0 in f. The partial sums load
+// with the rows, so one round trip serves both.
+template <bool LOC, int NS, class FS, class F>
+__device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, float *const (&rows)[NS],
+                                            const bool (&live)[NS], int nsl, const short *perm,
+                                            const float *initp, FS sum, F f) {
     int tid = threadIdx.x;
     // opaque to the optimiser: the row addresses below are rebuilt every frame instead of
     // being hoisted out of the frame loop as 64-bit values
     asm volatile("" : "+v"(tid));
     const int n = nsl * 64, lane = tid & 63;
-    const float *xb = X.buf + ((size_t)seq * 2 + buf) * X.G * X.blk;
-    float pv = 0.0f;
-    for (int i = lane; i < X.G * DEN_WAVES; i += 64)
-        pv += x_ld<LOC>(xb, (i / DEN_WAVES) * X.blk + i % DEN_WAVES);
-    float v[DEN_MAXS];
+    const float *xb = X.buf + ((size_t)unit * 2 + buf) * X.G * X.blk;
+    float pv[NS];
 #pragma unroll
-    for (int m = 0; m < DEN_MAXS; ++m) v[m] = x_ld<LOC>(row, min(tid + m * DEN_THREADS, n - 1));  // clamped
-    sum(wave_sum(pv));
+    for (int q = 0; q < NS; ++q) pv[q] = 0.0f;
+    for (int i = lane; i < X.G * DEN_WAVES; i += 64) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+            if (live[q]) pv[q] += x_ld<LOC>(xb, (i / DEN_WAVES) * X.blk + q * DEN_WAVES + i % DEN_WAVES);
+    }
+    float v[NS][DEN_MAXS], ip[DEN_MAXS];
+#pragma unroll
+    for (int m = 0; m < DEN_MAXS; ++m) ip[m] = initp ? initp[min(tid + m * DEN_THREADS, n - 1)] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        if (live[q]) {
+#pragma unroll
+            for (int m = 0; m < DEN_MAXS; ++m) v[q][m] = x_ld<LOC>(rows[q], min(tid + m * DEN_THREADS, n - 1));
+        } else {
+#pragma unroll
+            for (int m = 0; m < DEN_MAXS; ++m) v[q][m] = 0.0f;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+        if (live[q]) sum(q, wave_sum(pv[q]));
 #pragma unroll
     for (int m = 0; m < DEN_MAXS; ++m) {
         const int c = tid + m * DEN_THREADS;
         if (c < n) {
             const int st = perm[c];
-            if (st >= 0) f(st, v[m], initp[c]);
+            DenV<NS> val;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) val.x[q] = v[q][m];
+            if (st >= 0) f(st, val, ip[m]);
         }
     }
 }
 
-// float at LDS byte address `a` of the dynamic LDS (a pre-scaled record field)
-__device__ __forceinline__ float lds_at(const unsigned char *smem, int a) {
-    return *reinterpret_cast<const float *>(smem + a);
+// new state values of the live sequences into the NS-interleaved LDS row (a sequence
+// past its last frame keeps its final state for the end-of-launch totals)
+template <int NS>
+__device__ __forceinline__ void den_put(float *row, int st, const DenV<NS> &v, const bool (&live)[NS]) {
+    if constexpr (NS == 2) {
+        float2 *p = reinterpret_cast<float2 *>(row) + st;
+        if (live[0] && live[1]) *p = make_float2(v.x[0], v.x[1]);
+        else if (live[0]) row[2 * st] = v.x[0];
+        else if (live[1]) row[2 * st + 1] = v.x[1];
+    } else {
+        if (live[0]) row[st] = v.x[0];
+    }
 }
 
-// gather-sum over one slice of a SELL table (fixed arc order)
-template <class Term>
-__device__ __forceinline__ float sell_slice(const uint2 *arcs, int len, int off, int lane, Term term) {
+// gather-sum over one slice of a SELL table for the NS sequences (fixed arc order per
+// sequence). Records carry LDS byte offsets pre-scaled for the NS layout: state row at
+// `sv`, exp row at `sx`.
+template <int NS>
+__device__ __forceinline__ void sell_slice(const uint2 *arcs, int len, int off, int lane, const unsigned char *sv,
+                                           const unsigned char *sx, float (&acc)[NS]) {
+#pragma clang fp contract(off)  // (a * tp) * x + acc rounded as the oracle does, any NS
     const uint2 *e = arcs + (size_t)off * 64 + lane;
-    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) acc[q] = 0.f;
     for (int k = 0; k < len; k += 8) {  // 8 records in flight per lane (len is a multiple of 8)
         uint2 rr[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
+        DenV<NS> a[8], x[8];  // all 16 gathers in flight before the first product
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc += term(rr[i].x & 0xFFFF, rr[i].x >> 16, __uint_as_float(rr[i].y));
+        for (int i = 0; i < 8; ++i) {
+            a[i] = lds_v<NS>(sv, rr[i].x & 0xFFFF);
+            x[i] = lds_v<NS>(sx, rr[i].x >> 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float tp = __uint_as_float(rr[i].y);
+#pragma unroll
+            for (int q = 0; q < NS; ++q) acc[q] += a[i].x[q] * tp * x[i].x[q];
+        }
     }
-    return acc;
 }
 
-// Per-block SELL state in LDS: len / off / perm / initp of every slice, the slice
-// ownership (own[j] = block << 16 | slot) and this block's slot list (slot k is
-// processed by wave k % DEN_WAVES; -1 = empty).
+// Per-block SELL state: len / off / perm (16-bit) of every slice and this block's slot
+// list (slot k is processed by wave k % DEN_WAVES; -1 = empty) in LDS; initp stays in
+// global memory (L2-resident, read once per state per frame), which keeps the NS = 2
+// recursion small enough to share a CU with the numerator kernel on the side stream.
 struct SellLds {
     const int *len, *off;  // [nsl] each
-    const int *perm;       // [nsl*64]
-    const float *initp;    // [nsl*64]
-    const int *own;        // [nsl]
     const int *slot;       // [spg]
+    const short *perm;     // [nsl*64]
+    const float *initp;    // [nsl*64], global
 };
 __device__ __forceinline__ SellLds stage_sell(const SellDev &T, int lgG, int gi, int spg, unsigned char *base) {
     int *lenl = reinterpret_cast<int *>(base), *offl = lenl + T.nsl;
-    int *perml = offl + T.nsl;
-    float *initl = reinterpret_cast<float *>(perml + T.nsl * 64);
-    int *ownl = reinterpret_cast<int *>(initl + T.nsl * 64);
-    int *slotl = ownl + T.nsl;
+    int *slotl = offl + T.nsl;
+    short *perml = reinterpret_cast<short *>(slotl + spg);
     for (int i = threadIdx.x; i < T.nsl; i += DEN_THREADS) {
         lenl[i] = T.len[i];
         offl[i] = T.off[i];
-        ownl[i] = T.own[lgG][i];
     }
-    for (int i = threadIdx.x; i < T.nsl * 64; i += DEN_THREADS) {
-        perml[i] = T.perm[i];
-        initl[i] = T.initp[i];
-    }
+    for (int i = threadIdx.x; i < T.nsl * 64; i += DEN_THREADS) perml[i] = (short)T.perm[i];
     for (int i = threadIdx.x; i < spg; i += DEN_THREADS) slotl[i] = T.slot[lgG][gi * spg + i];
-    SellLds L{lenl, offl, perml, initl, ownl, slotl};
+    SellLds L{lenl, offl, slotl, perml, T.initp};
     return L;
 }
 
-// Forward pass (chain_den.cu:583-620), G blocks per sequence: block gi computes
-// alpha[t+1] for the destination rows of its slices (a load-balanced share, SellDev::
-// slot) and stores them (sc1) into row t+1 of the alpha store, which is also the
-// exchange: all blocks rebuild the full alpha'[t+1] in LDS from that row. The store keeps
-// the slices before the leaky term: alpha'[t] = row[t] + asum[t] * leaky * init, which
-// k_den_post applies when it loads the row (one write per frame, not two).
-template <typename XT, bool LOC>
+// The NS sequences of unit `unit` (sequence NS*unit + q; absent past nseqs) and their frame
+// counts, row offsets and liveness at iteration `it` of a recursion.
+template <int NS> struct DenUnit {
+    int seq[NS], T[NS];
+    long long r0[NS];
+    bool has[NS];
+    __device__ __forceinline__ DenUnit(const DenRun &r, const DenX &X, int unit) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            seq[q] = unit * NS + q;
+            has[q] = unit < X.nseq && seq[q] < X.nseqs;
+            T[q] = has[q] ? r.frames[seq[q]] : 0;
+            r0[q] = has[q] ? r.row0[seq[q]] : 0;
+        }
+    }
+    __device__ __forceinline__ int tmax() const {
+        int m = 0;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) m = max(m, T[q]);
+        return m;
+    }
+};
+
+// exp(clamp(x)) of the NS prefetched rows into the interleaved exp row; 0 for a sequence
+// with no row (`on` false)
+template <typename XT, int NS>
+__device__ __forceinline__ void den_put_exp(float *xe, int P, const RowPre<XT> (&pre)[NS], const bool (&on)[NS]) {
+#pragma unroll
+    for (int i = 0; i < DEN_MAXPT; ++i) {
+        const int p = threadIdx.x + i * DEN_THREADS;
+        if (p < P) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q)  // kernel_apply_exp
+                xe[NS * p + q] = on[q] ? expf(fmaxf(-30.0f, fminf(30.0f, pre[q].get(i, P)))) : 0.0f;
+        }
+    }
+}
+
+// Forward pass (chain_den.cu:583-620), G blocks per unit: block gi computes alpha[t+1]
+// for the destination rows of its slices (a load-balanced share, SellDev::slot) for the
+// NS sequences and stores them into row t+1 of each sequence's alpha store, which is also
+// the exchange: all blocks rebuild the full alpha'[t+1] in LDS from those rows. The store
+// keeps the slices before the leaky term: alpha'[t] = row[t] + asum[t] * leaky * init,
+// which k_den_post applies when it loads the row (one write per frame, not two).
+template <typename XT, bool LOC, int NS>
 __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
-                                             unsigned char *smem, int seq, int gi) {
+                                             unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int G = X.G, nsl = g.f.nsl, spg = X.spg;
     const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);          // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;        // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;      // [S] alpha'[t]
-    float *xe = va + S;                                    // [PP] exp(clamp(x))
-    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + PP);
+    float *va = reinterpret_cast<float *>(smem) + 64;      // [S][NS] alpha'[t]
+    float *xe = va + NS * S;                               // [PP][NS] exp(clamp(x))
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
+    const unsigned char *sv = reinterpret_cast<const unsigned char *>(va);
+    const unsigned char *sx = reinterpret_cast<const unsigned char *>(xe);
 
-    const int T = seq < X.nseq ? r.frames[seq] : 0;
-    const long long r0 = seq < X.nseq ? r.row0[seq] : 0;
+    const DenUnit<NS> U(r, X, unit);
+    const int Tm = U.tmax();
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const int rs = nsl * 64;  // stored rows are in slice order: contiguous, whole lines
     const float leaky = r.leaky;
-    float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rs;
-    float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
-
-    const bool scaled = g.f.arc_s != nullptr;
-    const uint2 *arcs = scaled ? g.f.arc_s : g.f.arc;
+    float *astore[NS], *asum[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const int sq = U.has[q] ? U.seq[q] : 0;
+        astore[q] = r.alpha_store + (size_t)sq * (r.max_frames + 1) * rs;
+        asum[q] = r.asum_store + (size_t)sq * (r.max_frames + 1);
+    }
+    const uint2 *arcs = g.f.arc_p[NS - 1];
     const SellLds F = stage_sell(g.f, X.lgG, gi, spg, sbase);
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
     const float as0 = block_sum<DEN_WAVES>(part, red);  // AlphaFirstFrame + AlphaDash(0)
-    float as = as0;
-    for (int s = tid; s < S; s += DEN_THREADS) va[s] = g.init[s] + as0 * leaky * g.init[s];
-    if (gi == 0 && seq < X.nseq) {
-        for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(F.initp[c], astore + c);
-        if (tid == 0) {
-            asum[0] = as0;
-            r.stats[(size_t)seq * 8 + 3] = 0.0f;  // accumulated by k_den_post
-            r.stats[(size_t)seq * 8 + 6] = 0.0f;
-        }
-    }
-    RowPre<XT> pre;
-    if (T > 0) {
-        pre.fetch(nnet + r0 * r.ld, P);
+    float as[NS];
 #pragma unroll
-        for (int i = 0; i < DEN_MAXPT; ++i) {
-            int p = tid + i * DEN_THREADS;
-            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));  // kernel_apply_exp
+    for (int q = 0; q < NS; ++q) as[q] = as0;
+    for (int s = tid; s < S; s += DEN_THREADS) {
+        const float v = g.init[s] + as0 * leaky * g.init[s];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) va[NS * s + q] = v;
+    }
+    if (gi == 0) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (!U.has[q]) continue;
+            for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(F.initp[c], astore[q] + c);
+            if (tid == 0) {
+                asum[q][0] = as0;
+                r.stats[(size_t)U.seq[q] * 8 + 3] = 0.0f;  // accumulated by k_den_post
+                r.stats[(size_t)U.seq[q] * 8 + 6] = 0.0f;
+            }
         }
     }
+    RowPre<XT> pre[NS];
+    bool on[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        on[q] = U.T[q] > 0;
+        if (on[q]) pre[q].fetch(nnet + U.r0[q] * r.ld, P);
+    }
+    den_put_exp<XT, NS>(xe, P, pre, on);
     __syncthreads();
-    const bool tr = r.trace && seq == 0 && gi == 0 && tid == 0;
+    const bool tr = r.trace && unit == 0 && gi == 0 && tid == 0;
 #define DEN_TP(i) \
     if (tr && t >= 16 && t < 48) r.trace[(t - 16) * 8 + (i)] = wall_clock64();
-    for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < Tm; ++t) {
         DEN_TP(0);
+        bool live[NS];
+        float *arow[NS], inv[NS], pq[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            live[q] = t < U.T[q];
+            arow[q] = astore[q] + (size_t)(t + 1) * rs;
+            inv[q] = as[q] > 0.0f ? 1.0f / as[q] : 1.0f;
+            pq[q] = 0.f;
+        }
         const int buf = (t + 1) & 1;
-        float *tail = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
-        float *arow = astore + (size_t)(t + 1) * rs;
-        const float inv = as > 0.0f ? 1.0f / as : 1.0f;
-        float pq = 0.f;
-        auto term = [&](int src, int pdf, float tp) { return va[src] * tp * xe[pdf]; };
-        auto term_s = [&](int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
+        float *tail = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
         for (int k = wave; k < spg; k += DEN_WAVES) {
             const int j = F.slot[k];
             if (j < 0) continue;
             const int st = F.perm[j * 64 + lane];
-            const float acc = scaled ? sell_slice(arcs, F.len[j], F.off[j], lane, term_s)
-                                     : sell_slice(arcs, F.len[j], F.off[j], lane, term);
-            const float v = st >= 0 ? acc * inv : 0.0f;
-            x_st<LOC>(arow, j * 64 + lane, v);
-            pq += v;
-        }
-        DEN_TP(1);
-        den_publish<LOC>(X, tail, wave_sum(pq), seq);
-        DEN_TP(2);
-        // the next frame's output row: fetched after the publish, so its latency hides under
-        // the exchange wait (fetched at the frame start, the record loads' in-order vmcnt
-        // waits queue behind it: frame 13.3 -> 15.3 us)
-        if (t + 1 < T) pre.fetch(nnet + (r0 + (long long)(t + 1) * r.stride) * r.ld, P);
-        DEN_TP(3);
-        if (!den_wait(X, seq, (unsigned)(G * (t + 1)), flag)) return;
-        DEN_TP(4);
-        float as1 = 0.f;
-        DEN_TP(5);
-        den_consume<LOC>(X, seq, buf, arow, nsl, F.perm, F.initp, [&](float v) { as1 = v; },
-                    [&](int st, float v, float ip) { va[st] = v + as1 * leaky * ip; });
-        DEN_TP(6);
-        // past the publish barrier nothing reads this frame's xe
-        if (t + 1 < T) {
+            float acc[NS];
+            sell_slice<NS>(arcs, F.len[j], F.off[j], lane, sv, sx, acc);
 #pragma unroll
-            for (int i = 0; i < DEN_MAXPT; ++i) {
-                int p = tid + i * DEN_THREADS;
-                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+            for (int q = 0; q < NS; ++q) {
+                const float v = st >= 0 ? acc[q] * inv[q] : 0.0f;
+                if (live[q]) x_st<LOC>(arow[q], j * 64 + lane, v);
+                pq[q] += v;
             }
         }
-        if (gi == 0 && tid == 0) asum[t + 1] = as1;
-        as = as1;
+        if (r.trace && unit == 0 && lane == 0 && t >= 16 && t < 48)  // per-wave arc end, blocks 0, 1
+            r.trace[256 + ((t - 16) * 2 + (gi & 1)) * DEN_WAVES + wave] = wall_clock64();
+        DEN_TP(1);
+        float ws[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) ws[q] = wave_sum(pq[q]);
+        den_publish<LOC, NS>(X, tail, ws, unit);
+        DEN_TP(2);
+        // the next frame's output rows: fetched after the publish, so their latency hides
+        // under the exchange wait (fetched at the frame start, the record loads' in-order
+        // vmcnt waits queue behind them)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            on[q] = t + 1 < U.T[q];
+            if (on[q]) pre[q].fetch(nnet + (U.r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
+        }
+        DEN_TP(3);
+        if (!den_wait(X, unit, (unsigned)(G * (t + 1)), flag)) return;
+        DEN_TP(4);
+        float as1[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) as1[q] = as[q];
+        DEN_TP(5);
+        den_consume<LOC, NS>(X, unit, buf, arow, live, nsl, F.perm, F.initp,
+                             [&](int q, float v) { as1[q] = v; },
+                             [&](int st, DenV<NS> v, float ip) {
+#pragma unroll
+                                 for (int q = 0; q < NS; ++q) v.x[q] += as1[q] * leaky * ip;
+                                 den_put<NS>(va, st, v, live);
+                             });
+        DEN_TP(6);
+        // past the publish barrier nothing reads this frame's xe
+        den_put_exp<XT, NS>(xe, P, pre, on);
+        if (gi == 0 && tid == 0) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q)
+                if (live[q]) asum[q][t + 1] = as1[q];
+        }
+#pragma unroll
+        for (int q = 0; q < NS; ++q) as[q] = as1[q];
         __syncthreads();
         DEN_TP(7);
     }
 #undef DEN_TP
-    if (gi != 0 || seq >= X.nseq) return;
+    if (gi != 0) return;
     // total_prob = sum(alpha'[T]); log_correction = sum_{t<T} log(alpha_sum[t])
-    part = 0.f;
-    for (int s = tid; s < S; s += DEN_THREADS) part += va[s];
-    const float total = block_sum<DEN_WAVES>(part, red);
-    double lc = 0.0;
-    for (int t = tid; t < T; t += DEN_THREADS) {
-        float a = asum[t];
-        if (a > 0.0f) lc += log((double)a);
-    }
-    double *redd = reinterpret_cast<double *>(smem) + 8;  // red[16..31]
-    __syncthreads();
-    lc = block_sum_d<DEN_WAVES>(lc, redd);
-    if (tid == 0) {
-        r.den_out[seq * 2 + 0] = total;
-        r.den_out[seq * 2 + 1] = (float)(log((double)total) + lc);
-        r.stats[(size_t)seq * 8 + 1] = r.den_out[seq * 2 + 1];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        if (!U.has[q]) continue;  // uniform
+        part = 0.f;
+        for (int s = tid; s < S; s += DEN_THREADS) part += va[NS * s + q];
+        const float total = block_sum<DEN_WAVES>(part, red);
+        double lc = 0.0;
+        for (int t = tid; t < U.T[q]; t += DEN_THREADS) {
+            float a = asum[q][t];
+            if (a > 0.0f) lc += log((double)a);
+        }
+        double *redd = reinterpret_cast<double *>(smem) + 8;  // red[16..31]
+        __syncthreads();
+        lc = block_sum_d<DEN_WAVES>(lc, redd);
+        if (tid == 0) {
+            const int sq = U.seq[q];
+            r.den_out[sq * 2 + 0] = total;
+            r.den_out[sq * 2 + 1] = (float)(log((double)total) + lc);
+            r.stats[(size_t)sq * 8 + 1] = r.den_out[sq * 2 + 1];
+        }
+        __syncthreads();
     }
 }
-template <typename XT>
+template <typename XT, int NS>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const DenRun r, const DenX X) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int seq, gi;
-    den_map(X, seq, gi);
-    const int loc = den_xcd_local(X, seq, reinterpret_cast<int *>(smem) + 32);
-    if (loc > 0) den_fwd_body<XT, true>(g, r, X, smem, seq, gi);
-    else if (loc == 0) den_fwd_body<XT, false>(g, r, X, smem, seq, gi);
+    int unit, gi;
+    den_map(X, unit, gi);
+    const int loc = den_xcd_local(X, unit, reinterpret_cast<int *>(smem) + 32);
+    if (loc > 0) den_fwd_body<XT, true, NS>(g, r, X, smem, unit, gi);
+    else if (loc == 0) den_fwd_body<XT, false, NS>(g, r, X, smem, unit, gi);
 }
 
-// Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per
-// sequence: beta'[t] over the source rows of this block's slices, stored (sc1) into row t
-// of the beta store, which is also the exchange; beta[t] = beta'[t] + leaky*<init,
-// beta'[t]>, the second term kept per frame in bsum (k_den_post adds it). The reference scales beta'[t] by 1/sum(alpha[t]) and starts from
-// 1/total_prob; any positive per-frame factor gives the same posteriors once
-// k_den_post normalises each frame (the den posteriors of a frame sum to one:
-// they are d log p / d x_t), so this pass scales by 1/<init, beta'[t+1]> and
-// starts from ones — it needs nothing from the forward pass and runs beside it.
-template <typename XT, bool LOC>
+// Backward recursion (chain_den.cu:632-684 without the posteriors), G blocks per unit:
+// beta'[t] over the source rows of this block's slices for the NS sequences, stored into
+// row t of each sequence's beta store, which is also the exchange; beta[t] = beta'[t] +
+// leaky*<init, beta'[t]>, the second term kept per frame in bsum (k_den_post adds it).
+// The reference scales beta'[t] by 1/sum(alpha[t]) and starts from 1/total_prob; any
+// positive per-frame factor gives the same posteriors once k_den_post normalises each
+// frame (the den posteriors of a frame sum to one: they are d log p / d x_t), so this
+// pass scales by 1/<init, beta'[t+1]> and starts from ones — it needs nothing from the
+// forward pass and runs beside it. Iteration `it` is frame T_q - 1 - it of sequence q.
+template <typename XT, bool LOC, int NS>
 __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, const DenX &X,
-                                             unsigned char *smem, int seq, int gi) {
+                                             unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int G = X.G, nsl = g.b.nsl, spg = X.spg;
     const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);      // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;    // [32]
-    float *vb = reinterpret_cast<float *>(smem) + 64;  // [S] beta[t+1]
-    float *xe = vb + S;                                // [PP] exp(clamp(x))
-    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + PP);
+    float *vb = reinterpret_cast<float *>(smem) + 64;  // [S][NS] beta[t+1]
+    float *xe = vb + NS * S;                           // [PP][NS] exp(clamp(x))
+    unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
+    const unsigned char *sv = reinterpret_cast<const unsigned char *>(vb);
+    const unsigned char *sx = reinterpret_cast<const unsigned char *>(xe);
 
-    const int T = seq < X.nseq ? r.frames[seq] : 0;
-    const long long r0 = seq < X.nseq ? r.row0[seq] : 0;
+    const DenUnit<NS> U(r, X, unit);
+    const int Tm = U.tmax();
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
     const int rs = nsl * 64;
-    float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rs;
-    float *bsum = r.bsum_store + (size_t)seq * (r.max_frames + 1);
     const float leaky = r.leaky;
-
-    const bool scaled = g.b.arc_s != nullptr;
-    const uint2 *arcs = scaled ? g.b.arc_s : g.b.arc;
+    float *bstore[NS], *bsum[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        const int sq = U.has[q] ? U.seq[q] : 0;
+        bstore[q] = r.beta_store + (size_t)sq * (r.max_frames + 1) * rs;
+        bsum[q] = r.bsum_store + (size_t)sq * (r.max_frames + 1);
+    }
+    const uint2 *arcs = g.b.arc_p[NS - 1];
     const SellLds B = stage_sell(g.b, X.lgG, gi, spg, sbase);
     // BetaDashLastFrame up to the per-frame factor: beta'[T] = 1, <init, 1> = sum(init)
     float part = 0.f;
     for (int s = tid; s < S; s += DEN_THREADS) part += g.init[s];
     const float n0 = block_sum<DEN_WAVES>(part, red);
-    float nrm = n0;
-    RowPre<XT> pre;
-    for (int s = tid; s < S; s += DEN_THREADS) vb[s] = 1.0f + leaky * n0;
-    if (gi == 0 && seq < X.nseq) {
-        float *bT = bstore + (size_t)T * rs;
-        for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(1.0f, bT + c);
-        if (tid == 0) bsum[T] = n0;
-    }
-    if (T > 0) {
-        pre.fetch(nnet + (r0 + (long long)(T - 1) * r.stride) * r.ld, P);
+    float nrm[NS];
 #pragma unroll
-        for (int i = 0; i < DEN_MAXPT; ++i) {
-            int p = tid + i * DEN_THREADS;
-            if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+    for (int q = 0; q < NS; ++q) nrm[q] = n0;
+    for (int s = tid; s < S; s += DEN_THREADS) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) vb[NS * s + q] = 1.0f + leaky * n0;
+    }
+    if (gi == 0) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            if (!U.has[q]) continue;
+            float *bT = bstore[q] + (size_t)U.T[q] * rs;
+            for (int c = tid; c < rs; c += DEN_THREADS) __builtin_nontemporal_store(1.0f, bT + c);
+            if (tid == 0) bsum[q][U.T[q]] = n0;
         }
     }
+    RowPre<XT> pre[NS];
+    bool on[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        on[q] = U.T[q] > 0;
+        if (on[q]) pre[q].fetch(nnet + (U.r0[q] + (long long)(U.T[q] - 1) * r.stride) * r.ld, P);
+    }
+    den_put_exp<XT, NS>(xe, P, pre, on);
     __syncthreads();
-    for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
-        const int buf = t & 1;
-        float *tail = X.buf + (((size_t)seq * 2 + buf) * G + gi) * X.blk;
-        float *brow = bstore + (size_t)t * rs;
-        const float inv = nrm > 0.0f ? 1.0f / nrm : 1.0f;
-        float pq = 0.f;
-        auto term = [&](int dst, int pdf, float tp) { return vb[dst] * tp * xe[pdf]; };
-        auto term_s = [&](int a1, int a2, float tp) { return lds_at(smem, a1) * tp * lds_at(smem, a2); };
+    for (int it = 0; it < Tm; ++it) {
+        bool live[NS];
+        int tq[NS];
+        float *brow[NS], inv[NS], pq[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            tq[q] = U.T[q] - 1 - it;
+            live[q] = tq[q] >= 0;
+            brow[q] = bstore[q] + (size_t)max(tq[q], 0) * rs;
+            inv[q] = nrm[q] > 0.0f ? 1.0f / nrm[q] : 1.0f;
+            pq[q] = 0.f;
+        }
+        const int buf = it & 1;
+        float *tail = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
         for (int k = wave; k < spg; k += DEN_WAVES) {  // kernel_den_backward_transitions
             const int j = B.slot[k];
             if (j < 0) continue;
             const int st = B.perm[j * 64 + lane];
-            const float acc = scaled ? sell_slice(arcs, B.len[j], B.off[j], lane, term_s)
-                                     : sell_slice(arcs, B.len[j], B.off[j], lane, term);
-            const float bd = st >= 0 ? acc * inv : 0.0f;
-            x_st<LOC>(brow, j * 64 + lane, bd);
-            pq += B.initp[j * 64 + lane] * bd;
-        }
-        den_publish<LOC>(X, tail, wave_sum(pq), seq);
-        if (t > 0) pre.fetch(nnet + (r0 + (long long)(t - 1) * r.stride) * r.ld, P);  // as den_fwd_body
-        if (!den_wait(X, seq, (unsigned)(G * (it + 1)), flag)) return;
-        float tb = 0.f;
-        den_consume<LOC>(X, seq, buf, brow, nsl, B.perm, B.initp,
-                    [&](float v) {
-                        nrm = v;  // <init, beta'[t]>: the next factor
-                        tb = leaky * nrm;
-                    },
-                    [&](int st, float v, float) { vb[st] = v + tb; });
-        if (gi == 0 && tid == 0) bsum[t] = nrm;
-        if (t > 0) {
+            const float ip = B.initp[j * 64 + lane];
+            float acc[NS];
+            sell_slice<NS>(arcs, B.len[j], B.off[j], lane, sv, sx, acc);
 #pragma unroll
-            for (int i = 0; i < DEN_MAXPT; ++i) {
-                int p = tid + i * DEN_THREADS;
-                if (p < P) xe[p] = expf(fmaxf(-30.0f, fminf(30.0f, pre.get(i))));
+            for (int q = 0; q < NS; ++q) {
+                const float bd = st >= 0 ? acc[q] * inv[q] : 0.0f;
+                if (live[q]) x_st<LOC>(brow[q], j * 64 + lane, bd);
+                pq[q] += ip * bd;
             }
         }
+        float ws[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) ws[q] = wave_sum(pq[q]);
+        den_publish<LOC, NS>(X, tail, ws, unit);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {  // as den_fwd_body
+            on[q] = tq[q] > 0;
+            if (on[q]) pre[q].fetch(nnet + (U.r0[q] + (long long)(tq[q] - 1) * r.stride) * r.ld, P);
+        }
+        if (!den_wait(X, unit, (unsigned)(G * (it + 1)), flag)) return;
+        float tb[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) tb[q] = 0.f;
+        den_consume<LOC, NS>(X, unit, buf, brow, live, nsl, B.perm, nullptr,
+                             [&](int q, float v) {
+                                 nrm[q] = v;  // <init, beta'[t]>: the next factor
+                                 tb[q] = leaky * v;
+                             },
+                             [&](int st, DenV<NS> v, float) {
+#pragma unroll
+                                 for (int q = 0; q < NS; ++q) v.x[q] += tb[q];
+                                 den_put<NS>(vb, st, v, live);
+                             });
+        if (gi == 0 && tid == 0) {
+#pragma unroll
+            for (int q = 0; q < NS; ++q)
+                if (live[q]) bsum[q][tq[q]] = nrm[q];
+        }
+        den_put_exp<XT, NS>(xe, P, pre, on);
         __syncthreads();
     }
 }
 
-// Forward and backward recursions of every sequence in one launch: blocks of the
-// first half run alpha with exchange XF, the second half beta with XB (the two
-// passes are independent, see den_bwd_body). One launch keeps all 2*nseq*G blocks
-// co-resident, which the bounded exchange polls rely on; the XCD grouping of
-// den_map is kept (G consecutive ids share an XCD).
-template <typename XT>
+// Forward and backward recursions of every unit in one launch: blocks of the first half
+// run alpha with exchange XF, the second half beta with XB (the two passes are
+// independent, see den_bwd_body). One launch keeps all 2*units*G blocks co-resident,
+// which the bounded exchange polls rely on; the XCD grouping of den_map is kept (G
+// consecutive ids share an XCD).
+template <typename XT, int NS>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const DenRun r, const DenX XF,
                                                         const DenX XB) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -990,15 +1171,15 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
     if (nb % 8 == 0 && (nb / 8) % XF.G == 0) w = (b % 8) * (nb / 8) + b / 8;
     const bool bwd = w >= half;
     const int inner = bwd ? w - half : w;
-    const int seq = inner >> XF.lgG, gi = inner & (XF.G - 1);
-    const int loc = den_xcd_local(bwd ? XB : XF, seq, reinterpret_cast<int *>(smem) + 32);
+    const int unit = inner >> XF.lgG, gi = inner & (XF.G - 1);
+    const int loc = den_xcd_local(bwd ? XB : XF, unit, reinterpret_cast<int *>(smem) + 32);
     if (loc < 0) return;  // timed out (reported through the timeout words)
     if (bwd) {
-        if (loc) den_bwd_body<XT, true>(g, r, XB, smem, seq, gi);
-        else den_bwd_body<XT, false>(g, r, XB, smem, seq, gi);
+        if (loc) den_bwd_body<XT, true, NS>(g, r, XB, smem, unit, gi);
+        else den_bwd_body<XT, false, NS>(g, r, XB, smem, unit, gi);
     } else {
-        if (loc) den_fwd_body<XT, true>(g, r, XF, smem, seq, gi);
-        else den_fwd_body<XT, false>(g, r, XF, smem, seq, gi);
+        if (loc) den_fwd_body<XT, true, NS>(g, r, XF, smem, unit, gi);
+        else den_fwd_body<XT, false, NS>(g, r, XF, smem, unit, gi);
     }
 }
 
@@ -1320,11 +1501,11 @@ T *dev_upload(const std::vector<T> &v, std::vector<void *> &owned) {
     return (T *)p;
 }
 
-// Slice ownership of SellDev::slot / own for G blocks of DEN_WAVES waves: longest
+// Slice ownership of SellDev::slot for G blocks of DEN_WAVES waves: longest
 // slice first onto the least loaded (block, wave) pair (a slice costs its rows plus a
 // fixed 4 for its per-slice work); bin b is block b % G, wave b / G, so the largest
 // slices also spread over the blocks.
-void den_balance(const std::vector<int> &len, int G, std::vector<int> &slot, std::vector<int> &own, int &spg) {
+void den_balance(const std::vector<int> &len, int G, std::vector<int> &slot, int &spg) {
     const int nsl = (int)len.size(), bins = G * DEN_WAVES;
     std::vector<int> order(nsl);
     for (int j = 0; j < nsl; ++j) order[j] = j;
@@ -1342,14 +1523,9 @@ void den_balance(const std::vector<int> &len, int G, std::vector<int> &slot, std
     for (auto &l : lists) maxc = std::max(maxc, l.size());
     spg = (int)maxc * DEN_WAVES;
     slot.assign((size_t)G * spg, -1);
-    own.assign(nsl, 0);
     for (int b = 0; b < bins; ++b) {
         const int gi = b % G, w = b / G;
-        for (size_t i = 0; i < lists[b].size(); ++i) {
-            const int k = w + DEN_WAVES * (int)i, j = lists[b][i];
-            slot[(size_t)gi * spg + k] = j;
-            own[j] = (gi << 16) | k;
-        }
+        for (size_t i = 0; i < lists[b].size(); ++i) slot[(size_t)gi * spg + w + DEN_WAVES * (int)i] = lists[b][i];
     }
 }
 
@@ -1375,9 +1551,10 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         *why = "num_pdfs > 4096 not supported";
         return nullptr;
     }
+    // S < 8192: the pair records hold 8 * state as a 16-bit LDS byte offset
     if (den_post_lds_bytes(S, P, (P + 63) / 64) > DEN_LDS_TOTAL ||
-        den_rec_fixed_bytes(S, P, (S + 63) / 64, (S + 63) / 64) > DEN_LDS_TOTAL || S > DEN_MAXS * DEN_THREADS) {
-        *why = "den graph too large for the LDS-resident kernels (S <= 8192, ~12*S + 14*P B)";
+        den_rec_fixed_bytes(S, P, (S + 63) / 64, (S + 63) / 64, 1) > DEN_LDS_TOTAL || S >= DEN_MAXS * DEN_THREADS) {
+        *why = "den graph too large for the LDS-resident kernels (S < 8192, ~12*S + 14*P B)";
         return nullptr;
     }
     for (int a = 0; a < A; ++a)
@@ -1402,40 +1579,41 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         o.arc = dev_upload(h.arcs, t->owned);
         ok = ok && o.perm && o.len && o.off && o.arc;
         for (int lg = 0; lg < 4; ++lg) {
-            o.slot[lg] = o.own[lg] = nullptr;
+            o.slot[lg] = nullptr;
             o.spg[lg] = 0;
             if (lg >= ngs) continue;
-            std::vector<int> slot, own;
-            den_balance(h.len, 1 << lg, slot, own, o.spg[lg]);
+            std::vector<int> slot;
+            den_balance(h.len, 1 << lg, slot, o.spg[lg]);
             o.slot[lg] = dev_upload(slot, t->owned);
-            o.own[lg] = dev_upload(own, t->owned);
-            ok = ok && o.slot[lg] && o.own[lg];
+            ok = ok && o.slot[lg];
         }
     };
     put(d.f, sf, 4);
     put(d.b, sb, 4);
     put(d.q, sq, 1);
-    for (int lg = 0; lg < 4 && ok; ++lg)
-        if (den_rec_fixed_bytes(S, P, d.f.nsl, std::max(d.f.spg[lg], d.b.spg[lg])) > DEN_LDS_TOTAL) {
+    d.pair_ok = 1;
+    for (int lg = 0; lg < 4 && ok; ++lg) {
+        const int spg = std::max(d.f.spg[lg], d.b.spg[lg]);
+        if (den_rec_fixed_bytes(S, P, d.f.nsl, spg, 1) > DEN_LDS_TOTAL) {
             delete t;
             *why = "den graph too large for the LDS-resident kernels (slice lists)";
             return nullptr;
         }
-    // pre-scaled copies for the NS = 1 recursions: value row at byte 256 (64 floats of
-    // reduction scratch before it), exp row at 256 + 4 S (den_fwd_body / den_bwd_body)
-    const bool fit16 = 256 + 4 * ((size_t)S + P + 1) < 65536;
-    auto scaled = [&](const Sell &h) {
+        if (den_rec_fixed_bytes(S, P, d.f.nsl, spg, 2) > DEN_LDS_TOTAL) d.pair_ok = 0;
+    }
+    // records with LDS byte offsets for the NS-interleaved rows (den_fwd_body / den_bwd_body)
+    auto scaled = [&](const Sell &h, uint32_t ns) {
         std::vector<uint2> a(h.arcs);
         for (auto &r : a) {
             const uint32_t f1 = r.x & 0xFFFF, f2 = r.x >> 16;
-            r.x = (256 + 4 * f1) | ((256 + 4 * ((uint32_t)S + f2)) << 16);
+            r.x = (4 * ns * f1) | ((4 * ns * f2) << 16);
         }
         return a;
     };
-    if (fit16) {
-        d.f.arc_s = dev_upload(scaled(sf), t->owned);
-        d.b.arc_s = dev_upload(scaled(sb), t->owned);
-        ok = ok && d.f.arc_s && d.b.arc_s;
+    for (int ns = 1; ns <= 2; ++ns) {
+        d.f.arc_p[ns - 1] = dev_upload(scaled(sf, ns), t->owned);
+        d.b.arc_p[ns - 1] = dev_upload(scaled(sb, ns), t->owned);
+        ok = ok && d.f.arc_p[ns - 1] && d.b.arc_p[ns - 1];
     }
     std::vector<float> zf(sf.perm.size(), 0.0f), zb(sb.perm.size(), 0.0f);
     d.f.initp = dev_upload(zf, t->owned);  // filled by den_tables_set_init
@@ -1502,16 +1680,18 @@ struct DenXBuf {
         if (buf) hipFree(buf);
         if (cnt) hipFree(cnt);
     }
-    // nseq sequences, G blocks each, over table `tb` (the f table for the forward
-    // recursion, b for the backward)
-    bool make(const DenDev &g, const SellDev &tb, int nseq, int G, DenX &X) {
+    // nseqs sequences in units of ns, G blocks per unit, over table `tb` (the f table for
+    // the forward recursion, b for the backward)
+    bool make(const DenDev &g, const SellDev &tb, int nseqs, int ns, int G, DenX &X) {
         X.G = G;
-        X.nseq = nseq;
+        X.ns = ns;
+        X.nseqs = nseqs;
+        X.nseq = (nseqs + ns - 1) / ns;
         X.lgG = G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
         X.spg = tb.spg[X.lgG];
         X.blk = 64;  // partial sums only: the slices go through the alpha / beta stores
-        X.lds_f = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.f.nsl, g.f.spg[X.lgG]);
-        X.lds_b = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.b.nsl, g.b.spg[X.lgG]);
+        X.lds_f = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.f.nsl, g.f.spg[X.lgG], ns);
+        X.lds_b = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.b.nsl, g.b.spg[X.lgG], ns);
         size_t nb = (size_t)X.nseq * 2 * G * X.blk * 4;
         size_t nc = (((size_t)X.nseq * 2 + 2) * 4 + 15) / 16 * 16;  // sticky, timeout, counters, census
         if (nb > buf_cap) {
@@ -1565,10 +1745,12 @@ void launch_den_fwd(const DenDev &g, const DenRun &r, const DenX &X, DenXBuf &xb
     hipStream_t st = kf_stream();
     xb.zero(st);
     dim3 grid(X.nseq * X.G);
-    if (fp32_in)
-        hipLaunchKernelGGL((k_den_fwd<float>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+    if (fp32_in)  // the den ABI: one sequence (X.ns == 1)
+        hipLaunchKernelGGL((k_den_fwd<float, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+    else if (X.ns == 2)
+        hipLaunchKernelGGL((k_den_fwd<h16, 2>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
     else
-        hipLaunchKernelGGL((k_den_fwd<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
+        hipLaunchKernelGGL((k_den_fwd<h16, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, X);
 }
 // both recursions in one launch (k_den_fb); XF / XB from two exchange buffers
 void launch_den_fb(const DenDev &g, const DenRun &r, const DenX &XF, DenXBuf &xf, const DenX &XB,
@@ -1578,13 +1760,14 @@ void launch_den_fb(const DenDev &g, const DenRun &r, const DenX &XF, DenXBuf &xf
     xbb.zero(st);
     dim3 grid(2 * XF.nseq * XF.G);
     const size_t lds = std::max(XF.lds_f, XB.lds_b);
-    if (fp32_in) hipLaunchKernelGGL((k_den_fb<float>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
-    else hipLaunchKernelGGL((k_den_fb<h16>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
+    if (fp32_in) hipLaunchKernelGGL((k_den_fb<float, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
+    else if (XF.ns == 2) hipLaunchKernelGGL((k_den_fb<h16, 2>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
+    else hipLaunchKernelGGL((k_den_fb<h16, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
 }
 void launch_den_post(const DenDev &g, const DenRun &r, const DenX &X, bool fp32_in, int mode) {
     hipStream_t st = kf_stream();
     const int nfb = (r.max_frames + POST_FRAMES - 1) / POST_FRAMES;
-    dim3 pgrid(X.nseq * nfb);
+    dim3 pgrid(X.nseqs * nfb);  // per sequence
     // frame pairs share the arc stream when both frames' alpha/beta fit in LDS
     const bool pair = den_post_lds_bytes(g.S, g.P, g.q.nsl, 2) <= DEN_LDS_TOTAL;
     size_t plds = den_post_lds_bytes(g.S, g.P, g.q.nsl, pair ? 2 : 1);
@@ -2266,7 +2449,7 @@ static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_i
     DenX X{}, XB{};
     DenXBuf xbuf, xbuf2;
     const int G = h_post ? den_pick_G(2) : den_pick_G(1);
-    if (!xbuf.make(g, g.f, 1, G, X) || (h_post && !xbuf2.make(g, g.b, 1, G, XB))) {
+    if (!xbuf.make(g, g.f, 1, 1, G, X) || (h_post && !xbuf2.make(g, g.b, 1, 1, G, XB))) {
         den_set_error("den_forward: hipMalloc failed");
         return -1e30f;
     }
@@ -2352,6 +2535,7 @@ struct KfChain {
     hipEvent_t ev_in = nullptr, ev_num = nullptr;
     DenXBuf xbuf;
     unsigned long long *trace = nullptr;  // kf_chain_trace (diagnostics)
+    int den_pairs = 1;                     // kf_chain_debug_den_pairs (tests)
     ~KfChain() {
         if (side) hipStreamDestroy(side);
         if (ev_in) hipEventDestroy(ev_in);
@@ -2636,10 +2820,11 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
     double bytes = frames * (3.0 * 8.0 * c->den->num_arcs + 8.0 * dd.S + 6.0 * dd.P);
     int pd = kf_prof_start(KF_PROF_CHAIN_DEN, bytes);
     DenX X{}, XB{};
-    // forward and backward blocks share the CUs (two sequences sharing each record
-    // read, G = 4, measured slower in r02: 11.6 vs 9.3 ms for 64 sequences)
-    const int G = den_pick_G(2 * nseq);
-    if (!c->xbuf.make(dd, dd.f, nseq, G, X) || !c->xbuf2.make(dd, dd.b, nseq, G, XB)) {
+    // forward and backward blocks share the CUs; sequence pairs (NS = 2) share each
+    // record and gather when their interleaved rows fit the LDS
+    const int ns = nseq >= 2 && dd.pair_ok && c->den_pairs ? 2 : 1;
+    const int G = den_pick_G(2 * ((nseq + ns - 1) / ns));
+    if (!c->xbuf.make(dd, dd.f, nseq, ns, G, X) || !c->xbuf2.make(dd, dd.b, nseq, ns, G, XB)) {
         kfc_set_error("kf_chain_compute: hipMalloc failed");
         return -1;
     }
@@ -2654,9 +2839,10 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
     return 0;
 }
 
-// Diagnostics: when `buf` (device, 32*8 u64) is non-null, the den forward kernel of
-// sequence 0 / block 0 records 8 phase timestamps (wall_clock64, 100 MHz) for frames
-// 16..47 of every later compute. Not part of the product contract.
+// Diagnostics: when `buf` (device, 32*8 + 32*2*16 u64) is non-null, the den forward
+// kernel of sequence 0 / block 0 records 8 phase timestamps (wall_clock64, 100 MHz) for
+// frames 16..47 of every later compute, then the arc-phase end of every wave of blocks
+// 0 and 1 of sequence 0. Not part of the product contract.
 extern "C" void kf_chain_trace(KfChain *c, unsigned long long *buf) {
     if (c) c->trace = buf;
 }
@@ -2667,6 +2853,12 @@ extern "C" void kf_chain_debug_spin_limit(KfChain *c, unsigned polls) {
     if (!c) return;
     const unsigned v = polls == 0xFFFFFFFFu ? (1u << 21) : polls;
     c->xbuf.spin_limit = c->xbuf2.spin_limit = v;
+}
+
+// diagnostics (tests): 0 runs the den recursions one sequence per unit (NS = 1) even
+// where sequence pairs fit; 1 = default
+extern "C" void kf_chain_debug_den_pairs(KfChain *c, int pairs) {
+    if (c) c->den_pairs = pairs ? 1 : 0;
 }
 
 // diagnostics (tests): 1 makes the den exchange use agent scope (sc1 through to memory)

@@ -67,6 +67,7 @@ _sig("kf_chain_seq_stats", _vp, _vp)
 _sig("kf_chain_result", _i, _vp, C.POINTER(KfChainResult))
 _sig("kf_chain_debug_spin_limit", None, _vp, C.c_uint)
 _sig("kf_chain_debug_exchange_sys", None, _vp, C.c_int)
+_sig("kf_chain_debug_den_pairs", None, _vp, C.c_int)
 _sig("chain_forward_backward", _i, _vp, C.POINTER(ChainFstGPU), _i, _i, _vp, _vp, _fp)
 _sig("chain_compute_posteriors", _i, _vp, C.POINTER(ChainFstGPU), _i, _i, _vp, _vp, _f, _vp)
 _sig("chain_compute_loss", _i, _vp, C.POINTER(ChainFstGPU), C.POINTER(ChainFstGPU), _i, _i, _vp,
@@ -200,6 +201,10 @@ class Chain:
     def debug_exchange_sys(self, force: bool):
         """Test knob: den exchange through memory (agent scope) even on one XCD."""
         core.kf_chain_debug_exchange_sys(self.h, 1 if force else 0)
+
+    def debug_den_pairs(self, pairs: bool):
+        """Test knob: den recursions on sequence pairs (default) or one sequence per unit."""
+        core.kf_chain_debug_den_pairs(self.h, 1 if pairs else 0)
 
     def seq_stats(self, nseq: int) -> np.ndarray:
         from . import read_f32, sync

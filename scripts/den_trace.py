@@ -17,15 +17,21 @@ og = torch.zeros((T, P), dtype=torch.float16, device="cuda")
 ch = chain.Chain(chain.DenGraph(synth.make_den_graph(num_pdfs=P)), egs, 490)
 nb = chain.NumBatch([synth.make_num_fst(e) for e in range(egs)])
 row0, nfr, stride = synth.chain_layout(egs)
-tb = torch.zeros(32 * 8, dtype=torch.int64, device="cuda")
+tb = torch.zeros(32 * 8 + 32 * 2 * 16, dtype=torch.int64, device="cuda")
 kfp16.core.kf_chain_trace(ch.h, tb.data_ptr())
 for _ in range(3):
     ch.compute(nb, x.data_ptr(), P, T, row0, nfr, stride, og.data_ptr(), P)
 torch.cuda.synchronize()
-a = tb.cpu().numpy().reshape(32, 8).astype(np.float64) * 10e-3  # 100 MHz ticks -> us
+raw = tb.cpu().numpy().astype(np.float64) * 10e-3  # 100 MHz ticks -> us
+a = raw[:256].reshape(32, 8)
+w = raw[256:].reshape(32, 2, 16) - a[:, None, :1]  # per-wave arc end relative to the frame start
 d = np.diff(a, axis=1)
 names = ["arc", "publish", "prefetch", "wait", "psum", "consume", "tail+bar"]
 print("G", os.environ.get("KF_DEN_G", "auto"), "egs", egs)
 print("mean us per phase:", {n: round(float(v), 2) for n, v in zip(names, d[1:].mean(0))})
 fr = np.diff(a[:, 0])
 print("frame period us: mean %.2f min %.2f max %.2f" % (fr.mean(), fr.min(), fr.max()))
+wend = w[1:].reshape(31, 32)
+print("arc end per wave (us after frame start): mean over waves %.2f, slowest %.2f, wave 0 %.2f" %
+      (wend.mean(), wend.max(1).mean(), w[1:, 0, 0].mean()))
+print("per-(block,wave) mean arc end:", np.round(w[1:].mean(0), 2).tolist())

@@ -232,6 +232,35 @@ def test_batched_objective_repeatable(gpu, den):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+def test_den_sequence_pairs_match_single(gpu, den):
+    """Sequence pairs (two sequences per workgroup set, interleaved LDS state) give the
+    single-sequence recursion's results bit for bit: ragged frame counts (a pair whose
+    members end at different frames, forward and backward) and an odd count (a unit
+    with an absent partner)."""
+    from kfp16 import chain
+    negs = 5
+    g, init, P, row0, frames, stride, fsts, x = _batch_setup(gpu, den, negs, seed=41)
+    frames = frames.copy()
+    frames[1] = 301
+    frames[2] = 420
+    dx = gpu.upload_fp16(x)
+    og = gpu.DeviceBuffer(x.size * 2)
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=negs, max_frames=490)
+    nb = chain.NumBatch(fsts)
+    outs = []
+    for pairs in (False, True):
+        ch.debug_den_pairs(pairs)
+        gpu.core.bridge_gpu_memset(og.ptr, 0, x.size * 2)
+        ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+        res = ch.result()
+        outs.append((res.objf, res.num_ok, ch.seq_stats(negs).copy(), gpu.read_fp16(og.ptr, x.shape)))
+    ch.debug_den_pairs(True)
+    assert outs[0][1] == outs[1][1] == negs
+    np.testing.assert_array_equal(outs[1][2], outs[0][2])
+    np.testing.assert_array_equal(outs[1][3], outs[0][3])
+    assert outs[1][0] == outs[0][0]
+
+
 @pytest.mark.parametrize("negs", [16, pytest.param(64, marks=pytest.mark.slow)])
 def test_den_exchange_xcd_local_matches_agent_scope(gpu, den, negs):
     """The den exchange between the blocks of a sequence that share an XCD (L2-local
