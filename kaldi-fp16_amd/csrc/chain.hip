@@ -430,10 +430,9 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
 struct SellDev {  // sliced ELL, 64 rows per slice, rows sorted by degree
     int nsl;
     const int *perm, *len, *off;
-    const uint2 *arc;     // {f1 | f2 << 16, tp}
-    // f and b only: the same records with f1, f2 replaced by the LDS byte offsets of their
-    // operands in the NS-interleaved state and exp rows (4 * NS * f1, 4 * NS * f2; index
-    // NS - 1), so the gathers need one address add each
+    // records {f1 | f2 << 16, tp} with f1, f2 as the LDS byte offsets of their operands
+    // in rows interleaving NS sequences (f, b) or frames (q): 4 * NS * f1, 4 * NS * f2,
+    // index NS - 1 — one address add per gather
     const uint2 *arc_p[2];
     const float *initp;   // init[perm[c]] in slice order (0 for padding rows), f and b only
     // Slice ownership for G = 1, 2, 4, 8 blocks per sequence (index log2 G): the slices
@@ -1190,9 +1189,12 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
 // runs; a non-finite objective only zeroes what is written. PAIR frames share one
 // stream of the pdf-ordered arc records (the pass is bound by that L2 stream).
 #define POST_FRAMES 4  // frames per block
+// records carry LDS byte offsets into the PAIR-interleaved alpha' / beta rows (one
+// 8-byte gather per operand serves both frames)
 template <int PAIR>
 __device__ __forceinline__ void post_slice(const uint2 *arcs, int len, int off, int lane,
-                                           const float *va, const float *vb, int S, float acc[PAIR]) {
+                                           const unsigned char *sva, const unsigned char *svb, float acc[PAIR]) {
+#pragma clang fp contract(off)  // (alpha * tp) * beta + acc, as the oracle rounds
     const uint2 *e = arcs + (size_t)off * 64 + lane;
 #pragma unroll
     for (int f = 0; f < PAIR; ++f) acc[f] = 0.f;
@@ -1202,10 +1204,10 @@ __device__ __forceinline__ void post_slice(const uint2 *arcs, int len, int off, 
         for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int src = rr[i].x & 0xFFFF, dst = rr[i].x >> 16;
+            const DenV<PAIR> a = lds_v<PAIR>(sva, rr[i].x & 0xFFFF), b = lds_v<PAIR>(svb, rr[i].x >> 16);
             const float tp = __uint_as_float(rr[i].y);
 #pragma unroll
-            for (int f = 0; f < PAIR; ++f) acc[f] += va[f * S + src] * tp * vb[f * S + dst];
+            for (int f = 0; f < PAIR; ++f) acc[f] += a.x[f] * tp * b.x[f];
         }
     }
 }
@@ -1216,8 +1218,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     const int seq = blockIdx.x / nfb, fb = blockIdx.x % nfb;
     const int nslq = g.q.nsl;
     float *red = reinterpret_cast<float *>(smem);      // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;  // [PAIR][S] alpha'[t]
-    float *vb = va + PAIR * S;                         // [PAIR][S] beta[t+1]
+    float *va = reinterpret_cast<float *>(smem) + 64;  // [S][PAIR] alpha'[t+f]
+    float *vb = va + PAIR * S;                         // [S][PAIR] beta[t+f+1]
     float *gam = vb + PAIR * S;                        // [PAIR][P] den, then the gradient
     int *metaq = reinterpret_cast<int *>(gam + PAIR * P);
     const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
@@ -1266,16 +1268,17 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     const bool do_oor = MODE == DEN_PRODUCT && r.opts.out_of_range_regularize > 0.0f;
     const bool do_l2 = MODE == DEN_PRODUCT && r.opts.l2_regularize > 0.0f;
     float oor = 0.f, sq = 0.f;
-    // this thread's rows c = tid + m * DEN_THREADS of both stores: their state and the
-    // initial probability, once for the block's frames (rs <= DEN_MAXS * DEN_THREADS)
-    int pfw[DEN_MAXS], pbw[DEN_MAXS];
+    // this thread's rows c = tid + m * DEN_THREADS of both stores: their states (16 bits
+    // each, 0xFFFF = none: S < 8192) and the initial probability, once for the block's
+    // frames (rs <= DEN_MAXS * DEN_THREADS)
+    unsigned pfb[DEN_MAXS];
     float ipf[DEN_MAXS];
 #pragma unroll
     for (int m = 0; m < DEN_MAXS; ++m) {
         const int c = tid + m * DEN_THREADS;
-        pfw[m] = c < rsf ? g.f.perm[c] : -1;
+        const int pf = c < rsf ? g.f.perm[c] : -1, pb = c < rsb ? g.b.perm[c] : -1;
+        pfb[m] = (unsigned)(pf & 0xFFFF) | ((unsigned)(pb & 0xFFFF) << 16);
         ipf[m] = c < rsf ? g.f.initp[c] : 0.f;
-        pbw[m] = c < rsb ? g.b.perm[c] : -1;
     }
     for (int t = t0; t < t1; t += PAIR) {
         const int nf2 = min(PAIR, t1 - t);
@@ -1299,8 +1302,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
             }
 #pragma unroll
             for (int m = 0; m < DEN_MAXS; ++m) {
-                if (pfw[m] >= 0) va[f * S + pfw[m]] = live ? va_[m] + as1 * leaky * ipf[m] : 0.f;
-                if (pbw[m] >= 0) vb[f * S + pbw[m]] = live ? vb_[m] + tb : 0.f;
+                const unsigned pf = pfb[m] & 0xFFFF, pb = pfb[m] >> 16;
+                if (pf != 0xFFFF) va[PAIR * pf + f] = live ? va_[m] + as1 * leaky * ipf[m] : 0.f;
+                if (pb != 0xFFFF) vb[PAIR * pb + f] = live ? vb_[m] + tb : 0.f;
             }
         }
         __syncthreads();
@@ -1312,7 +1316,8 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
             if (j < 0) continue;
             const int pdf = permq[j * 64 + lane];
             float acc[PAIR];
-            post_slice<PAIR>(g.q.arc, lenq[j], offq[j], lane, va, vb, S, acc);
+            post_slice<PAIR>(g.q.arc_p[PAIR - 1], lenq[j], offq[j], lane, reinterpret_cast<const unsigned char *>(va),
+                             reinterpret_cast<const unsigned char *>(vb), acc);
             if (pdf < 0) continue;
 #pragma unroll
             for (int f = 0; f < PAIR; ++f) {
@@ -1576,8 +1581,7 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         o.perm = dev_upload(h.perm, t->owned);
         o.len = dev_upload(h.len, t->owned);
         o.off = dev_upload(h.off, t->owned);
-        o.arc = dev_upload(h.arcs, t->owned);
-        ok = ok && o.perm && o.len && o.off && o.arc;
+        ok = ok && o.perm && o.len && o.off;
         for (int lg = 0; lg < 4; ++lg) {
             o.slot[lg] = nullptr;
             o.spg[lg] = 0;
@@ -1601,7 +1605,8 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         }
         if (den_rec_fixed_bytes(S, P, d.f.nsl, spg, 2) > DEN_LDS_TOTAL) d.pair_ok = 0;
     }
-    // records with LDS byte offsets for the NS-interleaved rows (den_fwd_body / den_bwd_body)
+    // records with LDS byte offsets for the interleaved rows (den_fwd_body / den_bwd_body,
+    // k_den_post)
     auto scaled = [&](const Sell &h, uint32_t ns) {
         std::vector<uint2> a(h.arcs);
         for (auto &r : a) {
@@ -1613,7 +1618,8 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
     for (int ns = 1; ns <= 2; ++ns) {
         d.f.arc_p[ns - 1] = dev_upload(scaled(sf, ns), t->owned);
         d.b.arc_p[ns - 1] = dev_upload(scaled(sb, ns), t->owned);
-        ok = ok && d.f.arc_p[ns - 1] && d.b.arc_p[ns - 1];
+        d.q.arc_p[ns - 1] = dev_upload(scaled(sq, ns), t->owned);
+        ok = ok && d.f.arc_p[ns - 1] && d.b.arc_p[ns - 1] && d.q.arc_p[ns - 1];
     }
     std::vector<float> zf(sf.perm.size(), 0.0f), zb(sb.perm.size(), 0.0f);
     d.f.initp = dev_upload(zf, t->owned);  // filled by den_tables_set_init
