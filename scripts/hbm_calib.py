@@ -26,4 +26,4 @@ def timeit(fn, reps=20):
 for name, fn, mult in [("fill (write)", lambda: c.fill_(1.0), 1), ("copy (r+w)", lambda: c.copy_(a), 2),
                        ("add (2r+w)", lambda: torch.add(a, b, out=c), 3)]:
     us = timeit(fn)
-    print(f"{name:14s} {us:8.1f} us  {mult * nbytes / us / 1e6:7.0f} GB/s")
+    print(f"{name:14s} {us:8.1f} us  {mult * nbytes / us / 1e3:7.0f} GB/s")
