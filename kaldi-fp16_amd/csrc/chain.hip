@@ -529,14 +529,17 @@ struct StatePre {  // alpha' row prefetch (S <= DEN_MAXS * DEN_THREADS)
     }
 };
 
-// fwd / bwd LDS: reduction scratch, the NS-interleaved state row (va or vb) and exp row
-// (xe), and the table's slice metadata (len / off / this block's slots / 16-bit perm)
+// fwd / bwd LDS: reduction scratch, the NS-interleaved state row (va or vb, nsl * 64
+// entries in the table's slice order) and exp row (xe), and the table's slice metadata
+// (len / off / this block's slots)
 #define DEN_LDS_TOTAL (160 * 1024)
-static size_t den_rec_fixed_bytes(int S, int P, int nsl, int spg, int ns) {
-    return (size_t)4 * (64 + (size_t)ns * ((size_t)S + P + (P & 1)) + 2 * (size_t)nsl + spg) + (size_t)2 * 64 * nsl + 64;
+static size_t den_rec_fixed_bytes(int P, int nsl, int spg, int ns) {
+    return (size_t)4 * (64 + (size_t)ns * ((size_t)nsl * 64 + P + (P & 1)) + 2 * (size_t)nsl + spg) + 64;
 }
-static size_t den_post_lds_bytes(int S, int P, int nslq, int pair = 1) {
-    return (size_t)4 * (64 + 2 * (size_t)pair * S + (size_t)pair * P + (size_t)nslq * 66);
+// posteriors: the alpha' and beta rows of `pair` frames in the f / b tables' slice orders
+// (rs = nsl * 64 entries each), the gamma rows and the q table's perm / len / off
+static size_t den_post_lds_bytes(int rs, int P, int nslq, int pair = 1) {
+    return (size_t)4 * (64 + 2 * (size_t)pair * rs + (size_t)pair * P + (size_t)nslq * 66);
 }
 
 // ---------------------------------------------------------------------------
@@ -700,13 +703,12 @@ __device__ __forceinline__ DenV<NS> lds_v(const unsigned char *base, unsigned of
 // Exchanged state rows of the NS sequences of a unit (rows[q], slice order: every slice
 // stored by the block that owns it) and the G x DEN_WAVES partial sums of buffer `buf`:
 // first sum(q, total) for every live q (fixed order, equal in every lane), then
-// f(state, values, initp) per row. Only live sequences are loaded (rows[q] of a sequence
+// f(slice position, values, initp) per position. Only live sequences are loaded (rows[q] of a sequence
 // past its last frame is never read); their values are 0 in f. The partial sums load
 // with the rows, so one round trip serves both.
 template <bool LOC, int NS, class FS, class F>
 __device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, float *const (&rows)[NS],
-                                            const bool (&live)[NS], int nsl, const short *perm,
-                                            const float *initp, FS sum, F f) {
+                                            const bool (&live)[NS], int nsl, const float *initp, FS sum, F f) {
     int tid = threadIdx.x;
     // opaque to the optimiser: the row addresses below are rebuilt every frame instead of
     // being hoisted out of the frame loop as 64-bit values
@@ -741,11 +743,10 @@ __device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, fl
     for (int m = 0; m < DEN_MAXS; ++m) {
         const int c = tid + m * DEN_THREADS;
         if (c < n) {
-            const int st = perm[c];
             DenV<NS> val;
 #pragma unroll
             for (int q = 0; q < NS; ++q) val.x[q] = v[q][m];
-            if (st >= 0) f(st, val, ip[m]);
+            f(c, val, ip[m]);
         }
     }
 }
@@ -793,27 +794,26 @@ __device__ __forceinline__ void sell_slice(const uint2 *arcs, int len, int off, 
     }
 }
 
-// Per-block SELL state: len / off / perm (16-bit) of every slice and this block's slot
-// list (slot k is processed by wave k % DEN_WAVES; -1 = empty) in LDS; initp stays in
-// global memory (L2-resident, read once per state per frame), which keeps the NS = 2
-// recursion small enough to share a CU with the numerator kernel on the side stream.
+// Per-block SELL state: len / off of every slice and this block's slot list (slot k is
+// processed by wave k % DEN_WAVES; -1 = empty) in LDS; initp stays in global memory
+// (L2-resident, read once per position per frame), which keeps the NS = 2 recursion small
+// enough to share a CU with the numerator kernel on the side stream. States are named by
+// slice position (make_den_tables), so no permutation is needed: positions >= S are
+// padding.
 struct SellLds {
     const int *len, *off;  // [nsl] each
     const int *slot;       // [spg]
-    const short *perm;     // [nsl*64]
     const float *initp;    // [nsl*64], global
 };
 __device__ __forceinline__ SellLds stage_sell(const SellDev &T, int lgG, int gi, int spg, unsigned char *base) {
     int *lenl = reinterpret_cast<int *>(base), *offl = lenl + T.nsl;
     int *slotl = offl + T.nsl;
-    short *perml = reinterpret_cast<short *>(slotl + spg);
     for (int i = threadIdx.x; i < T.nsl; i += DEN_THREADS) {
         lenl[i] = T.len[i];
         offl[i] = T.off[i];
     }
-    for (int i = threadIdx.x; i < T.nsl * 64; i += DEN_THREADS) perml[i] = (short)T.perm[i];
     for (int i = threadIdx.x; i < spg; i += DEN_THREADS) slotl[i] = T.slot[lgG][gi * spg + i];
-    SellLds L{lenl, offl, slotl, perml, T.initp};
+    SellLds L{lenl, offl, slotl, T.initp};
     return L;
 }
 
@@ -869,8 +869,9 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);          // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;        // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;      // [S][NS] alpha'[t]
-    float *xe = va + NS * S;                               // [PP][NS] exp(clamp(x))
+    const int rs = nsl * 64;  // rows (LDS and stored) are in slice order: contiguous, whole lines
+    float *va = reinterpret_cast<float *>(smem) + 64;      // [rs][NS] alpha'[t]
+    float *xe = va + NS * rs;                              // [PP][NS] exp(clamp(x))
     unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
     const unsigned char *sv = reinterpret_cast<const unsigned char *>(va);
     const unsigned char *sx = reinterpret_cast<const unsigned char *>(xe);
@@ -878,7 +879,6 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     const DenUnit<NS> U(r, X, unit);
     const int Tm = U.tmax();
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    const int rs = nsl * 64;  // stored rows are in slice order: contiguous, whole lines
     const float leaky = r.leaky;
     float *astore[NS], *asum[NS];
 #pragma unroll
@@ -895,10 +895,11 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     float as[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) as[q] = as0;
-    for (int s = tid; s < S; s += DEN_THREADS) {
-        const float v = g.init[s] + as0 * leaky * g.init[s];
+    for (int c = tid; c < rs; c += DEN_THREADS) {
+        const float ip = F.initp[c];  // init of the state at position c (0 for padding)
+        const float v = ip + as0 * leaky * ip;
 #pragma unroll
-        for (int q = 0; q < NS; ++q) va[NS * s + q] = v;
+        for (int q = 0; q < NS; ++q) va[NS * c + q] = v;
     }
     if (gi == 0) {
 #pragma unroll
@@ -940,12 +941,12 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         for (int k = wave; k < spg; k += DEN_WAVES) {
             const int j = F.slot[k];
             if (j < 0) continue;
-            const int st = F.perm[j * 64 + lane];
+            const bool real = j * 64 + lane < S;  // padding positions stay 0
             float acc[NS];
             sell_slice<NS>(arcs, F.len[j], F.off[j], lane, sv, sx, acc);
 #pragma unroll
             for (int q = 0; q < NS; ++q) {
-                const float v = st >= 0 ? acc[q] * inv[q] : 0.0f;
+                const float v = real ? acc[q] * inv[q] : 0.0f;
                 if (live[q]) x_st<LOC>(arow[q], j * 64 + lane, v);
                 pq[q] += v;
             }
@@ -973,7 +974,7 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
 #pragma unroll
         for (int q = 0; q < NS; ++q) as1[q] = as[q];
         DEN_TP(5);
-        den_consume<LOC, NS>(X, unit, buf, arow, live, nsl, F.perm, F.initp,
+        den_consume<LOC, NS>(X, unit, buf, arow, live, nsl, F.initp,
                              [&](int q, float v) { as1[q] = v; },
                              [&](int st, DenV<NS> v, float ip) {
 #pragma unroll
@@ -1000,7 +1001,7 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
     for (int q = 0; q < NS; ++q) {
         if (!U.has[q]) continue;  // uniform
         part = 0.f;
-        for (int s = tid; s < S; s += DEN_THREADS) part += va[NS * s + q];
+        for (int c = tid; c < rs; c += DEN_THREADS) part += va[NS * c + q];
         const float total = block_sum<DEN_WAVES>(part, red);
         double lc = 0.0;
         for (int t = tid; t < U.T[q]; t += DEN_THREADS) {
@@ -1046,8 +1047,9 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
     const int PP = P + (P & 1);
     float *red = reinterpret_cast<float *>(smem);      // [32]
     int *flag = reinterpret_cast<int *>(smem) + 32;    // [32]
-    float *vb = reinterpret_cast<float *>(smem) + 64;  // [S][NS] beta[t+1]
-    float *xe = vb + NS * S;                           // [PP][NS] exp(clamp(x))
+    const int rs = nsl * 64;
+    float *vb = reinterpret_cast<float *>(smem) + 64;  // [rs][NS] beta[t+1], slice order
+    float *xe = vb + NS * rs;                          // [PP][NS] exp(clamp(x))
     unsigned char *sbase = reinterpret_cast<unsigned char *>(xe + NS * PP);
     const unsigned char *sv = reinterpret_cast<const unsigned char *>(vb);
     const unsigned char *sx = reinterpret_cast<const unsigned char *>(xe);
@@ -1055,7 +1057,6 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
     const DenUnit<NS> U(r, X, unit);
     const int Tm = U.tmax();
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    const int rs = nsl * 64;
     const float leaky = r.leaky;
     float *bstore[NS], *bsum[NS];
 #pragma unroll
@@ -1073,9 +1074,9 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
     float nrm[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) nrm[q] = n0;
-    for (int s = tid; s < S; s += DEN_THREADS) {
+    for (int c = tid; c < rs; c += DEN_THREADS) {
 #pragma unroll
-        for (int q = 0; q < NS; ++q) vb[NS * s + q] = 1.0f + leaky * n0;
+        for (int q = 0; q < NS; ++q) vb[NS * c + q] = 1.0f + leaky * n0;
     }
     if (gi == 0) {
 #pragma unroll
@@ -1112,13 +1113,13 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
         for (int k = wave; k < spg; k += DEN_WAVES) {  // kernel_den_backward_transitions
             const int j = B.slot[k];
             if (j < 0) continue;
-            const int st = B.perm[j * 64 + lane];
+            const bool real = j * 64 + lane < S;  // padding positions stay 0
             const float ip = B.initp[j * 64 + lane];
             float acc[NS];
             sell_slice<NS>(arcs, B.len[j], B.off[j], lane, sv, sx, acc);
 #pragma unroll
             for (int q = 0; q < NS; ++q) {
-                const float bd = st >= 0 ? acc[q] * inv[q] : 0.0f;
+                const float bd = real ? acc[q] * inv[q] : 0.0f;
                 if (live[q]) x_st<LOC>(brow[q], j * 64 + lane, bd);
                 pq[q] += ip * bd;
             }
@@ -1136,7 +1137,7 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
         float tb[NS];
 #pragma unroll
         for (int q = 0; q < NS; ++q) tb[q] = 0.f;
-        den_consume<LOC, NS>(X, unit, buf, brow, live, nsl, B.perm, nullptr,
+        den_consume<LOC, NS>(X, unit, buf, brow, live, nsl, nullptr,
                              [&](int q, float v) {
                                  nrm[q] = v;  // <init, beta'[t]>: the next factor
                                  tb[q] = leaky * v;
@@ -1217,10 +1218,11 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int seq = blockIdx.x / nfb, fb = blockIdx.x % nfb;
     const int nslq = g.q.nsl;
+    const int rsf = g.f.nsl * 64, rsb = g.b.nsl * 64;  // slice-ordered rows (k_den_fb)
     float *red = reinterpret_cast<float *>(smem);      // [32]
-    float *va = reinterpret_cast<float *>(smem) + 64;  // [S][PAIR] alpha'[t+f]
-    float *vb = va + PAIR * S;                         // [S][PAIR] beta[t+f+1]
-    float *gam = vb + PAIR * S;                        // [PAIR][P] den, then the gradient
+    float *va = reinterpret_cast<float *>(smem) + 64;  // [rsf][PAIR] alpha'[t+f], f-table slice order
+    float *vb = va + PAIR * rsf;                       // [rsb][PAIR] beta[t+f+1], b-table slice order
+    float *gam = vb + PAIR * rsb;                      // [PAIR][P] den, then the gradient
     int *metaq = reinterpret_cast<int *>(gam + PAIR * P);
     const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
     for (int i = tid; i < nslq * 64; i += DEN_THREADS) metaq[i] = g.q.perm[i];
@@ -1234,7 +1236,6 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     if (t0 >= t1) return;
     const long long row0 = r.row0[seq];
     const XT *nnet = reinterpret_cast<const XT *>(r.nnet);
-    const int rsf = g.f.nsl * 64, rsb = g.b.nsl * 64;  // slice-ordered rows (k_den_fb)
     const float *astore = r.alpha_store + (size_t)seq * (r.max_frames + 1) * rsf;
     const float *bstore = r.beta_store + (size_t)seq * (r.max_frames + 1) * rsb;
     const float *asum = r.asum_store + (size_t)seq * (r.max_frames + 1);
@@ -1268,16 +1269,13 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     const bool do_oor = MODE == DEN_PRODUCT && r.opts.out_of_range_regularize > 0.0f;
     const bool do_l2 = MODE == DEN_PRODUCT && r.opts.l2_regularize > 0.0f;
     float oor = 0.f, sq = 0.f;
-    // this thread's rows c = tid + m * DEN_THREADS of both stores: their states (16 bits
-    // each, 0xFFFF = none: S < 8192) and the initial probability, once for the block's
-    // frames (rs <= DEN_MAXS * DEN_THREADS)
-    unsigned pfb[DEN_MAXS];
+    // this thread's positions c = tid + m * DEN_THREADS of the alpha' rows: the initial
+    // probability, once for the block's frames (rs <= DEN_MAXS * DEN_THREADS); the rows
+    // are copied to LDS position for position (the records name slice positions)
     float ipf[DEN_MAXS];
 #pragma unroll
     for (int m = 0; m < DEN_MAXS; ++m) {
         const int c = tid + m * DEN_THREADS;
-        const int pf = c < rsf ? g.f.perm[c] : -1, pb = c < rsb ? g.b.perm[c] : -1;
-        pfb[m] = (unsigned)(pf & 0xFFFF) | ((unsigned)(pb & 0xFFFF) << 16);
         ipf[m] = c < rsf ? g.f.initp[c] : 0.f;
     }
     for (int t = t0; t < t1; t += PAIR) {
@@ -1302,9 +1300,9 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
             }
 #pragma unroll
             for (int m = 0; m < DEN_MAXS; ++m) {
-                const unsigned pf = pfb[m] & 0xFFFF, pb = pfb[m] >> 16;
-                if (pf != 0xFFFF) va[PAIR * pf + f] = live ? va_[m] + as1 * leaky * ipf[m] : 0.f;
-                if (pb != 0xFFFF) vb[PAIR * pb + f] = live ? vb_[m] + tb : 0.f;
+                const int c = tid + m * DEN_THREADS;
+                if (c < rsf) va[PAIR * c + f] = live ? va_[m] + as1 * leaky * ipf[m] : 0.f;
+                if (c < rsb) vb[PAIR * c + f] = live ? vb_[m] + tb : 0.f;
             }
         }
         __syncthreads();
@@ -1408,6 +1406,17 @@ struct Sell {
 
 // rows = key states; each row lists (other | pdf<<16, tp) in arc order
 // rows = values of key[] in [0, nrows); each row lists {f1 | f2<<16, tp} in arc order
+// slice position of every row of a SELL table keyed by `key` (rows sorted by degree,
+// stable: the order build_sell uses)
+std::vector<int> sell_positions(int nrows, int A, const int32_t *key) {
+    std::vector<int> deg(nrows, 0), order(nrows), pos(nrows);
+    for (int a = 0; a < A; ++a) deg[key[a]]++;
+    for (int i = 0; i < nrows; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return deg[a] > deg[b]; });
+    for (int i = 0; i < nrows; ++i) pos[order[i]] = i;
+    return pos;
+}
+
 Sell build_sell(int nrows, int A, const int32_t *key, const int32_t *f1, const int32_t *f2,
                 const float *tp, int n1, int n2) {
     Sell s;
@@ -1556,9 +1565,10 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
         *why = "num_pdfs > 4096 not supported";
         return nullptr;
     }
-    // S < 8192: the pair records hold 8 * state as a 16-bit LDS byte offset
-    if (den_post_lds_bytes(S, P, (P + 63) / 64) > DEN_LDS_TOTAL ||
-        den_rec_fixed_bytes(S, P, (S + 63) / 64, (S + 63) / 64, 1) > DEN_LDS_TOTAL || S >= DEN_MAXS * DEN_THREADS) {
+    // S < 8192: the pair records hold 8 * (slice position) as a 16-bit LDS byte offset
+    const int rsS = (S + 63) / 64 * 64;
+    if (den_post_lds_bytes(rsS, P, (P + 63) / 64) > DEN_LDS_TOTAL ||
+        den_rec_fixed_bytes(P, (S + 63) / 64, (S + 63) / 64, 1) > DEN_LDS_TOTAL || S >= DEN_MAXS * DEN_THREADS) {
         *why = "den graph too large for the LDS-resident kernels (S < 8192, ~12*S + 14*P B)";
         return nullptr;
     }
@@ -1568,9 +1578,20 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
             *why = "den transition out of range (state, pdf or negative probability)";
             return nullptr;
         }
-    Sell sf = build_sell(S, A, dst, src, pdf0, tp, S, P);
-    Sell sb = build_sell(S, A, src, dst, pdf0, tp, S, P);
-    Sell sq = build_sell(P, A, pdf0, src, dst, tp, S, S);
+    // The recursions and the posteriors keep their state rows in LDS in the f (alpha') and
+    // b (beta) tables' slice orders, the layout the stores use: the records name states
+    // by slice position, so the per-frame row copies into LDS are linear (no permutation,
+    // no bank conflicts) and the padding positions hold zeros (or, in beta rows, values
+    // only tp = 0 padding records read).
+    const std::vector<int> posf = sell_positions(S, A, dst), posb = sell_positions(S, A, src);
+    std::vector<int32_t> src_f(A), dst_b(A);
+    for (int a = 0; a < A; ++a) {
+        src_f[a] = posf[src[a]];
+        dst_b[a] = posb[dst[a]];
+    }
+    Sell sf = build_sell(S, A, dst, src_f.data(), pdf0, tp, rsS, P);
+    Sell sb = build_sell(S, A, src, dst_b.data(), pdf0, tp, rsS, P);
+    Sell sq = build_sell(P, A, pdf0, src_f.data(), dst_b.data(), tp, rsS, rsS);
     auto *t = new DenTables();
     DenDev &d = t->dev;
     d.S = S;
@@ -1598,12 +1619,12 @@ DenTables *make_den_tables(int S, int P, int A, const int32_t *src, const int32_
     d.pair_ok = 1;
     for (int lg = 0; lg < 4 && ok; ++lg) {
         const int spg = std::max(d.f.spg[lg], d.b.spg[lg]);
-        if (den_rec_fixed_bytes(S, P, d.f.nsl, spg, 1) > DEN_LDS_TOTAL) {
+        if (den_rec_fixed_bytes(P, d.f.nsl, spg, 1) > DEN_LDS_TOTAL) {
             delete t;
             *why = "den graph too large for the LDS-resident kernels (slice lists)";
             return nullptr;
         }
-        if (den_rec_fixed_bytes(S, P, d.f.nsl, spg, 2) > DEN_LDS_TOTAL) d.pair_ok = 0;
+        if (den_rec_fixed_bytes(P, d.f.nsl, spg, 2) > DEN_LDS_TOTAL) d.pair_ok = 0;
     }
     // records with LDS byte offsets for the interleaved rows (den_fwd_body / den_bwd_body,
     // k_den_post)
@@ -1696,8 +1717,8 @@ struct DenXBuf {
         X.lgG = G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
         X.spg = tb.spg[X.lgG];
         X.blk = 64;  // partial sums only: the slices go through the alpha / beta stores
-        X.lds_f = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.f.nsl, g.f.spg[X.lgG], ns);
-        X.lds_b = (unsigned)den_rec_fixed_bytes(g.S, g.P, g.b.nsl, g.b.spg[X.lgG], ns);
+        X.lds_f = (unsigned)den_rec_fixed_bytes(g.P, g.f.nsl, g.f.spg[X.lgG], ns);
+        X.lds_b = (unsigned)den_rec_fixed_bytes(g.P, g.b.nsl, g.b.spg[X.lgG], ns);
         size_t nb = (size_t)X.nseq * 2 * G * X.blk * 4;
         size_t nc = (((size_t)X.nseq * 2 + 2) * 4 + 15) / 16 * 16;  // sticky, timeout, counters, census
         if (nb > buf_cap) {
@@ -1775,8 +1796,9 @@ void launch_den_post(const DenDev &g, const DenRun &r, const DenX &X, bool fp32_
     const int nfb = (r.max_frames + POST_FRAMES - 1) / POST_FRAMES;
     dim3 pgrid(X.nseqs * nfb);  // per sequence
     // frame pairs share the arc stream when both frames' alpha/beta fit in LDS
-    const bool pair = den_post_lds_bytes(g.S, g.P, g.q.nsl, 2) <= DEN_LDS_TOTAL;
-    size_t plds = den_post_lds_bytes(g.S, g.P, g.q.nsl, pair ? 2 : 1);
+    const int rs = g.f.nsl * 64;  // = g.b.nsl * 64
+    const bool pair = den_post_lds_bytes(rs, g.P, g.q.nsl, 2) <= DEN_LDS_TOTAL;
+    size_t plds = den_post_lds_bytes(rs, g.P, g.q.nsl, pair ? 2 : 1);
 #define KF_POST(XT_, MODE_, PAIR_) \
     hipLaunchKernelGGL((k_den_post<XT_, MODE_, PAIR_>), pgrid, dim3(DEN_THREADS), plds, st, g, r, nfb)
     if (mode == DEN_PRODUCT) {
