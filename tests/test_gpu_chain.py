@@ -261,6 +261,34 @@ def test_den_sequence_pairs_match_single(gpu, den):
     assert outs[1][0] == outs[0][0]
 
 
+def test_den_pairs_beyond_co_resident_grid(gpu, den):
+    """More sequences than the CUs hold at G >= 2 (300 egs of 20 frames): one workgroup
+    per unit (G = 1, no cross-workgroup exchange), sequence pairs and single sequences
+    bit-identical, every objective finite."""
+    from kfp16 import chain, synth
+    g, init = den
+    P, negs = g["P"], 300
+    row0, frames, stride = synth.chain_layout(negs, 90)
+    fsts = [synth.make_num_fst(i, num_states=10) for i in range(negs)]
+    x = _x(negs * 90, P, 51)
+    dx = gpu.upload_fp16(x)
+    og = gpu.DeviceBuffer(x.size * 2)
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=negs, max_frames=int(frames.max()))
+    nb = chain.NumBatch(fsts)
+    outs = []
+    for pairs in (False, True):
+        ch.debug_den_pairs(pairs)
+        gpu.core.bridge_gpu_memset(og.ptr, 0, x.size * 2)
+        ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+        res = ch.result()
+        outs.append((res.objf, res.num_ok, ch.seq_stats(negs).copy(), gpu.read_fp16(og.ptr, x.shape)))
+    ch.debug_den_pairs(True)
+    assert outs[0][1] == outs[1][1] == negs
+    assert np.isfinite(outs[1][0])
+    np.testing.assert_array_equal(outs[1][2], outs[0][2])
+    np.testing.assert_array_equal(outs[1][3], outs[0][3])
+
+
 @pytest.mark.parametrize("negs", [16, pytest.param(64, marks=pytest.mark.slow)])
 def test_den_exchange_xcd_local_matches_agent_scope(gpu, den, negs):
     """The den exchange between the blocks of a sequence that share an XCD (L2-local
