@@ -221,10 +221,26 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
     constexpr int ITEMS = 32 * CG / 64;
     static_assert(ITEMS * 64 == 32 * CG, "items per lane");
     static_assert(TM % 2 == 0, "epilogue stages 32 rows");
-    // row operands (residual, old C, input mask) of 32-row chunk ic + 1 are in
-    // flight while chunk ic is processed (two register slots)
-    half8 rres[2][ITEMS], cold[2][ITEMS];
+    // Row operands (residual, old C, input mask) of the 32-row chunks. The residual rows
+    // sit in a ring of NSL register slots, the others in two: chunk ic + NSL - 1 (ic + 1)
+    // is issued while chunk ic is processed. When the whole wave tile fits (NSL = TM / 2,
+    // small ITEMS), every chunk's residual loads are issued before the first chunk's
+    // stores, so no chunk's wait queues behind an earlier chunk's stores (vmcnt is in
+    // order): one memory round trip per tile for the bypass epilogue, not one per chunk.
+    constexpr int NCH = TM / 2;
+    constexpr int NSL = (NCH <= 4 && ITEMS * NCH <= 6) ? NCH : 2;
+    half8 rres[NSL][ITEMS], cold[2][ITEMS];
     unsigned mb[2][ITEMS];
+    auto prefetch_res = [&](auto ICc) {
+        constexpr int icp = decltype(ICc)::value, sl = icp % NSL;
+        static_for<ITEMS>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+            const int m = m0 + wm * WTM + icp * 32 + r, n = n0 + wn * WTN + 8 * cg;
+            rres[sl][k] = half8{};
+            if (m < M && n < N && E.resid) rres[sl][k] = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
+        });
+    };
     auto prefetch = [&](auto ICc) {
         constexpr int icp = decltype(ICc)::value, sl = icp & 1;
         static_for<ITEMS>([&](auto K) {
@@ -232,18 +248,18 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
             const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
             const int m = m0 + wm * WTM + icp * 32 + r, n = n0 + wn * WTN + 8 * cg;
             const bool ok = m < M && n < N;
-            rres[sl][k] = half8{};
             cold[sl][k] = half8{};
             mb[sl][k] = 0xFFu;
-            if (ok && E.resid) rres[sl][k] = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
             if (ok && E.beta != 0.f) cold[sl][k] = load_h8((const h16 *)E.out + (long long)m * E.ldo + n);
             if (ok && E.mask_in) mb[sl][k] = E.mask_in[((long long)m * E.ldo2 + n) >> 3];
         });
     };
+    static_for<NSL - 1>([&](auto IC) { prefetch_res(IC); });
     prefetch(std::integral_constant<int, 0>{});
-    static_for<TM / 2>([&](auto IC) {
-        constexpr int ic = decltype(IC)::value, sl = ic & 1;
-        if constexpr (ic + 1 < TM / 2) prefetch(std::integral_constant<int, ic + 1>{});
+    static_for<NCH>([&](auto IC) {
+        constexpr int ic = decltype(IC)::value, sl = ic & 1, slr = ic % NSL;
+        if constexpr (ic + NSL - 1 < NCH) prefetch_res(std::integral_constant<int, ic + NSL - 1>{});
+        if constexpr (ic + 1 < NCH) prefetch(std::integral_constant<int, ic + 1>{});
         static_for<2>([&](auto I2) {
             static_for<TN>([&](auto J) {
                 const int c = J * 16 + (lane & 15);
@@ -271,7 +287,7 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
                     v[e] = x0[e];
                     v[e + 4] = x1[e];
                 }
-                epilogue8(E, P, m, n, nl, v, cold[sl][k], rres[sl][k], mb[sl][k]);
+                epilogue8(E, P, m, n, nl, v, cold[sl][k], rres[slr][k], mb[sl][k]);
             }
             if constexpr (CG % 4 == 0) {
                 // MXFP8 copy: the 4 lanes l..l+3 (l % 4 == 0) hold one 32-column block
