@@ -53,14 +53,30 @@ struct ConvC1 {
     int dt[9], dh[9];
 };
 
-__global__ __launch_bounds__(256) void k_conv_c1_fwd(ConvC1 c, const h16 *x, const h16 *W,
-                                                     const h16 *bias, const float *scale,
-                                                     const float *shift, h16 *y, uint8_t *mask) {
-    // the grid stride is a multiple of `groups`, so each thread keeps one filter
-    // group for its whole loop: its 9x8 weights live in registers
-    const int groups = c.fout / 8;
-    const int first = blockIdx.x * blockDim.x + threadIdx.x;
-    const int g = first % groups;
+// First conv layer (one input filter, K <= 9, too thin for MFMA), forward with ReLU,
+// mask and frozen BatchNorm. The input frames a workgroup touches are staged in LDS
+// once: a workgroup owns C1_TB frames (all output heights), its input tile is
+// [C1_TB + dtmax - dtmin frames][heights dhmin .. (hout-1)*sub + dhmax] as fp32 with the
+// time / height padding as zeros, and every (row, 8-filter group) item reads its <= 9
+// taps from LDS (the 8 groups of a row broadcast one address, consecutive heights are
+// consecutive words) instead of as 2-byte global loads (361 -> 187 us per launch for
+// cnn1 at T = 96,000 against the global-load form). Each thread keeps one 8-filter
+// group's 9 x 8 weights in registers.
+#define C1_TB 16
+__global__ __launch_bounds__(256) void k_conv_c1_fwd_tile(ConvC1 c, int dtmin, int dtmax, int dhmin, int dhmax,
+                                                          const h16 *x, const h16 *W, const h16 *bias,
+                                                          const float *scale, const float *shift, h16 *y,
+                                                          uint8_t *mask) {
+    extern __shared__ float xs[];
+    const int groups = c.fout / 8, tid = threadIdx.x;
+    const int t0 = blockIdx.x * C1_TB, nt = min(C1_TB, c.T - t0);
+    const int wd = (c.hout - 1) * c.sub + dhmax - dhmin + 1, nf = nt + dtmax - dtmin;
+    for (int i = tid; i < nf * wd; i += 256) {
+        const int tt = i / wd, hh = i - tt * wd;
+        const int ts = t0 + dtmin + tt, hs = dhmin + hh;
+        xs[i] = (ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin) ? h2f(x[(long long)ts * c.hin + hs]) : 0.f;
+    }
+    const int g = tid % groups;
     float w[9][8], b[8], sc[8], sf[8];
 #pragma unroll
     for (int o = 0; o < 9; ++o)
@@ -72,69 +88,67 @@ __global__ __launch_bounds__(256) void k_conv_c1_fwd(ConvC1 c, const h16 *x, con
         sc[e] = scale ? scale[8 * g + e] : 1.f;
         sf[e] = scale ? shift[8 * g + e] : 0.f;
     }
-    const int total = c.T * c.hout * groups;  // < 2^31, checked on the host
-    // U items per thread per iteration: their 9 x U tap loads are in flight together
-    // (one item per iteration left the kernel latency-bound at ~1.3 TB/s)
-    constexpr int U = 4;
-    const int stride = gridDim.x * blockDim.x;
-    for (int it0 = first; it0 < total; it0 += U * stride) {
-        float xv[U][9];
-        int rowu[U];
+    int tap[9];  // LDS word offset of each tap relative to (row's frame, h * sub)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int it = it0 + u * stride;
-            const int row = (it < total ? it : first) / groups;  // dead items: any valid row
-            rowu[u] = row;
-            const int t = row / c.hout, h = row - t * c.hout;
+    for (int o = 0; o < 9; ++o) tap[o] = o < c.noff ? (c.dt[o] - dtmin) * wd + c.dh[o] - dhmin : 0;
+    __syncthreads();
+    const int rows = nt * c.hout, step = 256 / groups;
+    for (int row = tid / groups; row < rows; row += step) {
+        const int tl = row / c.hout, h = row - tl * c.hout;
+        const float *xr = xs + tl * wd + h * c.sub;
+        float v[8];
 #pragma unroll
-            for (int o = 0; o < 9; ++o) {
-                const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
-                const bool ok = o < c.noff && ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin;
-                const float v = h2f(x[ok ? ts * c.hin + hs : 0]);
-                xv[u][o] = ok ? v : 0.f;
-            }
+        for (int e = 0; e < 8; ++e) v[e] = b[e];
+#pragma unroll
+        for (int o = 0; o < 9; ++o) {
+            const float xv = o < c.noff ? xr[tap[o]] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaf(xv, w[o][e], v[e]);
         }
+        unsigned bits = 0;
+        half8 out;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int it = it0 + u * stride;
-            if (it >= total) break;
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = b[e];
-#pragma unroll
-            for (int o = 0; o < 9; ++o)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = fmaf(xv[u][o], w[o][e], v[e]);
-            unsigned bits = 0;
-            half8 out;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                float a = v[e];
-                if (a > 0.f) bits |= 1u << e;
-                else a = 0.f;
-                if (scale) a = fmaf(a, sc[e], sf[e]);
-                out[e] = f2h(a);
-            }
-            const long long idx = (long long)rowu[u] * c.fout + 8 * g;
-            store_h8(y + idx, out);
-            if (mask) mask[idx >> 3] = (uint8_t)bits;  // (a dword per 4 lanes via shuffles: slower)
+        for (int e = 0; e < 8; ++e) {
+            float a = v[e];
+            if (a > 0.f) bits |= 1u << e;
+            else a = 0.f;
+            if (scale) a = fmaf(a, sc[e], sf[e]);
+            out[e] = f2h(a);
         }
+        const long long idx = ((long long)(t0 + tl) * c.hout + h) * c.fout + 8 * g;
+        store_h8(y + idx, out);
+        if (mask) mask[idx >> 3] = (uint8_t)bits;
     }
 }
 
 // partial dW / db of the 1-filter conv. Thread = (row group, 8 consecutive
 // filters): 16-byte dz loads, the <= 9 input taps per row read through L1.
 // Each block reduces a contiguous range of rows in a fixed order into
-// slab[block][noff+1][fout] (row noff = bias): deterministic, HBM-rate.
+// slab[block][noff+1][fout] (row noff = bias): deterministic, HBM-rate. The input frames
+// of the block's rows sit in LDS as fp32 with zero padding (as k_conv_c1_fwd_tile), so
+// the taps are LDS reads, not 2-byte global loads.
 constexpr int C1_UNROLL = 4;
-__global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, const h16 *x, const h16 *dz,
-                                                       float *slab, int rows_per_block) {
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [256][10*8]
+__global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, int dtmin, int dtmax, int dhmin, int dhmax,
+                                                       const h16 *x, const h16 *dz, float *slab,
+                                                       int rows_per_block) {
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [256][10*8], then the input tile
     const int fg = c.fout / 8;                 // threads per row
     const int lane_f = threadIdx.x % fg, rg = threadIdx.x / fg, nrg = blockDim.x / fg;
     const int rows = c.T * c.hout;             // < 2^31, checked on the host
     const int r0 = blockIdx.x * rows_per_block;
     const int r1 = min(rows, r0 + rows_per_block);
+    float *xs = red + 256 * 80;
+    const int tb = r0 / c.hout, wd = (c.hout - 1) * c.sub + dhmax - dhmin + 1;
+    const int nf = (max(r1 - 1, r0) / c.hout - tb + 1) + dtmax - dtmin;
+    for (int i = threadIdx.x; i < nf * wd; i += 256) {
+        const int tt = i / wd, hh = i - tt * wd;
+        const int ts = tb + dtmin + tt, hs = dhmin + hh;
+        xs[i] = (ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin) ? h2f(x[(long long)ts * c.hin + hs]) : 0.f;
+    }
+    int tap[9];
+#pragma unroll
+    for (int o = 0; o < 9; ++o) tap[o] = o < c.noff ? (c.dt[o] - dtmin) * wd + c.dh[o] - dhmin : 0;
+    __syncthreads();
     float acc[10][8];
 #pragma unroll
     for (int o = 0; o < 10; ++o)
@@ -151,13 +165,9 @@ __global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, const h16 *x, c
             g[u] = load_h8(dz + (long long)rr * c.fout + 8 * lane_f);
             if (!live) g[u] = half8{};
             const int t = rr / c.hout, h = rr - t * c.hout;
+            const float *xr = xs + (t - tb) * wd + h * c.sub;
 #pragma unroll
-            for (int o = 0; o < 9; ++o) {
-                const int ts = t + c.dt[o], hs = h * c.sub + c.dh[o];
-                const bool ok = o < c.noff && ts >= 0 && ts < c.T && hs >= 0 && hs < c.hin;
-                const float v = h2f(x[ok ? ts * c.hin + hs : 0]);
-                xv[u][o] = ok ? v : 0.f;
-            }
+            for (int o = 0; o < 9; ++o) xv[u][o] = o < c.noff ? xr[tap[o]] : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < C1_UNROLL; ++u)
@@ -289,10 +299,23 @@ int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, co
         c.dt[i] = dt[i];
         c.dh[i] = dh[i];
     }
-    // (a row-per-thread form with all 64 filters measured slower: 359 -> 740 us)
-    const long long total = (long long)T * hout * (fout / 8);
-    k_conv_c1_fwd<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
-        c, (const h16 *)x, (const h16 *)W, (const h16 *)bias, scale, shift, (h16 *)y, mask);
+    // (a row-per-thread form with all 64 filters measured slower)
+    int dtmin = 0, dtmax = 0, dhmin = 0, dhmax = 0;
+    for (int i = 0; i < noff; ++i) {
+        dtmin = std::min(dtmin, dt[i]);
+        dtmax = std::max(dtmax, dt[i]);
+        dhmin = std::min(dhmin, dh[i]);
+        dhmax = std::max(dhmax, dh[i]);
+    }
+    const size_t lds = (size_t)4 * (C1_TB + dtmax - dtmin) * ((hout - 1) * sub + dhmax - dhmin + 1);
+    if (lds > 64 * 1024) {
+        lay_set_error("conv_c1_forward: input tile of %zu bytes exceeds the LDS budget", lds);
+        return -1;
+    }
+    if (T <= 0) return 0;
+    k_conv_c1_fwd_tile<<<(T + C1_TB - 1) / C1_TB, 256, lds, kf_stream()>>>(
+        c, dtmin, dtmax, dhmin, dhmax, (const h16 *)x, (const h16 *)W, (const h16 *)bias, scale, shift, (h16 *)y,
+        mask);
     return lay_check("conv_c1_forward");
 }
 
@@ -320,8 +343,23 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
         lay_set_error("conv_c1_wgrad: workspace");
         return -1;
     }
-    k_conv_c1_wgrad<<<nblk, 256, 256 * 80 * 4, kf_stream()>>>(c, (const h16 *)x, (const h16 *)dz,
-                                                              slab, rpb);
+    int dtmin = 0, dtmax = 0, dhmin = 0, dhmax = 0;
+    for (int i = 0; i < noff; ++i) {
+        dtmin = std::min(dtmin, dt[i]);
+        dtmax = std::max(dtmax, dt[i]);
+        dhmin = std::min(dhmin, dh[i]);
+        dhmax = std::max(dhmax, dh[i]);
+    }
+    // input tile: the frames of rpb rows (+1 for a range straddling frames) plus the time
+    // offsets, heights dhmin .. (hout-1)*sub + dhmax
+    const size_t tile = (size_t)4 * ((rpb + hout - 1) / hout + 1 + dtmax - dtmin) *
+                        ((hout - 1) * sub + dhmax - dhmin + 1);
+    if (256 * 80 * 4 + tile > 160 * 1024) {
+        lay_set_error("conv_c1_wgrad: input tile of %zu bytes exceeds the LDS", tile);
+        return -1;
+    }
+    k_conv_c1_wgrad<<<nblk, 256, 256 * 80 * 4 + tile, kf_stream()>>>(c, dtmin, dtmax, dhmin, dhmax, (const h16 *)x,
+                                                                     (const h16 *)dz, slab, rpb);
     k_conv_c1_reduce<<<n, 256, 0, kf_stream()>>>(slab, nblk, n, dW, db, noff * fout);
     return lay_check("conv_c1_wgrad");
 }
