@@ -1166,6 +1166,9 @@ template <typename XT, int NS>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const DenRun r, const DenX XF,
                                                         const DenX XB) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // the numerator kernel's waves share some of these CUs (side stream, it has ~2 ms of
+    // slack under this launch): the recursion's waves win the issue arbitration
+    __builtin_amdgcn_s_setprio(3);
     const int half = XF.nseq * XF.G, nb = 2 * half, b = blockIdx.x;
     int w = b;
     if (nb % 8 == 0 && (nb / 8) % XF.G == 0) w = (b % 8) * (nb / 8) + b / 8;
