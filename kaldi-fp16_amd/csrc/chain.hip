@@ -216,16 +216,14 @@ __global__ __launch_bounds__(256) void k_logfb(const LogFstDev *fsts, const h16 
 #define NUM_PRE 4  // S, G <= 1024 (larger FSTs use k_logfb)
 
 struct NumLds {  // word offsets into dynamic LDS
-    int a0, a1, ar0, ar1, xg0, xg1, in_ptr, in_src, in_g, in_w, row_ptr, arc_dst, arc_g, arc_w,
-        grp_ptr, gsrc, gdst, gw, gpdf, misc, words;
+    int a0, a1, xg0, xg1, in_ptr, in_src, in_g, in_w, row_ptr, arc_dst, arc_g, arc_w, gpdf, misc, words;
 };
 __host__ __device__ inline NumLds num_lds_layout(int S, int A, int G, int Ag) {
+    (void)Ag;  // the pdf-group arcs are read by k_num_post from global memory
     NumLds L;
     int o = 0;
     L.a0 = o; o += S;
     L.a1 = o; o += S;
-    L.ar0 = o; o += S;
-    L.ar1 = o; o += S;
     L.xg0 = o; o += G;
     L.xg1 = o; o += G;
     L.in_ptr = o; o += S + 1;
@@ -236,20 +234,22 @@ __host__ __device__ inline NumLds num_lds_layout(int S, int A, int G, int Ag) {
     L.arc_dst = o; o += A;
     L.arc_g = o; o += A;
     L.arc_w = o; o += A;
-    L.grp_ptr = o; o += G + 1;
-    L.gsrc = o; o += Ag;
-    L.gdst = o; o += Ag;
-    L.gw = o; o += Ag;
     L.gpdf = o; o += G;
     L.misc = o; o += 4;
     L.words = o;
     return L;
 }
 
+// Workgroups [0, nseq) run the forwards (alpha rows and the total), [nseq, 2 nseq) the
+// backwards at the same time (the backward needs neither alpha nor the total: it stores
+// its beta rows); k_num_post then forms the posteriors from the stored rows. (One
+// workgroup per sequence running both passes took 2.7 ms alone, 4.6 ms beside the den
+// recursion; the split takes 1.8 + 0.7 ms and costs the recursion ~0.25 ms less.)
 __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, const h16 *nnet,
-                                                        long long ld, int P) {
+                                                        long long ld, int P, int nseq) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const LogFstDev f = fsts[blockIdx.x];
+    const bool do_fwd = (int)blockIdx.x < nseq;
+    const LogFstDev f = fsts[(int)blockIdx.x % nseq];
     const int S = f.S, A = f.A, G = f.G, T = f.T, tid = threadIdx.x;
     const int Ag = f.G > 0 ? f.grp_ptr[f.G] : 0;
     const NumLds L = num_lds_layout(S, A, G, Ag);
@@ -261,7 +261,6 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
         I[L.row_ptr + i] = f.row_ptr[i];
     }
     for (int q = tid; q < G; q += NUM_THREADS) I[L.gpdf + q] = f.grp_pdf[q];
-    for (int q = tid; q <= G; q += NUM_THREADS) I[L.grp_ptr + q] = f.grp_ptr[q];
     for (int k = tid; k < A; k += NUM_THREADS) {
         int g0 = f.in_g[k], g1 = f.arc_g[k];
         int p0 = g0 >= 0 ? f.grp_pdf[g0] : 0, p1 = g1 >= 0 ? f.grp_pdf[g1] : 0;
@@ -272,17 +271,13 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
         I[L.arc_g + k] = (p1 > 0 && p1 <= P) ? g1 : -1;
         W[L.arc_w + k] = f.arc_w[k];
     }
-    for (int k = tid; k < Ag; k += NUM_THREADS) {
-        I[L.gsrc + k] = f.gsrc[k];
-        I[L.gdst + k] = f.gdst[k];
-        W[L.gw + k] = f.gw[k];
-    }
     float *cur = W + L.a0, *nxt = W + L.a1;
-    for (int s = tid; s < S; s += NUM_THREADS) {
-        float v = (s == f.start) ? 0.0f : kLogZero;
-        cur[s] = v;
-        f.alpha[s] = v;
-    }
+    if (do_fwd)
+        for (int s = tid; s < S; s += NUM_THREADS) {
+            float v = (s == f.start) ? 0.0f : kLogZero;
+            cur[s] = v;
+            f.alpha[s] = v;
+        }
     __syncthreads();
     auto row_of = [&](int t) { return nnet + (f.row0 + (long long)t * f.stride) * ld; };
     float pre[NUM_PRE];
@@ -304,6 +299,7 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
         }
     };
     // ---- forward
+    if (do_fwd) {
     if (T > 0) {
         fetch_x(0);
         store_x(W + L.xg0);
@@ -341,45 +337,24 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
         W[L.misc] = tot;
         *f.total = tot;
     }
-    // ---- backward + posteriors
+        return;
+    }  // forward
+    // ---- backward: beta rows into f.beta (rows 0 .. T)
     float *bn = W + L.a0, *bc = W + L.a1;  // beta[t+1], beta[t]
     __syncthreads();
-    const float total = W[L.misc];
     for (int s = tid; s < S; s += NUM_THREADS) bn[s] = kLogZero;
-    float apre[NUM_PRE];
-    auto fetch_alpha = [&](int t) {
-        const float *ar = f.alpha + (size_t)t * S;
-#pragma unroll
-        for (int i = 0; i < NUM_PRE; ++i) {
-            int s = tid + i * NUM_THREADS;
-            float v = ar[min(s, S - 1)];
-            apre[i] = s < S ? v : 0.0f;
-        }
-    };
-    auto store_alpha = [&](float *dst) {
-#pragma unroll
-        for (int i = 0; i < NUM_PRE; ++i) {
-            int s = tid + i * NUM_THREADS;
-            if (s < S) dst[s] = apre[i];
-        }
-    };
     if (T > 0) {
         fetch_x(T - 1);
         store_x(W + L.xg0);
-        fetch_alpha(T - 1);
-        store_alpha(W + L.ar0);
-        if (T > 1) {
-            fetch_x(T - 2);
-            fetch_alpha(T - 2);
-        }
+        if (T > 1) fetch_x(T - 2);
     }
     __syncthreads();
     if (tid == 0)
         for (int i = 0; i < f.nfinal; ++i) bn[f.fin_state[i]] = f.fin_w[i];
     __syncthreads();
+    for (int s = tid; s < S; s += NUM_THREADS) f.beta[(size_t)T * S + s] = bn[s];
     for (int t = T - 1, it = 0; t >= 0; --t, ++it) {
         const float *xg = W + ((it & 1) ? L.xg1 : L.xg0);
-        const float *ar = W + ((it & 1) ? L.ar1 : L.ar0);
         for (int s = tid; s < S; s += NUM_THREADS) {
             float v = kLogZero;
             for (int k = I[L.row_ptr + s]; k < I[L.row_ptr + s + 1]; ++k) {
@@ -390,37 +365,49 @@ __global__ __launch_bounds__(NUM_THREADS) void k_num_fb(const LogFstDev *fsts, c
                 v = logadd_dev(v, b + xg[g] + W[L.arc_w + k]);
             }
             bc[s] = v;
-        }
-        float *ps = f.post_sparse + (size_t)t * G;
-        for (int q = tid; q < G; q += NUM_THREADS) {
-            int p = I[L.gpdf + q];
-            float acc = 0.0f;
-            if (p > 0 && p <= P) {
-                const float xv = xg[q];
-                for (int k = I[L.grp_ptr + q]; k < I[L.grp_ptr + q + 1]; ++k) {
-                    float av = ar[I[L.gsrc + k]];
-                    if (av <= kLogZero) continue;
-                    float b = bn[I[L.gdst + k]];
-                    if (b <= kLogZero) continue;
-                    float lp = av + xv + W[L.gw + k] + b - total;
-                    if (lp > 0.0f) lp = 0.0f;  // chain.cu:309-311
-                    acc += expf(lp);
-                }
-            }
-            ps[q] = acc;
+            f.beta[(size_t)t * S + s] = v;
         }
         if (t > 0) {
             store_x(W + ((it & 1) ? L.xg0 : L.xg1));
-            store_alpha(W + ((it & 1) ? L.ar0 : L.ar1));
-            if (t > 1) {
-                fetch_x(t - 2);
-                fetch_alpha(t - 2);
-            }
+            if (t > 1) fetch_x(t - 2);
         }
         __syncthreads();
         float *tmp = bn;
         bn = bc;
         bc = tmp;
+    }
+}
+
+// posteriors of the numerator (after k_num_fb): one workgroup per (sequence,
+// NUM_POST_FR frames) from the stored alpha[t], beta[t+1] and the total — the arithmetic
+// and order of k_num_fb's fused posterior loop
+#define NUM_POST_FR 8
+__global__ __launch_bounds__(NUM_THREADS) void k_num_post(const LogFstDev *fsts, const h16 *nnet, long long ld,
+                                                          int P, int nfb) {
+    const LogFstDev f = fsts[blockIdx.x / nfb];
+    const int t0 = (blockIdx.x % nfb) * NUM_POST_FR;
+    const float total = *f.total;
+    for (int t = t0; t < min(f.T, t0 + NUM_POST_FR); ++t) {
+    const float *ar = f.alpha + (size_t)t * f.S, *bn = f.beta + (size_t)(t + 1) * f.S;
+    const h16 *xr = nnet + (f.row0 + (long long)t * f.stride) * ld;
+    float *ps = f.post_sparse + (size_t)t * f.G;
+    for (int q = threadIdx.x; q < f.G; q += NUM_THREADS) {
+        const int p = f.grp_pdf[q];
+        float acc = 0.0f;
+        if (p > 0 && p <= P) {
+            const float xv = (float)xr[p - 1];
+            for (int k = f.grp_ptr[q]; k < f.grp_ptr[q + 1]; ++k) {
+                float av = ar[f.gsrc[k]];
+                if (av <= kLogZero) continue;
+                float b = bn[f.gdst[k]];
+                if (b <= kLogZero) continue;
+                float lp = av + xv + f.gw[k] + b - total;
+                if (lp > 0.0f) lp = 0.0f;  // chain.cu:309-311
+                acc += expf(lp);
+            }
+        }
+        ps[q] = acc;
+    }
     }
 }
 
@@ -2814,9 +2801,18 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
         hipStream_t saved = kf_stream();
         kf_set_stream((void *)c->side);
         int pn = kf_prof_start(KF_PROF_CHAIN_NUM, num_arcs);
-        if (c->num_lds)
-            hipLaunchKernelGGL(k_num_fb, dim3(nseq), dim3(NUM_THREADS), c->num_lds, c->side,
-                               (const LogFstDev *)c->d_desc, (const h16 *)nnet_output, ld, P);
+        if (c->num_lds) {
+            // forwards and backwards at the same time, then the posteriors (the numerator
+            // shares CUs with the den recursion: the shorter, the less it costs it)
+            hipLaunchKernelGGL(k_num_fb, dim3(2 * nseq), dim3(NUM_THREADS), c->num_lds, c->side,
+                               (const LogFstDev *)c->d_desc, (const h16 *)nnet_output, ld, P, nseq);
+            int maxT = 0;
+            for (int i = 0; i < nseq; ++i) maxT = std::max(maxT, seq_frames[i]);
+            const int nfb = (maxT + NUM_POST_FR - 1) / NUM_POST_FR;
+            if (maxT > 0)
+                hipLaunchKernelGGL(k_num_post, dim3(nseq * nfb), dim3(NUM_THREADS), 0, c->side,
+                                   (const LogFstDev *)c->d_desc, (const h16 *)nnet_output, ld, P, nfb);
+        }
         else
             hipLaunchKernelGGL(k_logfb, dim3(nseq), dim3(256), 0, c->side,
                                (const LogFstDev *)c->d_desc, (const h16 *)nnet_output, ld, P);
