@@ -289,6 +289,45 @@ def test_den_pairs_beyond_co_resident_grid(gpu, den):
     np.testing.assert_array_equal(outs[1][3], outs[0][3])
 
 
+def test_numerator_beyond_lds_path_matches_oracle(gpu, den):
+    """A numerator FST with more than 1024 states (beyond k_num_fb's LDS layout) sends the
+    batch to the global-memory numerator (k_logfb): objective and gradient of both
+    sequences against the oracle, and the small sequence's gradient rows bit-identical to
+    the LDS path's (the two numerator kernels share the arithmetic and its order)."""
+    from kfp16 import chain, synth
+    g, init = den
+    P = g["P"]
+    row0, frames, stride = synth.chain_layout(2, 3400)   # 1123 frames: the 1100-state path fits
+    fsts = [synth.make_num_fst(0), synth.make_num_fst(1, num_states=1100)]
+    x = _x(2 * 3400, P, 61)
+    dx = gpu.upload_fp16(x)
+    og = gpu.DeviceBuffer(x.size * 2)
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=2, max_frames=int(frames.max()))
+    ch.debug_den_pairs(False)   # the one-sequence run below then has the same den units
+    gpu.core.bridge_gpu_memset(og.ptr, 0, x.size * 2)
+    ch.compute(chain.NumBatch(fsts), dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+    res = ch.result()
+    got = gpu.read_fp16(og.ptr, x.shape)
+    stats = ch.seq_stats(2)
+    assert res.num_ok == 2
+    xf = x.astype(np.float32)
+    for i in range(2):
+        rows = row0[i] + np.arange(frames[i]) * stride
+        deriv, r = oracle.chain_objf(g, init, fsts[i], xf[rows])
+        assert abs(stats[i, 0] - r["num_logprob"]) <= 1e-2
+        assert abs(stats[i, 2] - r["objf"]) / frames[i] <= 1e-3
+        ref = -deriv
+        err = np.abs(got[rows].astype(np.float32) - ref) - (1e-4 + np.abs(ref) * 2 ** -10)
+        assert np.all(err <= 0), (i, float(err.max()))
+    # sequence 0 alone fits the LDS numerator
+    gpu.core.bridge_gpu_memset(og.ptr, 0, x.size * 2)
+    ch.compute(chain.NumBatch(fsts[:1]), dx.ptr, P, x.shape[0], row0[:1], frames[:1], stride, og.ptr, P)
+    ch.result()
+    ch.debug_den_pairs(True)
+    rows0 = row0[0] + np.arange(frames[0]) * stride
+    np.testing.assert_array_equal(gpu.read_fp16(og.ptr, x.shape)[rows0], got[rows0])
+
+
 @pytest.mark.parametrize("negs", [16, pytest.param(64, marks=pytest.mark.slow)])
 def test_den_exchange_xcd_local_matches_agent_scope(gpu, den, negs):
     """The den exchange between the blocks of a sequence that share an XCD (L2-local
