@@ -47,6 +47,14 @@ PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5000.0    # MI355X dense FP8 (MX-scaled K=128 MFMA)
 PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 FRAMES_PER_EG = 1500
+# algorithmic MFLOP per input frame: forward, and forward +
+# backward (dW of every layer, dX of all but IDCT and cnn1) — the step's FLOPs for the
+# whole-step MFMA-roofline fraction north_star asks for
+MODEL_MFLOP_PER_FRAME = {"cnn_tdnn_17f.xconfig": (66.24, 198.68),
+                         "cnn_tdnn_17f_3072.xconfig": (165.27, 495.76)}
+# kf_prof classes (include/kf_ops.h) and the step classes the bench line reports
+PROF_CLASSES = {"gemm_fused": (0,), "conv_halo": (4,), "gemm_wgrad": (1,), "conv_wgrad": (5,),
+                "slab_reduce": (6,), "chain_num": (2,), "chain_den": (3,)}
 
 
 def parse(argv=None):
@@ -140,6 +148,32 @@ def host_cores():
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 1
+
+
+def step_classes(cls, steps, peak_tflops):
+    """Per-class table of the timed steps (HIP events on each class's launch stream):
+    launches and ms per step, and the class's algorithmic FLOPs / HBM bytes over its time as
+    fractions of the dense MFMA and HBM peaks. The chain classes count other work: the
+    numerator's arc updates (no fraction) and the den's algorithmic bytes, which stream the
+    ~1 MB arc tables from L2 (fraction of the HBM peak shown for scale only)."""
+    out = []
+    for name, (n, ms, fl, by) in cls.items():
+        if n == 0:
+            continue
+        sec = ms * 1e-3
+        row = {"class": name, "launches_per_step": round(n / steps, 2), "ms_per_step": round(ms / steps, 3)}
+        if name == "chain_num":
+            row["arc_updates_per_s"] = round(fl / sec, 1) if sec > 0 else None
+        elif name == "chain_den":
+            row["alg_GBps"] = round(fl / sec / 1e9, 1) if sec > 0 else None
+            row["hbm_frac"] = round(fl / sec / 1e9 / PEAK_HBM_GBPS, 4) if sec > 0 else None
+        else:
+            tf = fl / sec / 1e12 if sec > 0 else 0.0
+            gbps = by / sec / 1e9 if sec > 0 else 0.0
+            row.update({"mfma_tflops": round(tf, 1), "mfma_frac": round(tf / peak_tflops, 4),
+                        "alg_GBps": round(gbps, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4)})
+        out.append(row)
+    return out
 
 
 def roofline(prof, steps, peak_tflops):
@@ -447,12 +481,17 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
     elapsed = dp.max_over_ranks(elapsed, "cuda")
     dp1 = comm.stats() if comm is not None else (0, 0)
 
-    prof, chain_prof = {}, {}
+    prof, chain_prof, classes = {}, {}, {}
     if prof_on:
-        for cls, name in ((0, "gemm_fused"), (1, "gemm_wgrad")):
-            prof[name] = kfp16.prof_collect2(cls)
-        for cls, name in ((2, "chain_num"), (3, "chain_den")):
-            chain_prof[name] = kfp16.prof_collect(cls)
+        for name, ids in PROF_CLASSES.items():
+            classes[name] = kfp16.prof_collect2(ids[0])
+        # the dominant class of the roofline: every fused launch (tiled GEMM + conv halo),
+        # and every weight-gradient GEMM launch
+        add = lambda a, b: tuple(x + y for x, y in zip(a, b))  # noqa: E731
+        prof["gemm_fused"] = add(classes["gemm_fused"], classes["conv_halo"])
+        prof["gemm_wgrad"] = add(classes["gemm_wgrad"], classes["conv_wgrad"])
+        for name in ("chain_num", "chain_den"):
+            chain_prof[name] = classes[name][:3]
         kfp16.core.kf_prof_reset()
     stats = [0.0] * 5
     if mode == "train":
@@ -461,7 +500,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         res = objective.result()
         stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
                                   "cuda")
-    out = {"T": T, "elapsed": elapsed, "steps": steps, "prof": prof, "chain_prof": chain_prof,
+    out = {"T": T, "elapsed": elapsed, "steps": steps, "prof": prof, "chain_prof": chain_prof, "classes": classes,
+           "xconfig": xconfig, "mode": mode,
            "stats": stats, "ivd": ivd, "dp": (dp1[0] - dp0[0], dp1[1] - dp0[1]),
            "buckets": len(net.dp_plan(bucket_bytes)) if comm is not None else 0}
     ctx = (xcfg, params, bns, den_g, P) if keep else None
@@ -474,8 +514,18 @@ def describe(r, a, world, mode, fp8, xconfig, peak):
     ms_step = r["elapsed"] / r["steps"] * 1e3
     value = r["T"] * world * r["steps"] / r["elapsed"]
     d = {"value": round(value, 1), "ms_per_step": round(ms_step, 3)}
+    mf = MODEL_MFLOP_PER_FRAME.get(r["xconfig"])
+    if mf is not None:
+        # whole step against the dense MFMA roofline: frames/s x algorithmic FLOPs per frame
+        fpf = mf[1] if r["mode"] == "train" else mf[0]
+        d["step_mfma_frac"] = round(value * fpf * 1e6 / (peak * 1e12), 4)
+        d["step_mflop_per_frame"] = fpf
     if r["prof"]:
         d["roofline"] = roofline(r["prof"], r["steps"], peak)
+        d["roofline"]["classes"] = step_classes(r["classes"], r["steps"], peak)
+        # GEMM FLOPs the step executed on MFMA per frame (check of the constant above)
+        gemm_fl = sum(r["classes"][k][2] for k in ("gemm_fused", "conv_halo", "gemm_wgrad", "conv_wgrad"))
+        d["roofline"]["executed_gemm_mflop_per_frame"] = round(gemm_fl / (r["T"] * r["steps"]) / 1e6, 2)
     if mode == "train":
         st = r["stats"]
         d["objf_per_frame"] = round(float(st[0]) / max(float(st[3]), 1.0), 5)
@@ -553,7 +603,7 @@ def main():
                        "global_batch_egs": a.egs * world, "parallelism": f"dp{world}",
                        "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)"},
         }
-        for k in ("objf_per_frame", "objective_finite_seqs"):
+        for k in ("step_mfma_frac", "step_mflop_per_frame", "objf_per_frame", "objective_finite_seqs"):
             if k in d:
                 out[k] = d[k]
         if not fwd_only:

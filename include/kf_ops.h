@@ -215,8 +215,11 @@ int kf_rows_wgrad(const void *x, long long ldx, const void *g, long long ldg, fl
 /* y[r][c] = x[r][c] * scale[c] (fp16 in / out, fp32 scale) */
 int kf_scale_cols(const void *x, long long ldx, const float *scale, void *y, long long ldy, int rows, int cols);
 
-/* optional HIP-event timing of every GEMM launch on the current stream
- * (class 0 = kf_gemm_fused, 1 = kf_gemm_wgrad); collect sums since reset */
+/* optional HIP-event timing of the step's kernel classes on the stream each runs on;
+ * collect sums since reset. Classes: 0 = kf_gemm_fused on the tiled GEMM, 1 = kf_gemm_wgrad
+ * GEMM, 2 = chain numerator (flops = arc updates), 3 = chain den (flops = algorithmic
+ * L2/HBM bytes), 4 = kf_gemm_fused on the 3x3 conv halo kernel, 5 = the conv halo weight
+ * gradient, 6 = the split-K slab reduce (bytes only) */
 void kf_prof_enable(int on);
 int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
 /* the same plus the algorithmic HBM bytes of those launches (GEMM classes: each

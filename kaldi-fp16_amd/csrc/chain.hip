@@ -1737,7 +1737,26 @@ struct DenXBuf {
         X.xm = cnt + 2 + X.nseq;
         X.spin_limit = spin_limit;
         X.force_sys = force_sys;
+        last_units = X.nseq;
+        last_G = G;
         return true;
+    }
+    int last_units = 0, last_G = 0;
+    // units of the last launch whose G workgroups all ran on one XCD (the census words
+    // stay in memory after the launch); -1 on a read error
+    int census_local(hipStream_t st) {
+        if (!cnt || !last_units) return 0;
+        std::vector<unsigned> w(last_units);
+        hipMemcpyAsync(w.data(), cnt + 2 + last_units, (size_t)last_units * 4, hipMemcpyDeviceToHost, st);
+        if (hipStreamSynchronize(st) != hipSuccess) return -1;
+        int n = 0;
+        for (unsigned v : w)
+            for (int k = 0; k < 8; ++k)
+                if (((v >> (4 * k)) & 15) == (unsigned)last_G) {
+                    ++n;
+                    break;
+                }
+        return n;
     }
     // counters and the per-launch timeout word; never the sticky word
     void zero(hipStream_t st) { hipMemsetAsync(cnt + 1, 0, cnt_cap - 4, st); }
@@ -2892,6 +2911,25 @@ extern "C" void kf_chain_debug_den_pairs(KfChain *c, int pairs) {
 // even where the blocks of a sequence share an XCD; 0 = default (L2-local when they do)
 extern "C" void kf_chain_debug_exchange_sys(KfChain *c, int force) {
     if (c) c->xbuf.force_sys = c->xbuf2.force_sys = force ? 1 : 0;
+}
+
+// diagnostics (tests): the XCD census of the last compute's den launch. *units = exchange
+// units per direction; *local_fwd / *local_bwd = units whose G workgroups all ran on one
+// XCD, i.e. took the L2-local exchange unless kf_chain_debug_exchange_sys forced agent
+// scope (*forced = 1). 0, or -1 on error.
+extern "C" int kf_chain_debug_census(KfChain *c, int *units, int *local_fwd, int *local_bwd, int *forced) {
+    if (!c) return -1;
+    hipStream_t st = kf_stream();
+    const int f = c->xbuf.census_local(st), b = c->xbuf2.census_local(st);
+    if (f < 0 || b < 0) {
+        kfc_set_error("kf_chain_debug_census: read failed");
+        return -1;
+    }
+    if (units) *units = c->xbuf.last_units;
+    if (local_fwd) *local_fwd = f;
+    if (local_bwd) *local_bwd = b;
+    if (forced) *forced = c->xbuf.force_sys;
+    return 0;
 }
 
 extern "C" const float *kf_chain_seq_stats(const KfChain *c) { return c ? c->stats : nullptr; }

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wgrad_halo_kernel(OpD B,
 
     SB sb;
     sb.init(B, n0, wave, lane);
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc(H.x), rb = make_rsrc(B.base);
+    const Rsrc rx = make_rsrc(H.x), rb = make_rsrc(B.base);
 
     // halo of K-step ks into image `img`: source frames tb + dtmin .. + nf - 1. Every
     // wave issues exactly hpw pieces (the surplus ones load zeros into `dummy`), so the
@@ -139,8 +139,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wgrad_halo_kernel(OpD B,
                 const unsigned voff = pfo[i] >= 0 && (unsigned)t < (unsigned)H.T
                                           ? (unsigned)t * ldb + (unsigned)(pfo[i] & 0xFFFFF) : BAD;
                 char *d = q < H.npieces ? dst + q * 1024 : dummy;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rx, (__attribute__((address_space(3))) void *)d, 16, voff, 0, 0, 0);
+                lds_dma<16>(rx, d, voff);
             }
         });
     };
@@ -338,7 +337,7 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     }
     H.slab = (float *)ws;
     H.bias_slab = bias_grad ? (float *)(ws + ((slab_bytes + 255) & ~(size_t)255)) : nullptr;
-    const int prof = kf_prof_start2(1, 2.0 * M * N * (double)K,
+    const int prof = kf_prof_start2(5, 2.0 * M * N * (double)K,
                                     (double)a.T * a.hsrc * a.pw * 2.0 + (double)K * N * 2.0 + (double)M * N * 4.0);
     const dim3 grid(tiles * H.splits);
     if (BN == 128) {

@@ -107,8 +107,8 @@ struct ScaleStager {
         });
     }
     // k0 in 2-byte units (the fp16 stagers' unit): fp8 element 2*k0 starts the step
-    __device__ __forceinline__ void issue(const OpD &A, const OpD &B, __amdgpu_buffer_rsrc_t ra,
-                                          __amdgpu_buffer_rsrc_t rb, int k0, char *dst, int wave,
+    __device__ __forceinline__ void issue(const OpD &A, const OpD &B, Rsrc ra,
+                                          Rsrc rb, int k0, char *dst, int wave,
                                           int lane) {
         const int k8 = 2 * k0;
         static_for<SPW>([&](auto I) {
@@ -131,9 +131,8 @@ struct ScaleStager {
                 voff = b0[i] + (unsigned)(k8 >> 5);
             }
             // a wave-uniform branch, not a select: a selected 128-bit resource goes to scratch
-            auto *ldst = (__attribute__((address_space(3))) void *)(dst + ins * 256);
-            if (isA) __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, ldst, 4, voff, 0, 0, 0);
-            else __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, ldst, 4, voff, 0, 0, 0);
+            if (isA) lds_dma<4>(ra, dst + ins * 256, voff);
+            else lds_dma<4>(rb, dst + ins * 256, voff);
         });
     }
 };
@@ -395,8 +394,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     sa.init(A, m0, wave, lane);
     sb.init(B, n0, wave, lane);
     if constexpr (F8) ss.init(A, B, m0, n0, wave, lane);
-    const __amdgpu_buffer_rsrc_t ra = make_rsrc(A.base), rb = make_rsrc(B.base);
-    __amdgpu_buffer_rsrc_t rsa = ra, rsb = rb;
+    const Rsrc ra = make_rsrc(A.base), rb = make_rsrc(B.base);
+    Rsrc rsa = ra, rsb = rb;
     if constexpr (F8) {
         rsa = make_rsrc(A.sc);
         rsb = make_rsrc(B.sc);
@@ -534,11 +533,22 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
 // Halo image: row R = f * hpos + pos holds source frame tbase + f and padded
 // height shp = idx * hmul + par, where pos = par * hpe + idx (heights de-interleaved
 // by parity when hmul = 2, so consecutive output heights read consecutive rows for
-// every tap); 128 bytes per row, 16-byte chunks XOR-swizzled like kc_off.
+// every tap); 128 bytes per row. Row R's 16-byte chunk c sits at halo_off(R, c): 1 KiB
+// piece R / 8, 16-byte slot (c + 2R) mod 16 of 256-byte block c / 2. A fragment read
+// (16 lanes per ds_read_b128 group: eight rows at chunk c0, eight at c0 + 1, c0 even)
+// then hits 16 distinct slots whenever its rows are consecutive halo rows, whatever the
+// first row; with hpos = hout (mod 8) the rows of 16 consecutive output rows are
+// consecutive modulo 8 across frame boundaries too (the host pads hpos when the LDS
+// allows). The kc_off swizzle ((R >> 1) & 7) was 2-way conflicted for half of the
+// starting rows and at every frame boundary (SQ_LDS_BANK_CONFLICT 0.30-0.40 of the
+// LDS cycles).
 // Output row m = (t, h) under tap p reads halo row
 //     (t - tbase) * hpos + h + ctap[p]
 // with ctap[p] = (dt_p - dtmin) * hpos + ((dh_p + pad) % hmul) * hpe + (dh_p + pad) / hmul.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ int halo_off(int R, int c) {
+    return (R >> 3) * 1024 + 256 * (c >> 1) + 16 * ((c + 2 * R) & 15);
+}
 struct HaloArgs {
     const h16 *x;           // source [T x ...] rows of ld elements, heights of pw channels
     long long ld;
@@ -613,26 +623,26 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
 
     SB sb;
     sb.init(B, n0, wave, lane);
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc(H.x), rb = make_rsrc(B.base);
+    const Rsrc rx = make_rsrc(H.x), rb = make_rsrc(B.base);
     const int K = H.ntaps * H.pw;
 
     // halo pieces [q0, q1) of chunk c into image `img`, wave-strided
     auto halo_issue = [&](int c, int img, int q0, int q1) {
         char *dst = dsm + img * H.halo_bytes;
+        // lane l fills 16-byte position l of the piece: chunk kc, row 8q + r with
+        // halo_off(R, kc) = 1024 q + 16 l (block kc / 2 = l / 16, slot (kc + 2r) mod 16 = l mod 16)
+        const int slot = lane & 15, kc = 2 * (lane >> 4) + (slot & 1), r = ((slot - kc) & 15) >> 1;
         for (int q = q0 + wave; q < q1; q += NW) {
-            const int R = 8 * q + (lane >> 3);
+            const int R = 8 * q + r;
             unsigned voff = BAD;
             if (R < H.rows) {
                 const int f = R / H.hpos, pos = R - f * H.hpos;
                 const int par = pos / H.hpe, idx = pos - par * H.hpe;
                 const int sh = idx * H.hmul + par - H.pad, t = tbase + f;
-                if ((unsigned)t < (unsigned)H.T && (unsigned)sh < (unsigned)H.hsrc) {
-                    const int kc = (lane & 7) ^ ((R >> 1) & 7);
+                if ((unsigned)t < (unsigned)H.T && (unsigned)sh < (unsigned)H.hsrc)
                     voff = (unsigned)(((long long)t * H.ld + (long long)sh * H.pw + c * BK + kc * 8) * 2);
-                }
             }
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rx, (__attribute__((address_space(3))) void *)(dst + q * 1024), 16, voff, 0, 0, 0);
+            lds_dma<16>(rx, dst + q * 1024, voff);
         }
     };
 
@@ -726,7 +736,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
             half8 fa[TM], fb[TN];
             static_for<TM>([&](auto I) {
                 const int R = rb0[I] + ct;
-                fa[I] = *reinterpret_cast<const half8 *>(ta + kc_off(R, s * 4 + (lane >> 4)));
+                fa[I] = *reinterpret_cast<const half8 *>(ta + halo_off(R, s * 4 + (lane >> 4)));
             });
             static_for<TN>([&](auto J) { fb[J] = load_frag<BKC, BN>(tb, wn * WTN + J * 16, s, lane); });
             static_for<TM>([&](auto I) {
@@ -852,7 +862,9 @@ hipEvent_t prof_event() {
     return e;
 }
 }  // namespace
-enum { KF_PROF_FUSED = 0, KF_PROF_WGRAD = 1, KF_PROF_NCLS = 2 };
+// classes (kf_ops.h): 0 fused GEMM, 1 wgrad GEMM, 2 chain numerator, 3 chain den, 4 conv
+// halo forward / input gradient, 5 conv halo weight gradient, 6 split-K slab reduce
+enum { KF_PROF_FUSED = 0, KF_PROF_WGRAD = 1, KF_PROF_HALO = 4, KF_PROF_REDUCE = 6 };
 
 // generic bracket for other kernel classes (kf_common.h): returns a record
 // index, or -1 when profiling is off
@@ -1101,7 +1113,7 @@ static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const Ha
     if (g_prof) {
         rec.a = prof_event();
         rec.b = prof_event();
-        rec.cls = KF_PROF_FUSED;
+        rec.cls = KF_PROF_HALO;
         rec.flops = 2.0 * M * N * (double)H.ntaps * H.pw;
         rec.bytes = (double)H.T * H.hsrc * H.pw * 2.0 + (double)H.ntaps * H.pw * N * 2.0 + epi_bytes(E, M, N);
         hipExtLaunchKernelGGL(conv_halo_kernel<BM, BN, WM, WN, BKC, BMODE, BROW, ST>, dim3(mt * nt),
@@ -1159,17 +1171,10 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     H.pad = std::max(0, -dhmin);
     const int maxshp = (a.hout - 1) * a.hmul + dhmax + H.pad;
     const int HP = std::max(a.hsrc + H.pad, maxshp + 1);
-    H.hpe = (HP + a.hmul - 1) / a.hmul;
-    H.hpos = H.hpe * a.hmul;
+    const int hpe0 = (HP + a.hmul - 1) / a.hmul;
     H.dtmin = dtmin;
     H.ntaps = a.nparts;
     H.nch = a.pw / BK;
-    H.nbuf = H.nch > 1 ? 2 : 1;
-    for (int p = 0; p < a.nparts; ++p) {
-        const int x = a.dh[p] + H.pad;
-        H.ctap[p] = (a.dt[p] - dtmin) * H.hpos + (x % a.hmul) * H.hpe + x / a.hmul;
-        H.bshift[p] = brow ? b.dt[p] : 0;
-    }
     // 32-bit source offsets: the largest byte offset the halo can form
     if (((long long)a.T * a.ld + (long long)a.hsrc * a.pw) * 2 >= (1LL << 32) - 64) return 0;
     const int BN_ = N <= 64 ? 64 : N <= 128 ? 128 : 256;
@@ -1179,20 +1184,45 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     const bool residue = brow && a.nparts < 9;
     const int BM_ = residue ? 128 : 256;
     H.nf = (BM_ - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
+    const int nw = BN_ == 64 ? 4 : 8;
+    const size_t epi = 16 * BN_ + 32 * (64 + 4) * 4 * nw;
+    // LDS of a halo geometry: two images when there are several channel chunks, else one
+    // (two too large, e.g. cnn5's stride-2 forward: 80 KB each beside a 64 KB B ring: one
+    // image, reloaded between channel chunks)
+    auto geometry = [&](int hpe, int &nbuf, int &halo_bytes) {
+        halo_bytes = (H.nf * hpe * a.hmul + 7) / 8 * 1024;
+        nbuf = H.nch > 1 ? 2 : 1;
+        size_t l = std::max((size_t)nbuf * halo_bytes + 2 * BN_ * BK * 2, epi);
+        if (l > 160 * 1024 && nbuf == 2) {
+            nbuf = 1;
+            l = std::max((size_t)halo_bytes + 2 * BN_ * BK * 2, epi);
+        }
+        return l;
+    };
+    int nb0, hb0;
+    const size_t lds0 = geometry(hpe0, nb0, hb0);
+    // hpos = hout (mod 8): conflict-free fragment reads across frame boundaries (halo_off),
+    // taken when it keeps the image count and the workgroups per CU (80 KB: two)
+    int hpe = hpe0;
+    while ((hpe * a.hmul - a.hout) % 8) ++hpe;
+    int nb1, hb1;
+    const size_t lds1 = geometry(hpe, nb1, hb1);
+    const bool pad8 = lds1 <= 160 * 1024 && nb1 == nb0 && (lds0 > 80 * 1024 || lds1 <= 80 * 1024);
+    if (!pad8) hpe = hpe0;
+    H.hpe = hpe;
+    H.hpos = hpe * a.hmul;
+    H.nbuf = pad8 ? nb1 : nb0;
+    H.halo_bytes = pad8 ? hb1 : hb0;
+    const size_t lds = pad8 ? lds1 : lds0;
+    if (lds > 160 * 1024) return 0;
     H.rows = H.nf * H.hpos;
     H.npieces = (H.rows + 7) / 8;
     H.slice = (H.npieces + H.ntaps - 1) / H.ntaps;
-    H.halo_bytes = H.npieces * 1024;
-    const int nw = BN_ == 64 ? 4 : 8;
-    const size_t epi = 16 * BN_ + 32 * (64 + 4) * 4 * nw;
-    size_t lds = std::max((size_t)H.nbuf * H.halo_bytes + 2 * BN_ * BK * 2, epi);
-    // two halo images too large (cnn5's stride-2 forward: 80 KB each beside a 64 KB
-    // B ring): one image, reloaded between channel chunks
-    if (lds > 160 * 1024 && H.nbuf == 2) {
-        H.nbuf = 1;
-        lds = std::max((size_t)H.halo_bytes + 2 * BN_ * BK * 2, epi);
+    for (int p = 0; p < a.nparts; ++p) {
+        const int x = a.dh[p] + H.pad;
+        H.ctap[p] = (a.dt[p] - dtmin) * H.hpos + (x % a.hmul) * H.hpe + x / a.hmul;
+        H.bshift[p] = brow ? b.dt[p] : 0;
     }
-    if (lds > 160 * 1024) return 0;
     // (measured and dropped: a 4-stage weight ring at one workgroup per CU, cnn2 517 ->
     // 884 us; 64-column tiles on two 128x64-tile waves, cnn2 529 -> 781 us)
 #define KF_HALO(BKC_, BMODE_, BROW_)                                                                     \
@@ -1304,13 +1334,28 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
 void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int M, int N, float *dW,
                      long long ldw, float *bias_grad, int accumulate) {
     const int nb = kf_blocks((long long)M * N / 4 + 1, 256, 4096);
-    if (bias_grad) {
-        const int ncb = (N + 63) / 64;
+    const int ncb = bias_grad ? (N + 63) / 64 : 0;
+    ProfRec rec{};
+    hipEvent_t ea = nullptr, eb = nullptr;
+    if (g_prof) {  // timestamps in the dispatch packet, as for the GEMMs
+        ea = rec.a = prof_event();
+        eb = rec.b = prof_event();
+        rec.cls = KF_PROF_REDUCE;
+        // the slabs read once, dW (and the bias) written once (+ read when accumulating)
+        rec.bytes = ((double)splits * (M + (bias_grad ? 1 : 0)) + (accumulate ? 2.0 : 1.0) * (M + 1)) * N * 4.0;
+        g_prof_recs.push_back(rec);
+    }
+    if (bias_grad && g_prof)
+        hipExtLaunchKernelGGL(k_slab_reduce_both, dim3(ncb + nb), dim3(256), 0, kf_stream(), ea, eb, 0, slab, splits,
+                              M, N, dW, ldw, accumulate, bias_slab, bias_grad, ncb);
+    else if (bias_grad)
         k_slab_reduce_both<<<ncb + nb, 256, 0, kf_stream()>>>(slab, splits, M, N, dW, ldw, accumulate, bias_slab,
                                                              bias_grad, ncb);
-    } else {
+    else if (g_prof)
+        hipExtLaunchKernelGGL(k_slab_reduce, dim3(nb), dim3(256), 0, kf_stream(), ea, eb, 0, slab, splits, M, N, dW,
+                              ldw, accumulate);
+    else
         k_slab_reduce<<<nb, 256, 0, kf_stream()>>>(slab, splits, M, N, dW, ldw, accumulate);
-    }
 }
 
 int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
@@ -1469,6 +1514,48 @@ __global__ void k_gemm_small(int M, int N, int K, float alpha, const h16 *A, int
     }
 }
 
+// short-K products on 8-column vectors (K <= 8: AddBias is ops_gemm with K = 1 against a
+// ones column, internal/gpu/ops.go:335-351): a thread owns one 8-column vector of C for
+// all its rows and keeps B's K x 8 block in registers; A's K values of a row are the same
+// for every thread of that row (one cached line). Same arithmetic and order as
+// k_gemm_small: s = sum_k a*b in fp32, v = alpha * s (+ beta * C), one RNE store.
+constexpr int kSmallK = 8;
+__global__ __launch_bounds__(256) void k_gemm_smallk_v8(int M, int ncv, int K, long long R, float alpha,
+                                                        const h16 *A, int lda, const h16 *B, int ldb,
+                                                        float beta, h16 *C, int ldc) {
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (long long)ncv * R) return;
+    const int cv = (int)(g % ncv);
+    float b[kSmallK][8];
+#pragma unroll
+    for (int k = 0; k < kSmallK; ++k) {
+        if (k < K) {
+            const half8 v = *reinterpret_cast<const half8 *>(B + (long long)k * ldb + 8 * cv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) b[k][e] = (float)v[e];
+        }
+    }
+    for (long long m = g / ncv; m < M; m += R) {
+        float a[kSmallK];
+#pragma unroll
+        for (int k = 0; k < kSmallK; ++k) a[k] = k < K ? h2f(A[m * lda + k]) : 0.f;
+        h16 *c = C + m * ldc + 8 * cv;
+        half8 out;
+        const half8 c0 = beta != 0.f ? *reinterpret_cast<const half8 *>(c) : half8{};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float s = 0.f;
+#pragma unroll
+            for (int k = 0; k < kSmallK; ++k)
+                if (k < K) s += a[k] * b[k][e];
+            float v = alpha * s;
+            if (beta != 0.f) v += beta * (float)c0[e];
+            out[e] = f2h(v);
+        }
+        *reinterpret_cast<half8 *>(c) = out;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // MXFP8 quantisation (kf_ops.h): one thread per (row, 32-element block)
 // ---------------------------------------------------------------------------
@@ -1534,7 +1621,16 @@ int kf_ops_gemm_impl(int M, int N, int K, float alpha, const void *A, int lda, c
     if (ldc <= 0) ldc = N;
     const bool fast = (K % 8 == 0) && (N % 8 == 0) && (lda % 8 == 0) && (ldb % 8 == 0) &&
                       (ldc % 8 == 0) && !(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) & 15);
-    if (!fast || K == 0) {
+    const bool smallk_vec = K <= kSmallK && N % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+                            !(((uintptr_t)B | (uintptr_t)C) & 15);
+    if (smallk_vec) {
+        const int ncv = N / 8;
+        long long R = 262144 / ncv;
+        if (R < 1) R = 1;
+        if (R > M) R = M;
+        k_gemm_smallk_v8<<<(unsigned)((ncv * R + 255) / 256), 256, 0, kf_stream()>>>(
+            M, ncv, K, R, alpha, (const h16 *)A, lda, (const h16 *)B, ldb, beta, (h16 *)C, ldc);
+    } else if (!fast || K == 0) {
         k_gemm_small<<<kf_blocks((long long)M * N, 256, 8192), 256, 0, kf_stream()>>>(
             M, N, K, alpha, (const h16 *)A, lda, (const h16 *)B, ldb, beta, (h16 *)C, ldc);
     } else {

@@ -132,9 +132,40 @@ __device__ __forceinline__ half8 load_frag(const char *tile, int idx0, int s, in
 enum { OP_SIMPLE = 0, OP_P2 = 1, OP_GEN = 2 };
 constexpr unsigned BAD = 0xFFFFFFFFu;  // byte offset that reads as zero (buffer range check)
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)0xFFFFFFFF,
-                                             0x00020000);
+// buffer resource (SGPR quad): base, stride 0, 2^32 - 1 records (an offset of BAD reads
+// as zero through the range check), the raw-buffer flags word
+typedef unsigned Rsrc __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ Rsrc make_rsrc(const void *base) {
+    const unsigned long long b = (unsigned long long)base;
+    return Rsrc{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)b),
+                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) & 0xFFFFu, 0xFFFFFFFFu, 0x00020000u};
+}
+
+// LDS-DMA: lane l's BYTES (16 or 4) at buffer offset voff land at lds_dst + BYTES * l
+// (lds_dst wave-uniform). Issued from inline asm so that hipcc does not track it: as a
+// tracked LDS write (__builtin_amdgcn_raw_ptr_buffer_load_lds) it made hipcc emit
+// s_waitcnt vmcnt(0) before every ds_read_b64_tr_b16 after it — the next stage's loads
+// drained before the current stage's fragment reads, in every kernel with a
+// reduction-major operand (the wgrads, the halo forward, N-major B). Every wait on these
+// loads is explicit: wait_vmcnt<N>() / wait_vmcnt_rt() before the barrier that precedes
+// the reads of a stage (cdna_hip_programming.md, "What hipcc does not do", LDS-DMA recipe).
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(Rsrc rs, const void *lds_dst, unsigned voff) {
+    const unsigned m0v = (unsigned)__builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void *)lds_dst);
+    unsigned keep;
+    if constexpr (BYTES == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(rs), "s"(m0v)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(rs), "s"(m0v)
+                     : "memory");
 }
 
 // byte offset of (row t,h ; part p ; in-part column kk) or BAD
@@ -208,7 +239,7 @@ struct Stager {
     }
 
     // issue the NC LDS-DMA loads of the tile at reduction offset k0 into `dst`
-    __device__ __forceinline__ void issue(const OpD &d, __amdgpu_buffer_rsrc_t rs, int k0, int kend,
+    __device__ __forceinline__ void issue(const OpD &d, Rsrc rs, int k0, int kend,
                                           char *dst, int wave, int lane) {
         const int klim = min(kend, KC ? d.ncols : d.nrows);
         if constexpr (KC && MODE == OP_GEN) {
@@ -283,9 +314,7 @@ struct Stager {
                     }
                 }
             }
-            if (EVEN || q < NP)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rs, (__attribute__((address_space(3))) void *)(dst + q * 1024), 16, voff, 0, 0, 0);
+            if (EVEN || q < NP) lds_dma<16>(rs, dst + q * 1024, voff);
         });
     }
 };

@@ -42,7 +42,8 @@ hipStream_t kf_stream();
 void kf_report_error(const char *fmt, ...);
 
 // kf_prof_* timing of a launch bracket on the current stream (gemm.hip);
-// classes: 0 fused GEMM, 1 wgrad GEMM, 2 chain numerator, 3 chain denominator
+// classes: 0 fused GEMM, 1 wgrad GEMM, 2 chain numerator, 3 chain denominator,
+// 4 conv halo fwd / dX, 5 conv halo wgrad, 6 slab reduce (include/kf_ops.h)
 enum { KF_PROF_CHAIN_NUM = 2, KF_PROF_CHAIN_DEN = 3 };
 int kf_prof_start(int cls, double work);
 void kf_prof_stop(int idx);

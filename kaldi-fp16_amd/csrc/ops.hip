@@ -114,7 +114,32 @@ __global__ void k_softmax(h16 *data, int cols, int logmode) {
     }
 }
 
+// ------------------------------- row-vector layout ------------------------
+// [rows x cols] element-wise ops on 8-column (16-byte) vectors: a thread owns ONE column
+// vector cv for all its rows (its per-column parameters are loaded once, no per-element
+// index division) and walks rows r0, r0 + R, ... Consecutive threads take consecutive
+// column vectors of a row, then the next row, so a wave reads contiguous row bytes.
+struct RowVec {
+    int ncv;      // column vectors per row
+    long long R;  // row stride of the walk (threads = ncv * R)
+};
+static inline RowVec rowvec_plan(long long rows, int ncv, int &blocks) {
+    long long R = 262144 / ncv;  // ~256K threads in flight
+    if (R < 1) R = 1;
+    if (R > rows) R = rows;
+    blocks = (int)((ncv * R + 255) / 256);
+    return RowVec{ncv, R};
+}
+#define ROWVEC_THREAD(P, cv, r0)                                          \
+    const long long g_ = (long long)blockIdx.x * blockDim.x + threadIdx.x; \
+    if (g_ >= (long long)(P).ncv * (P).R) return;                         \
+    const int cv = (int)(g_ % (P).ncv);                                   \
+    const long long r0 = g_ / (P).ncv
+
 // ------------------------------- batchnorm ---------------------------------
+// norm = (x - mean) / sqrtf(var + eps); gamma * norm + beta (or norm * target_rms), the
+// reference's expression per element (ops.cu:171-204). The vector form evaluates the
+// same expression with the per-column sqrtf taken once per thread.
 __global__ void k_bn(h16 *x, long long total, int D, const float *mean, const float *var,
                      const float *gamma, const float *beta, float target_rms, float eps,
                      int rms) {
@@ -124,6 +149,46 @@ __global__ void k_bn(h16 *x, long long total, int D, const float *mean, const fl
         x[i] = f2h(rms ? norm * target_rms : gamma[d] * norm + beta[d]);
     }
 }
+__global__ __launch_bounds__(256) void k_bn_v8(h16 *x, long long rows, RowVec P, const float *mean,
+                                               const float *var, const float *gamma, const float *beta,
+                                               float target_rms, float eps, int rms) {
+    ROWVEC_THREAD(P, cv, r0);
+    float mu[8], sd[8], g[8], b[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int c = 8 * cv + e;
+        mu[e] = mean[c];
+        sd[e] = sqrtf(var[c] + eps);
+        g[e] = rms ? target_rms : gamma[c];
+        b[e] = rms ? 0.f : beta[c];
+    }
+    const long long ld = 8LL * P.ncv;
+    h16 *p = x + 8LL * cv;
+    long long r = r0;
+    for (; r + 3 * P.R < rows; r += 4 * P.R) {  // four rows in flight per thread
+        half8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = load_h8(p + (r + u * P.R) * ld);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float norm = ((float)v[u][e] - mu[e]) / sd[e];
+                v[u][e] = f2h(rms ? norm * g[e] : g[e] * norm + b[e]);
+            }
+            store_h8(p + (r + u * P.R) * ld, v[u]);
+        }
+    }
+    for (; r < rows; r += P.R) {
+        half8 v = load_h8(p + r * ld);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float norm = ((float)v[e] - mu[e]) / sd[e];
+            v[e] = f2h(rms ? norm * g[e] : g[e] * norm + b[e]);
+        }
+        store_h8(p + r * ld, v);
+    }
+}
 
 __global__ void k_bn_bwd(const h16 *go, h16 *gi, const float *gamma, const float *var,
                          float eps, long long total, int cols) {
@@ -131,6 +196,50 @@ __global__ void k_bn_bwd(const h16 *go, h16 *gi, const float *gamma, const float
         const int d = (int)(i % cols);
         gi[i] = f2h(h2f(go[i]) * (gamma[d] / sqrtf(var[d] + eps)));
     }
+}
+__global__ __launch_bounds__(256) void k_bn_bwd_v8(const h16 *go, h16 *gi, const float *gamma,
+                                                   const float *var, float eps, long long rows, RowVec P) {
+    ROWVEC_THREAD(P, cv, r0);
+    float sc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sc[e] = gamma[8 * cv + e] / sqrtf(var[8 * cv + e] + eps);
+    const long long ld = 8LL * P.ncv, c0 = 8LL * cv;
+    long long r = r0;
+    for (; r + 3 * P.R < rows; r += 4 * P.R) {
+        half8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = load_h8(go + (r + u * P.R) * ld + c0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[u][e] = f2h((float)v[u][e] * sc[e]);
+            store_h8(gi + (r + u * P.R) * ld + c0, v[u]);
+        }
+    }
+    for (; r < rows; r += P.R) {
+        half8 v = load_h8(go + r * ld + c0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = f2h((float)v[e] * sc[e]);
+        store_h8(gi + r * ld + c0, v);
+    }
+}
+
+// column placement (concat) / extraction (slice) of 8-column vectors: dst row r, column
+// dcol0 + 8 cv  <-  src row r, column scol0 + 8 cv
+__global__ __launch_bounds__(256) void k_cols_copy_v8(h16 *dst, long long ldd, int dcol0, const h16 *src,
+                                                      long long lds, int scol0, long long rows, RowVec P) {
+    ROWVEC_THREAD(P, cv, r0);
+    h16 *d = dst + dcol0 + 8LL * cv;
+    const h16 *s = src + scol0 + 8LL * cv;
+    long long r = r0;
+    for (; r + 3 * P.R < rows; r += 4 * P.R) {
+        half8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = load_h8(s + (r + u * P.R) * lds);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) store_h8(d + (r + u * P.R) * ldd, v[u]);
+    }
+    for (; r < rows; r += P.R) store_h8(d + r * ldd, load_h8(s + r * lds));
 }
 
 // ------------------------------- element-wise ------------------------------
@@ -151,9 +260,17 @@ __global__ void k_add_scaled(h16 *dst, const h16 *src, long long n, float a, flo
     }
 }
 
-__global__ void k_fill(h16 *dst, long long n, float v) {
+__global__ void k_fill(h16 *dst, long long n, float v, int vec) {
     const h16 hv = f2h(v);
-    GRID_STRIDE(i, n) dst[i] = hv;
+    if (vec) {
+        half8 w;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w[e] = hv;
+        GRID_STRIDE(i, n / 8) store_h8(dst + 8 * i, w);
+        GRID_STRIDE(i, n % 8) dst[n / 8 * 8 + i] = hv;
+    } else {
+        GRID_STRIDE(i, n) dst[i] = hv;
+    }
 }
 
 __global__ void k_concat_cols(h16 *dst, int T, int dst_cols, const h16 *src, int src_cols,
@@ -192,20 +309,33 @@ __global__ void k_subsample_rows(h16 *dst, const h16 *src, int out_rows, int col
     }
 }
 
-__global__ void k_act_bwd(const h16 *x, h16 *g, long long n, int kind) {
+__device__ __forceinline__ float act_bwd_elem(int kind, float xv, float gv) {
     // no fma contraction: LLVM would fold fpext(fp16 product) into an fp32 fma and
     // drop the intermediate fp16 rounding the reference's __hmul chain performs
 #pragma clang fp contract(off)
-    GRID_STRIDE(i, n) {
-        const float xv = h2f(x[i]), gv = h2f(g[i]);
-        // fp16 arithmetic as the reference's __hmul / __hsub chain
-        // (backward_wrappers.cu:41-74): every product / difference rounds to fp16
-        // (a product of two fp16 values is exact in fp32, so one RNE matches __hmul)
-        float r;
-        if (kind == ACT_RELU) r = xv > 0.f ? gv : 0.f;
-        else if (kind == ACT_SIGMOID) r = h2f(f2h(gv * xv)) * h2f(f2h(1.f - xv));
-        else r = gv * h2f(f2h(1.f - h2f(f2h(xv * xv))));
-        g[i] = f2h(r);
+    // fp16 arithmetic as the reference's __hmul / __hsub chain
+    // (backward_wrappers.cu:41-74): every product / difference rounds to fp16
+    // (a product of two fp16 values is exact in fp32, so one RNE matches __hmul)
+    if (kind == ACT_RELU) return xv > 0.f ? gv : 0.f;
+    if (kind == ACT_SIGMOID) return h2f(f2h(gv * xv)) * h2f(f2h(1.f - xv));
+    return gv * h2f(f2h(1.f - h2f(f2h(xv * xv))));
+}
+__global__ void k_act_bwd(const h16 *x, h16 *g, long long n, int kind, int vec) {
+#pragma clang fp contract(off)
+    if (vec) {
+        GRID_STRIDE(i, n / 8) {
+            const half8 xv = load_h8(x + 8 * i);
+            half8 gv = load_h8(g + 8 * i);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) gv[e] = f2h(act_bwd_elem(kind, (float)xv[e], (float)gv[e]));
+            store_h8(g + 8 * i, gv);
+        }
+        GRID_STRIDE(i, n % 8) {
+            const long long j = n / 8 * 8 + i;
+            g[j] = f2h(act_bwd_elem(kind, h2f(x[j]), h2f(g[j])));
+        }
+    } else {
+        GRID_STRIDE(i, n) g[i] = f2h(act_bwd_elem(kind, h2f(x[i]), h2f(g[i])));
     }
 }
 
@@ -224,7 +354,21 @@ __global__ void k_transpose(const h16 *src, h16 *dst, int M, int N) {
     }
 }
 
-__global__ void k_h2f(const h16 *s, float *d, long long n) { GRID_STRIDE(i, n) d[i] = h2f(s[i]); }
+__global__ void k_h2f(const h16 *s, float *d, long long n, int vec) {
+    if (vec) {
+        GRID_STRIDE(i, n / 8) {
+            const half8 v = load_h8(s + 8 * i);
+            float4v a, b;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[e] = (float)v[e], b[e] = (float)v[4 + e];
+            *reinterpret_cast<float4v *>(d + 8 * i) = a;
+            *reinterpret_cast<float4v *>(d + 8 * i + 4) = b;
+        }
+        GRID_STRIDE(i, n % 8) d[n / 8 * 8 + i] = h2f(s[n / 8 * 8 + i]);
+    } else {
+        GRID_STRIDE(i, n) d[i] = h2f(s[i]);
+    }
+}
 
 // kf_dp_debug KF_DP_DEBUG_PEER_MEAN (csrc/dp.cpp): a two-rank average whose other rank's
 // bucket is `peer`, on the communication stream
@@ -239,15 +383,40 @@ int kf_dp_debug_mean_launch(float *buf, const float *peer, size_t n, hipStream_t
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+__device__ __forceinline__ void sgd_elem(float *w32, h16 *w16, const h16 *g, float *v, float lr, float mom,
+                                         long long i) {
+    const float vv = mom * v[i] + h2f(g[i]);
+    v[i] = vv;
+    const float w = w32[i] - lr * vv;
+    w32[i] = w;
+    w16[i] = f2h(w);
+}
+// vec: every pointer 16-byte aligned; 8 parameters per thread (two float4 of w32 / v)
 __global__ void k_sgd(float *w32, h16 *w16, const h16 *g, float *v, float lr, float mom,
-                      long long n) {
-    GRID_STRIDE(i, n) {
-        const float vv = mom * v[i] + h2f(g[i]);
-        v[i] = vv;
-        const float w = w32[i] - lr * vv;
-        w32[i] = w;
-        w16[i] = f2h(w);
+                      long long n, int vec) {
+    if (!vec) {
+        GRID_STRIDE(i, n) sgd_elem(w32, w16, g, v, lr, mom, i);
+        return;
     }
+    GRID_STRIDE(i, n / 8) {
+        const half8 gv = load_h8(g + 8 * i);
+        half8 wh;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            float4v vv = *reinterpret_cast<const float4v *>(v + 8 * i + 4 * q);
+            float4v ww = *reinterpret_cast<const float4v *>(w32 + 8 * i + 4 * q);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                vv[e] = mom * vv[e] + (float)gv[4 * q + e];
+                ww[e] = ww[e] - lr * vv[e];
+                wh[4 * q + e] = f2h(ww[e]);
+            }
+            *reinterpret_cast<float4v *>(v + 8 * i + 4 * q) = vv;
+            *reinterpret_cast<float4v *>(w32 + 8 * i + 4 * q) = ww;
+        }
+        store_h8(w16 + 8 * i, wh);
+    }
+    GRID_STRIDE(i, n % 8) sgd_elem(w32, w16, g, v, lr, mom, n / 8 * 8 + i);
 }
 
 // ---------------------------------------------------------------------------
@@ -349,21 +518,31 @@ int ops_log_softmax(void *data, int rows, int cols) {
     return ops_check("log_softmax kernel");
 }
 
+static int run_bn(void *x, int T, int D, const float *mean, const float *var, const float *gamma,
+                  const float *beta, float target_rms, float eps, int rms, const char *name) {
+    const long long total = (long long)T * D;
+    if (D % 8 == 0 && aligned16(x)) {
+        int blocks;
+        const RowVec P = rowvec_plan(T, D / 8, blocks);
+        k_bn_v8<<<blocks, 256, 0, kf_stream()>>>((h16 *)x, T, P, mean, var, gamma, beta, target_rms, eps, rms);
+    } else {
+        k_bn<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>((h16 *)x, total, D, mean, var, gamma, beta,
+                                                                  target_rms, eps, rms);
+    }
+    return ops_check(name);
+}
+
 int ops_batchnorm_forward(void *x, int T, int D, const float *mean, const float *var,
                           const float *gamma, const float *beta, float epsilon) {
     long long total = (long long)T * D;
     if (total <= 0) return 0;
-    k_bn<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>((h16 *)x, total, D, mean, var,
-                                                              gamma, beta, 1.f, epsilon, 0);
-    return ops_check("batchnorm kernel");
+    return run_bn(x, T, D, mean, var, gamma, beta, 1.f, epsilon, 0, "batchnorm kernel");
 }
 int ops_batchnorm_forward_rms(void *x, int T, int D, const float *mean, const float *var,
                               float target_rms, float epsilon) {
     long long total = (long long)T * D;
     if (total <= 0) return 0;
-    k_bn<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
-        (h16 *)x, total, D, mean, var, nullptr, nullptr, target_rms, epsilon, 1);
-    return ops_check("batchnorm rms kernel");
+    return run_bn(x, T, D, mean, var, nullptr, nullptr, target_rms, epsilon, 1, "batchnorm rms kernel");
 }
 
 int ops_add_scaled(void *dst, const void *src, int count, float alpha, float beta) {
@@ -386,7 +565,7 @@ int ops_copy(void *dst, const void *src, int count) {
 }
 int ops_fill(void *dst, int count, float val) {
     if (count <= 0) return 0;
-    k_fill<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((h16 *)dst, count, val);
+    k_fill<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>((h16 *)dst, count, val, aligned16(dst));
     return ops_check("fill");
 }
 
@@ -397,8 +576,15 @@ int ops_concat_cols(void *dst, int T, int dst_cols, const void *src, int src_col
         ops_set_error("concat_cols: offset %d + %d > %d", dst_col_offset, src_cols, dst_cols);
         return -1;
     }
-    k_concat_cols<<<kf_blocks((long long)T * src_cols, 256, 8192), 256, 0, kf_stream()>>>(
-        (h16 *)dst, T, dst_cols, (const h16 *)src, src_cols, dst_col_offset);
+    if (src_cols % 8 == 0 && dst_cols % 8 == 0 && dst_col_offset % 8 == 0 && aligned16(dst) && aligned16(src)) {
+        int blocks;
+        const RowVec P = rowvec_plan(T, src_cols / 8, blocks);
+        k_cols_copy_v8<<<blocks, 256, 0, kf_stream()>>>((h16 *)dst, dst_cols, dst_col_offset, (const h16 *)src,
+                                                        src_cols, 0, T, P);
+    } else {
+        k_concat_cols<<<kf_blocks((long long)T * src_cols, 256, 8192), 256, 0, kf_stream()>>>(
+            (h16 *)dst, T, dst_cols, (const h16 *)src, src_cols, dst_col_offset);
+    }
     return ops_check("concat_cols");
 }
 int ops_slice_cols(const void *src, int T, int src_cols, void *dst, int dst_cols,
@@ -408,8 +594,15 @@ int ops_slice_cols(const void *src, int T, int src_cols, void *dst, int dst_cols
         ops_set_error("slice_cols: offset %d + %d > %d", src_col_offset, dst_cols, src_cols);
         return -1;
     }
-    k_slice_cols<<<kf_blocks((long long)T * dst_cols, 256, 8192), 256, 0, kf_stream()>>>(
-        (h16 *)dst, T, dst_cols, (const h16 *)src, src_cols, src_col_offset);
+    if (src_cols % 8 == 0 && dst_cols % 8 == 0 && src_col_offset % 8 == 0 && aligned16(dst) && aligned16(src)) {
+        int blocks;
+        const RowVec P = rowvec_plan(T, dst_cols / 8, blocks);
+        k_cols_copy_v8<<<blocks, 256, 0, kf_stream()>>>((h16 *)dst, dst_cols, 0, (const h16 *)src, src_cols,
+                                                        src_col_offset, T, P);
+    } else {
+        k_slice_cols<<<kf_blocks((long long)T * dst_cols, 256, 8192), 256, 0, kf_stream()>>>(
+            (h16 *)dst, T, dst_cols, (const h16 *)src, src_cols, src_col_offset);
+    }
     return ops_check("slice_cols");
 }
 
@@ -443,20 +636,20 @@ void ops_subsample_rows(void *dst, const void *src, int in_rows, int cols, int s
 
 int ops_relu_backward(const void *x, void *grad, int count) {
     if (count <= 0) return 0;
-    k_act_bwd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)x, (h16 *)grad,
-                                                                    count, ACT_RELU);
+    k_act_bwd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
+        (const h16 *)x, (h16 *)grad, count, ACT_RELU, aligned16(x) && aligned16(grad));
     return ops_check("relu_backward");
 }
 int ops_sigmoid_backward(const void *out, void *grad, int count) {
     if (count <= 0) return 0;
-    k_act_bwd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>(
-        (const h16 *)out, (h16 *)grad, count, ACT_SIGMOID);
+    k_act_bwd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
+        (const h16 *)out, (h16 *)grad, count, ACT_SIGMOID, aligned16(out) && aligned16(grad));
     return ops_check("sigmoid_backward");
 }
 int ops_tanh_backward(const void *out, void *grad, int count) {
     if (count <= 0) return 0;
-    k_act_bwd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)out,
-                                                                    (h16 *)grad, count, ACT_TANH);
+    k_act_bwd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
+        (const h16 *)out, (h16 *)grad, count, ACT_TANH, aligned16(out) && aligned16(grad));
     return ops_check("tanh_backward");
 }
 // several transposes in one launch (the network's transposed weight copies after an
@@ -523,20 +716,29 @@ int ops_batchnorm_backward(const void *grad_out, void *grad_in, const float *gam
                            const float *variance, float eps, int rows, int cols) {
     const long long total = (long long)rows * cols;
     if (total <= 0) return 0;
-    k_bn_bwd<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
-        (const h16 *)grad_out, (h16 *)grad_in, gamma, variance, eps, total, cols);
+    if (cols % 8 == 0 && aligned16(grad_out) && aligned16(grad_in)) {
+        int blocks;
+        const RowVec P = rowvec_plan(rows, cols / 8, blocks);
+        k_bn_bwd_v8<<<blocks, 256, 0, kf_stream()>>>((const h16 *)grad_out, (h16 *)grad_in, gamma, variance, eps,
+                                                     rows, P);
+    } else {
+        k_bn_bwd<<<kf_blocks(total, 256, 8192), 256, 0, kf_stream()>>>(
+            (const h16 *)grad_out, (h16 *)grad_in, gamma, variance, eps, total, cols);
+    }
     return ops_check("batchnorm_backward");
 }
 int ops_fp16_to_fp32(const void *src, float *dst, int count) {
     if (count <= 0) return 0;
-    k_h2f<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)src, dst, count);
+    k_h2f<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)src, dst, count,
+                                                                       aligned16(src) && aligned16(dst));
     return ops_check("fp16_to_fp32");
 }
 int ops_sgd_update(float *w_fp32, void *w_fp16, const void *grad_fp16, float *velocity,
                    float lr, float momentum, int count) {
     if (count <= 0) return 0;
-    k_sgd<<<kf_blocks(count, 256, 8192), 256, 0, kf_stream()>>>(
-        w_fp32, (h16 *)w_fp16, (const h16 *)grad_fp16, velocity, lr, momentum, count);
+    const int vec = aligned16(w_fp32) && aligned16(w_fp16) && aligned16(grad_fp16) && aligned16(velocity);
+    k_sgd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
+        w_fp32, (h16 *)w_fp16, (const h16 *)grad_fp16, velocity, lr, momentum, count, vec);
     return ops_check("sgd_update");
 }
 

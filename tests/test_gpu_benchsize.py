@@ -244,3 +244,143 @@ def test_kstep_interleave_matches_part_order(gpu):
         _within(o, ref, tol, "kil")
     # the two orders differ at most by two fp16 roundings of the same value
     assert np.all(np.abs(outs[0] - outs[1]) <= 2 * tol)
+
+
+# ---------------------------------------------------------------------------------------
+# 3x3 convolutions at the bench's size (conv_halo_kernel forward / input gradient,
+# conv_wgrad_halo_kernel with the split count chosen for T = 96,000), operands built as
+# host/network.cpp builds them (op_im2col / op_col2im / op_wrows, :1160-1192, :1608-1658),
+# with the network's epilogues: forward bias + ReLU + mask + BN scale / shift, input
+# gradient into the layer below's dz (BN scale x ReLU mask). Reference semantics:
+# internal/nnet/forward.go:418-524 (host im2col + GEMM), network_backward.go:468-537.
+OFFS = [(a, b) for a in (-1, 0, 1) for b in (-1, 0, 1)]
+# (name, hin, fin, hout, sub, fout): cnn2 (one 64-channel chunk, 512-split wgrad), cnn3
+# (height stride 2, per-residue input gradient), cnn5 (two chunks, stride 2)
+CONV = [("cnn2", 40, 64, 40, 1, 64), ("cnn3", 40, 64, 20, 2, 128), ("cnn5", 20, 128, 10, 2, 256)]
+
+
+def _im2col_rows(x3, t, h, sub):
+    """[n x 9 fin] im2col rows (t, h) of x3 [T, hin, fin] (zero outside), fp64"""
+    Tn, hin, _ = x3.shape
+    parts = []
+    for dt, dh in OFFS:
+        ts, hs = t + dt, h * sub + dh
+        ok = (ts >= 0) & (ts < Tn) & (hs >= 0) & (hs < hin)
+        parts.append(np.where(ok[:, None], x3[np.clip(ts, 0, Tn - 1), np.clip(hs, 0, hin - 1)].astype(np.float64), 0))
+    return np.concatenate(parts, 1)
+
+
+def _col2im_rows(dz3, W, t, h, sub, fin):
+    """input-gradient rows (t, h): sum over taps of dz[t - dt, h'] . W_tap^T, h = h' sub + dh;
+    also the bound sum |dz||W|"""
+    Tn, hout, _ = dz3.shape
+    acc = np.zeros((t.size, fin))
+    mag = np.zeros((t.size, fin))
+    for o, (dt, dh) in enumerate(OFFS):
+        ts, r = t - dt, h - dh
+        hp = r // sub
+        ok = (ts >= 0) & (ts < Tn) & (r % sub == 0) & (hp >= 0) & (hp < hout)
+        d = np.where(ok[:, None], dz3[np.clip(ts, 0, Tn - 1), np.clip(hp, 0, hout - 1)].astype(np.float64), 0)
+        Wo = W[o * fin:(o + 1) * fin].astype(np.float64)
+        acc += d @ Wo.T
+        mag += np.abs(d) @ np.abs(Wo).T
+    return acc, mag
+
+
+@pytest.mark.parametrize("name,hin,fin,hout,sub,fout", CONV)
+def test_conv_at_bench_size(gpu, name, hin, fin, hout, sub, fout):
+    kf = gpu
+    rng = np.random.default_rng(hin * fout)
+    K, M = 9 * fin, T * hout
+    x = _h(np.maximum(rng.standard_normal((T, hin * fin), dtype=np.float32), -0.5))
+    W = _h(rng.standard_normal((K, fout), dtype=np.float32) / np.sqrt(K))
+    bias = _h(rng.standard_normal(fout) * 0.1)
+    scale = rng.uniform(0.5, 1.5, fout).astype(np.float32)
+    shift = (rng.standard_normal(fout) * 0.1).astype(np.float32)
+    dz = _h(rng.standard_normal((M, fout), dtype=np.float32) * 0.05)
+    scale2 = rng.uniform(0.5, 1.5, fin).astype(np.float32)      # BN scale of the layer below
+    mask_in = rng.integers(0, 256, T * hin * fin // 8, dtype=np.uint8)
+    dx_, dW, db_, ddz = kf.upload_fp16(x), kf.upload_fp16(W), kf.upload_fp16(bias), kf.upload_fp16(dz)
+    dsc, dsh, dsc2 = kf.upload_f32(scale), kf.upload_f32(shift), kf.upload_f32(scale2)
+    dmi = kf.DeviceBuffer(mask_in.nbytes)
+    kf.check(kf.core.bridge_transfer_int32(dmi.ptr, mask_in.ctypes.data, mask_in.nbytes // 4), "mask upload")
+    y, ymask = kf.DeviceBuffer(M * fout * 2), kf.DeviceBuffer(M * fout // 8)
+    gx = kf.DeviceBuffer(T * hin * fin * 2)
+    gW, gb = kf.DeviceBuffer(K * fout * 4), kf.DeviceBuffer(fout * 4)
+
+    # forward: op_im2col (k-contiguous), plain weights, the conv layer's epilogue
+    a = kf.operand(dx_.ptr, hin * fin, M, K, 1, nparts=9, part_width=fin, T=T, hout=hout, hsrc=hin,
+                   hmul=sub, hdiv=1, tpolicy=0, dt=[o[0] for o in OFFS], dh=[o[1] for o in OFFS])
+    b = kf.operand(dW.ptr, fout, K, fout, 0)
+    e = kf.KfEpilogue(out=y.ptr, ldo=fout, alpha=1.0, bias=db_.ptr, relu=1, mask_out=ymask.ptr, scale=dsc.ptr,
+                      shift=dsh.ptr)
+    kf.check(kf.core.kf_gemm_fused(M, fout, K, C.byref(a), C.byref(b), C.byref(e)), name + " forward")
+    # input gradient: op_col2im with op_wrows, out2 = v * scale2 * mask (the layer below's dz)
+    if sub == 1:
+        a2 = kf.operand(ddz.ptr, hout * fout, T * hin, 9 * fout, 1, nparts=9, part_width=fout, T=T, hout=hin,
+                        hsrc=hout, hmul=1, hdiv=1, tpolicy=0, dt=[-o[0] for o in OFFS], dh=[-o[1] for o in OFFS])
+        b2 = kf.operand(dW.ptr, fout, fin, 9 * fout, 1, nparts=9, part_width=fout, T=K,
+                        dt=[p * fin for p in range(9)])
+        e2 = kf.KfEpilogue(out2=gx.ptr, ldo2=fin, scale2=dsc2.ptr, mask_in=dmi.ptr, alpha=1.0)
+        kf.check(kf.core.kf_gemm_fused(T * hin, fin, 9 * fout, C.byref(a2), C.byref(b2), C.byref(e2)),
+                 name + " dgrad")
+    else:
+        for pi in range(sub):   # one GEMM per input-height residue (network.cpp:1620-1650)
+            taps = [(o, dt, (pi - dh) // sub) for o, (dt, dh) in enumerate(OFFS) if (pi - dh) % sub == 0]
+            n = len(taps)
+            a2 = kf.operand(ddz.ptr, hout * fout, T * (hin // sub), n * fout, 1, nparts=n, part_width=fout, T=T,
+                            hout=hin // sub, hsrc=hout, hmul=1, hdiv=1, tpolicy=0,
+                            dt=[-tp[1] for tp in taps], dh=[tp[2] for tp in taps])
+            b2 = kf.operand(dW.ptr, fout, fin, n * fout, 1, nparts=n, part_width=fout, T=K,
+                            dt=[tp[0] * fin for tp in taps])
+            e2 = kf.KfEpilogue(out2=gx.ptr + pi * fin * 2, ldo2=sub * fin, scale2=dsc2.ptr,
+                               mask_in=dmi.ptr + pi * fin // 8, alpha=1.0)
+            kf.check(kf.core.kf_gemm_fused(T * (hin // sub), fin, n * fout, C.byref(a2), C.byref(b2), C.byref(e2)),
+                     name + " dgrad residue %d" % pi)
+    # weight gradient: op_im2col reduction-major, split-K over the 3.84 M / 1.92 M / 0.96 M rows
+    aw = kf.operand(dx_.ptr, hin * fin, M, K, 0, nparts=9, part_width=fin, T=T, hout=hout, hsrc=hin,
+                    hmul=sub, hdiv=1, tpolicy=0, dt=[o[0] for o in OFFS], dh=[o[1] for o in OFFS])
+    bw = kf.operand(ddz.ptr, fout, M, fout, 0)
+    kf.check(kf.core.kf_gemm_wgrad(K, fout, M, C.byref(aw), C.byref(bw), gW.ptr, fout, gb.ptr, 0), name + " wgrad")
+    kf.sync()
+
+    x3 = x.reshape(T, hin, fin)
+    edge_t = [0, 1, T - 2, T - 1, 1499, 1500]
+    # forward on 4,096 sampled output rows plus the edge frames / heights
+    ts = np.concatenate([rng.integers(0, T, 4096), np.repeat(edge_t, 2)])
+    hs = np.concatenate([rng.integers(0, hout, 4096), np.tile([0, hout - 1], len(edge_t))])
+    P = _im2col_rows(x3, ts, hs, sub)
+    acc = P @ W.astype(np.float64) + bias.astype(np.float64)
+    bound = K * U23 * (np.abs(P) @ np.abs(W.astype(np.float64))) + 1e-6 * np.abs(acc)
+    ref = np.maximum(acc, 0) * scale + shift
+    rows = ts * hout + hs
+    g_y = kf.read_fp16(y.ptr, (M, fout))[rows].astype(np.float64)
+    _within(g_y, ref, bound * scale + np.abs(ref) * 2 ** -10 + 1e-6 * np.abs(ref) + 2 ** -24, name + " forward")
+    mbits = _bits(kf.read_fp16(ymask.ptr, (M * fout // 16,)).view(np.uint8), rows, fout)
+    sure = np.abs(acc) > bound
+    assert np.array_equal(mbits[sure], (acc > 0)[sure]), name + " ReLU mask"
+    # input gradient on 4,096 sampled input rows plus the edges
+    ts = np.concatenate([rng.integers(0, T, 4096), np.repeat(edge_t, 2)])
+    hs = np.concatenate([rng.integers(0, hin, 4096), np.tile([0, hin - 1], len(edge_t))])
+    v, mag = _col2im_rows(dz.reshape(T, hout, fout), W, ts, hs, sub, fin)
+    rows = ts * hin + hs
+    mb = _bits(mask_in, rows, fin)
+    v2 = v * scale2 * mb
+    tol2 = (9 * fout * U23 * mag + 1e-6 * np.abs(v)) * scale2 + np.abs(v2) * 2 ** -10 + 2 ** -24
+    g_x = kf.read_fp16(gx.ptr, (T * hin, fin))[rows].astype(np.float64)
+    _within(g_x, v2, tol2, name + " dgrad")
+    # weight gradient and bias sums, every element, blockwise fp64 P^T dZ
+    refw = np.zeros((K, fout))
+    magw = np.zeros((K, fout))
+    dz3 = dz.reshape(T, hout, fout)
+    for t0 in range(0, T, 2000):
+        tt = np.repeat(np.arange(t0, min(T, t0 + 2000)), hout)
+        hh = np.tile(np.arange(hout), tt.size // hout)
+        Pb = _im2col_rows(x3, tt, hh, sub)
+        Db = dz3[tt, hh].astype(np.float64)
+        refw += Pb.T @ Db
+        magw += np.abs(Pb).T @ np.abs(Db)
+    _within(kf.read_f32(gW.ptr, (K, fout)).astype(np.float64), refw, M * U23 * magw * 1.01 + 1e-30, name + " dW")
+    dz64 = dz.astype(np.float64)
+    _within(kf.read_f32(gb.ptr, (fout,)).astype(np.float64), dz64.sum(0), M * U23 * np.abs(dz64).sum(0) * 1.01,
+            name + " db")

@@ -346,11 +346,54 @@ def test_den_exchange_xcd_local_matches_agent_scope(gpu, den, negs):
         ch.compute(nb, dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
         res = ch.result()
         outs.append((res.objf, res.num_ok, ch.seq_stats(negs).copy(), gpu.read_fp16(og.ptr, x.shape)))
+        c = ch.debug_census()
+        assert c["forced"] == force and c["units"] == (negs + 1) // 2
+        if not force:
+            # the default run really took the L2-local exchange: every unit's workgroups
+            # shared one XCD in both recursions (else this compares agent scope with itself)
+            assert c["local_fwd"] == c["local_bwd"] == c["units"], c
     ch.debug_exchange_sys(False)
     for o in outs[1:]:
         assert o[0] == outs[0][0] and o[1] == outs[0][1] == negs
         np.testing.assert_array_equal(o[2], outs[0][2])
         np.testing.assert_array_equal(o[3], outs[0][3])
+
+
+@pytest.mark.slow
+def test_bench_size_objective_matches_oracle(gpu, den):
+    """The bench's own objective configuration — 64 egs x 1500 frames, sequence pairs,
+    G = 4 workgroups per unit, default (XCD-local) placement, the numerator co-resident on
+    the side stream — against oracle.chain_objf (backward.go:224-371, chain_den.cu:496-706)
+    on a sample of sequences: both members of pair 0, one mid-grid pair, the last unit and
+    one ragged pair (members of unequal length). Bars of SURVEY §8d: |d objf/frame| <=
+    1e-3, numerator |d| <= 1e-2, gradient rows <= 1e-4 + one fp16 ulp."""
+    from kfp16 import chain
+    negs = 64
+    g, init, P, row0, frames, stride, fsts, x = _batch_setup(gpu, den, negs, seed=77)
+    frames = frames.copy()
+    frames[45] = 333                     # unit 22 = sequences 44, 45: a ragged pair
+    dx = gpu.upload_fp16(x)
+    og = gpu.upload_fp16(np.full(x.shape, 7.0, np.float16))
+    ch = chain.Chain(chain.DenGraph(g, init), max_seqs=negs, max_frames=490)
+    ch.compute(chain.NumBatch(fsts), dx.ptr, P, x.shape[0], row0, frames, stride, og.ptr, P)
+    res = ch.result()
+    c = ch.debug_census()
+    assert res.num_ok == negs and c["units"] == negs // 2
+    assert c["local_fwd"] == c["local_bwd"] == c["units"] and not c["forced"], c
+    stats = ch.seq_stats(negs)
+    xf = x.astype(np.float32)
+    for i in (0, 1, 30, 31, 44, 45, 62, 63):
+        rows = row0[i] + np.arange(frames[i]) * stride
+        got = gpu.read_fp16(og.ptr + int(rows[0]) * P * 2, (int(rows[-1] - rows[0]) + 1, P))[::stride]
+        deriv, r = oracle.chain_objf(g, init, fsts[i], xf[rows])
+        assert abs(stats[i, 0] - r["num_logprob"]) <= 1e-2, (i, stats[i, 0], r["num_logprob"])
+        assert abs(stats[i, 2] - r["objf"]) / frames[i] <= 1e-3, (i, stats[i, 2], r["objf"])
+        ref = -deriv
+        err = np.abs(got.astype(np.float32) - ref) - (1e-4 + np.abs(ref) * 2 ** -10)
+        assert np.all(err <= 0), (i, float(err.max()))
+    # the ragged member's rows past its end keep the sentinel
+    tail = row0[45] + frames[45] * stride
+    assert np.all(gpu.read_fp16(og.ptr + int(tail) * P * 2, (3, P)) == 7.0)
 
 
 def test_den_exchange_timeout_is_sticky(gpu, den):

@@ -37,7 +37,10 @@ def test_ops_gemm_matches_fp32(gpu):
     h = kfp16.core.ops_cublas_create()
     for (M, N, K, alpha, beta) in [(256, 128, 64, 1.0, 0.0), (300, 3080, 256, 1.0, 0.0),
                                    (1, 64, 96000, 1.0, 0.0), (130, 160, 3072, 0.5, 1.0),
-                                   (37, 24, 9, 1.0, 0.0), (64, 40, 40, 2.0, -1.0)]:
+                                   (37, 24, 9, 1.0, 0.0), (64, 40, 40, 2.0, -1.0),
+                                   # short K on the 8-column vector kernel: AddBias's K = 1 form
+                                   # (ops.go:335-351, beta = 1), K = 3, K = 8
+                                   (1000, 1536, 1, 1.0, 1.0), (77, 40, 3, 0.5, -1.0), (50, 64, 8, 1.0, 0.0)]:
         A = rng.standard_normal((M, K)).astype(np.float16)
         B = (rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float16)
         C0 = rng.standard_normal((M, N)).astype(np.float16)

@@ -173,21 +173,28 @@ def _bn_params(rng, D):
     return mean, var, gamma, beta
 
 
-@pytest.mark.parametrize("T,D", [(1, 1), (13, 37), (64, 128), (7, 1536)])
+@pytest.mark.parametrize("T,D", [(1, 1), (13, 37), (64, 128), (7, 1536), (1001, 160), (3, 8)])
 def test_batchnorm_forward_and_rms(gpu, ab, T, D):
-    """ops.cu:171-204 (inference BN with frozen statistics)."""
+    """ops.cu:171-204 (inference BN with frozen statistics): one fp16 ulp of the float64
+    value, plus the fp32 evaluation's own error where gamma * norm and beta cancel (the
+    subtraction, sqrtf, division and fma each round once: <= 2^-21 (|gamma norm| + |beta|))."""
     rng = rng_for("bn", T, D)
     x = f16(rng.standard_normal((T, D)) * 2)
     mean, var, gamma, beta = _bn_params(rng, D)
     dm, dv, dg, db = (gpu.upload_f32(a) for a in (mean, var, gamma, beta))
     eps = 1e-3
     norm = (x.astype(np.float64) - mean) / np.sqrt(var.astype(np.float64) + np.float32(eps))
+
+    def within(got, ref, terms):
+        sp = np.spacing(np.abs(ref).astype(np.float16)).astype(np.float64)
+        err = np.abs(np.asarray(got, np.float64) - ref)
+        assert np.all(err <= sp + 2.0 ** -21 * terms), float(np.max((err - 2.0 ** -21 * terms) / sp))
     s = Slot(gpu, x)
     assert gpu.core.ops_batchnorm_forward(s.ptr, T, D, dm.ptr, dv.ptr, dg.ptr, db.ptr, eps) == 0
-    assert ulp_dist(s.read().reshape(T, D), gamma * norm + beta).max() <= 1.0
+    within(s.read().reshape(T, D), gamma * norm + beta, np.abs(gamma * norm) + np.abs(beta))
     s = Slot(gpu, x)
     assert gpu.core.ops_batchnorm_forward_rms(s.ptr, T, D, dm.ptr, dv.ptr, 0.5, eps) == 0
-    assert ulp_dist(s.read().reshape(T, D), norm * 0.5).max() <= 1.0
+    within(s.read().reshape(T, D), norm * 0.5, np.abs(norm * 0.5))
 
 
 def test_batchnorm_backward_backtest_pin(gpu, ab):
@@ -208,6 +215,21 @@ def test_batchnorm_backward_backtest_pin(gpu, ab):
     rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-6)
     assert rel.max() <= 0.02
     assert ulp_dist(got, ref).max() <= 1.0
+
+
+@pytest.mark.parametrize("rows,cols,off", [(13, 37, 0), (1001, 160, 0), (9, 64, 1)])
+def test_batchnorm_backward_shapes(gpu, ab, rows, cols, off):
+    """backward_wrappers.cu:105-115 on the scalar kernel (ragged cols, misaligned) and the
+    8-column vector kernel (16-byte-granular rows): 1 ulp of grad * gamma / sqrt(var + eps)."""
+    rng = rng_for("bnb", rows, cols, off)
+    g = f16(rng.standard_normal((rows, cols)))
+    gamma = (rng.random(cols) + 0.5).astype(np.float32)
+    var = (rng.random(cols) * 1.5 + 0.5).astype(np.float32)
+    dgm, dv = gpu.upload_f32(gamma), gpu.upload_f32(var)
+    go, gi = Slot(gpu, g, off), Slot(gpu, np.zeros_like(g), off)
+    assert gpu.core.ops_batchnorm_backward(go.ptr, gi.ptr, dgm.ptr, dv.ptr, 1e-3, rows, cols) == 0
+    ref = g.astype(np.float64) * (gamma / np.sqrt(var.astype(np.float64) + np.float32(1e-3)))
+    assert ulp_dist(gi.read().reshape(rows, cols), ref).max() <= 1.0
 
 
 # ----------------------------------------------------------------- element-wise
@@ -243,14 +265,18 @@ def test_copy_fill_fp16_to_fp32(gpu, ab, count):
 
 
 # ----------------------------------------------------------------- layout ops
-@pytest.mark.parametrize("T,src_cols,dst_cols,off", [(1, 1, 3, 2), (11, 40, 72, 32), (37, 129, 300, 7)])
-def test_concat_slice_cols(gpu, ab, T, src_cols, dst_cols, off):
-    """ops.cu:241-254 and :308-320: column placement / extraction, bit-exact."""
+@pytest.mark.parametrize("T,src_cols,dst_cols,off,soff", [(1, 1, 3, 2, 1), (11, 40, 72, 32, 1), (37, 129, 300, 7, 1),
+                                                           (11, 40, 72, 32, 0), (301, 160, 320, 160, 0),
+                                                           (5, 1536, 3072, 0, 0), (9, 24, 64, 8, 0)])
+def test_concat_slice_cols(gpu, ab, T, src_cols, dst_cols, off, soff):
+    """ops.cu:241-254 and :308-320: column placement / extraction, bit-exact. soff = 1
+    misaligns the source (scalar kernel); 16-byte-granular shapes with soff = 0 run the
+    8-column vector kernel."""
     rng = rng_for("cat", T, src_cols)
     src = f16(rng.standard_normal((T, src_cols)))
     base = f16(rng.standard_normal((T, dst_cols)))
     d = Slot(gpu, base)
-    s = Slot(gpu, src, 1)
+    s = Slot(gpu, src, soff)
     assert gpu.core.ops_concat_cols(d.ptr, T, dst_cols, s.ptr, src_cols, off) == 0
     ref = base.copy()
     ref[:, off:off + src_cols] = src
