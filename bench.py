@@ -46,6 +46,7 @@ METRIC_FWD = "frames/sec CNN-TDNN forward only, 40-dim×1500-frame egs, 1 MI355X
 PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5000.0    # MI355X dense FP8 (MX-scaled K=128 MFMA)
 PEAK_HBM_GBPS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
+PEAK_L2_BPS = 34.5e12       # MI355X aggregate L2 read bandwidth (the den's arc-table streams)
 FRAMES_PER_EG = 1500
 # algorithmic MFLOP per input frame: forward, and forward +
 # backward (dW of every layer, dX of all but IDCT and cnn1) — the step's FLOPs for the
@@ -165,8 +166,9 @@ def step_classes(cls, steps, peak_tflops):
         if name == "chain_num":
             row["arc_updates_per_s"] = round(fl / sec, 1) if sec > 0 else None
         elif name == "chain_den":
-            row["alg_GBps"] = round(fl / sec / 1e9, 1) if sec > 0 else None
-            row["hbm_frac"] = round(fl / sec / 1e9 / PEAK_HBM_GBPS, 4) if sec > 0 else None
+            # algorithmic bytes of the recursion and posteriors, mostly L2 arc-table streams
+            row["alg_L2_GBps"] = round(fl / sec / 1e9, 1) if sec > 0 else None
+            row["l2_frac"] = round(fl / sec / PEAK_L2_BPS, 4) if sec > 0 else None
         else:
             tf = fl / sec / 1e12 if sec > 0 else 0.0
             gbps = by / sec / 1e9 if sec > 0 else 0.0
@@ -621,7 +623,7 @@ def main():
                             "den_ms_per_step": round(dms / a.steps, 3),
                             # the den streams its arc tables from L2 (~1 MB, resident): L2 bytes
                             "den_L2_GBps": round(dbytes / (dms * 1e-3) / 1e9, 1) if dms else None,
-                            "den_L2_frac": round(dbytes / (dms * 1e-3) / 34.5e12, 4) if dms else None,
+                            "den_L2_frac": round(dbytes / (dms * 1e-3) / PEAK_L2_BPS, 4) if dms else None,
                             "ok_seqs": int(head["stats"][4])}
         if "roofline" in d:
             rl = d["roofline"]
