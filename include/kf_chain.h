@@ -117,9 +117,10 @@ void kf_chain_debug_exchange_sys(KfChain *c, int force);
  * even where two sequences could share each record (the default, pairs == 1). */
 void kf_chain_debug_den_pairs(KfChain *c, int pairs);
 /* Diagnostics (tests): the XCD census of the last compute's den launch. *units = exchange
- * units per direction; *local_fwd / *local_bwd = units whose G workgroups all ran on one
- * XCD (those take the L2-local exchange unless *forced = 1, kf_chain_debug_exchange_sys). */
-int kf_chain_debug_census(KfChain *c, int *units, int *local_fwd, int *local_bwd, int *forced);
+ * units per direction, *G = workgroups per unit; *local_fwd / *local_bwd = units whose G
+ * workgroups all ran on one XCD (those take the L2-local exchange unless *forced = 1,
+ * kf_chain_debug_exchange_sys). Any out pointer may be NULL. */
+int kf_chain_debug_census(KfChain *c, int *units, int *local_fwd, int *local_bwd, int *forced, int *G);
 
 const char *kf_chain_last_error(void);
 void kf_chain_clear_error(void);

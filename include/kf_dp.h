@@ -67,10 +67,12 @@ int kf_dp_stats(const KfDp *dp, long long *launches, long long *values);
  *                          offset: a two-rank average whose other rank's gradient is
  *                          aux_base (a test supplies a second shard's gradient), so the
  *                          gates, the bucket coverage and kf_dp_join all change results.
+ * count: fp32 values of grad_base (and of aux_base). While a mode is on, an exchange of a
+ * bucket outside [grad_base, grad_base + count) fails instead of touching aux out of range.
  * mode 0 turns them off. The two modes are exclusive. -1: bad arguments. */
 #define KF_DP_DEBUG_SNAPSHOT 1
 #define KF_DP_DEBUG_PEER_MEAN 2
-int kf_dp_debug(KfDp *dp, int mode, const float *grad_base, float *aux_base);
+int kf_dp_debug(KfDp *dp, int mode, const float *grad_base, float *aux_base, size_t count);
 
 /* Bucket plan of a flat gradient buffer (host only, no device work).
  * steps: the backward visits nsteps parameter groups in order; group i occupies

@@ -938,8 +938,8 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
                 pq[q] += v;
             }
         }
-        if (r.trace && unit == 0 && lane == 0 && t >= 16 && t < 48)  // per-wave arc end, blocks 0, 1
-            r.trace[256 + ((t - 16) * 2 + (gi & 1)) * DEN_WAVES + wave] = wall_clock64();
+        if (r.trace && unit == 0 && gi < 2 && lane == 0 && t >= 16 && t < 48)  // per-wave arc end, blocks 0, 1
+            r.trace[256 + ((t - 16) * 2 + gi) * DEN_WAVES + wave] = wall_clock64();
         DEN_TP(1);
         float ws[NS];
 #pragma unroll
@@ -2914,10 +2914,10 @@ extern "C" void kf_chain_debug_exchange_sys(KfChain *c, int force) {
 }
 
 // diagnostics (tests): the XCD census of the last compute's den launch. *units = exchange
-// units per direction; *local_fwd / *local_bwd = units whose G workgroups all ran on one
-// XCD, i.e. took the L2-local exchange unless kf_chain_debug_exchange_sys forced agent
-// scope (*forced = 1). 0, or -1 on error.
-extern "C" int kf_chain_debug_census(KfChain *c, int *units, int *local_fwd, int *local_bwd, int *forced) {
+// units per direction, *G = workgroups per unit; *local_fwd / *local_bwd = units whose G
+// workgroups all ran on one XCD, i.e. took the L2-local exchange unless
+// kf_chain_debug_exchange_sys forced agent scope (*forced = 1). 0, or -1 on error.
+extern "C" int kf_chain_debug_census(KfChain *c, int *units, int *local_fwd, int *local_bwd, int *forced, int *G) {
     if (!c) return -1;
     hipStream_t st = kf_stream();
     const int f = c->xbuf.census_local(st), b = c->xbuf2.census_local(st);
@@ -2929,6 +2929,7 @@ extern "C" int kf_chain_debug_census(KfChain *c, int *units, int *local_fwd, int
     if (local_fwd) *local_fwd = f;
     if (local_bwd) *local_bwd = b;
     if (forced) *forced = c->xbuf.force_sys;
+    if (G) *G = c->xbuf.last_G;
     return 0;
 }
 

@@ -95,6 +95,7 @@ struct KfDp {
     int debug = 0;
     const float *dbg_base = nullptr;  // the gradient buffer the buckets lie in
     float *dbg_aux = nullptr;         // snapshot / peer buffer, same layout
+    size_t dbg_n = 0;                 // values in both
 };
 
 extern "C" const char *kf_dp_last_error(void) { return g_err[0] ? g_err : nullptr; }
@@ -167,7 +168,14 @@ extern "C" int kf_dp_allreduce_mean_async(KfDp *dp, float *buf, size_t count) {
     if (!hip_ok(hipEventRecord(gate, kf_stream()), "hipEventRecord") ||
         !hip_ok(hipStreamWaitEvent(dp->comm_stream, gate, 0), "hipStreamWaitEvent"))
         return -1;
-    const bool dbg = dp->debug && buf >= dp->dbg_base;
+    // the hooks apply to buckets inside [grad_base, grad_base + n) only; any other
+    // buffer would send the snapshot / peer mean past the end of aux
+    const bool dbg = dp->debug != 0;
+    if (dbg && (buf < dp->dbg_base || (size_t)(buf - dp->dbg_base) > dp->dbg_n ||
+                count > dp->dbg_n - (size_t)(buf - dp->dbg_base))) {
+        set_err("kf_dp_allreduce_mean_async: debug hooks on, bucket outside the registered gradient");
+        return -1;
+    }
     float *aux = dbg ? dp->dbg_aux + (buf - dp->dbg_base) : nullptr;
     // what the exchange would send, captured at the moment it starts
     if (dbg && (dp->debug & KF_DP_DEBUG_SNAPSHOT) &&
@@ -186,9 +194,9 @@ extern "C" int kf_dp_allreduce_mean_async(KfDp *dp, float *buf, size_t count) {
     return 0;
 }
 
-extern "C" int kf_dp_debug(KfDp *dp, int mode, const float *grad_base, float *aux_base) {
+extern "C" int kf_dp_debug(KfDp *dp, int mode, const float *grad_base, float *aux_base, size_t count) {
     if (!dp || (mode & ~(KF_DP_DEBUG_SNAPSHOT | KF_DP_DEBUG_PEER_MEAN)) ||
-        (mode && (!grad_base || !aux_base)) ||
+        (mode && (!grad_base || !aux_base || !count)) ||
         ((mode & KF_DP_DEBUG_SNAPSHOT) && (mode & KF_DP_DEBUG_PEER_MEAN))) {
         set_err("kf_dp_debug: bad arguments");
         return -1;
@@ -196,6 +204,7 @@ extern "C" int kf_dp_debug(KfDp *dp, int mode, const float *grad_base, float *au
     dp->debug = mode;
     dp->dbg_base = mode ? grad_base : nullptr;
     dp->dbg_aux = mode ? aux_base : nullptr;
+    dp->dbg_n = mode ? count : 0;
     return 0;
 }
 

@@ -561,6 +561,7 @@ struct HaloArgs {
     int nbuf;               // halo images (2 when nch > 1)
     int ctap[KF_MAX_PARTS];
     int bshift[KF_MAX_PARTS];  // BROW: row shift of tap p's weight block (op_wrows)
+    unsigned mhpos;            // ceil(2^32 / hpos): R / hpos = umulhi(R, mhpos)
     unsigned long long *trace;  // diagnostics (kf_halo_trace): block 300 wave 0 stamps, else null
 };
 
@@ -601,8 +602,14 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     constexpr int B_STAGE = BN * BK * 2;
-    using SB = Stager<BKC, BN, BMODE, NW>;
-    static_assert(SB::EVEN, "uniform B loads per wave");
+    // Waves 0 .. NWB-1 stage B (weights, L2), the others the next chunk's halo slices
+    // (HBM). vmcnt is per wave and loads retire in order, so a B wave's per-step wait no
+    // longer queues behind halo loads, and a halo wave waits only at a chunk start: the
+    // slices get the whole chunk to land instead of one step.
+    constexpr int NWB = NW / 2;
+    using SB = Stager<BKC, BN, BMODE, NWB>;
+    static_assert(SB::EVEN, "uniform B loads per B wave");
+    static_assert(ST == 2, "the split-wave waits are written for a two-stage B ring");
     extern __shared__ __attribute__((aligned(16))) char dsm[];
     char *bring = dsm + H.nbuf * H.halo_bytes;  // ST B stages after the halo images
 
@@ -621,23 +628,27 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
     const int m0 = mt * BM, n0 = nt * BN;
     const int tbase = m0 / H.hout + H.dtmin;
 
+    const bool bwave = wave < NWB;
     SB sb;
-    sb.init(B, n0, wave, lane);
+    if (bwave) sb.init(B, n0, wave, lane);
     const Rsrc rx = make_rsrc(H.x), rb = make_rsrc(B.base);
     const int K = H.ntaps * H.pw;
 
-    // halo pieces [q0, q1) of chunk c into image `img`, wave-strided
-    auto halo_issue = [&](int c, int img, int q0, int q1) {
+    // halo pieces [q0, q1) of chunk c into image `img`, strided over waves w0 .. w0+nw-1
+    auto halo_issue = [&](int c, int img, int q0, int q1, int w0, int nw) {
         char *dst = dsm + img * H.halo_bytes;
         // lane l fills 16-byte position l of the piece: chunk kc, row 8q + r with
         // halo_off(R, kc) = 1024 q + 16 l (block kc / 2 = l / 16, slot (kc + 2r) mod 16 = l mod 16)
         const int slot = lane & 15, kc = 2 * (lane >> 4) + (slot & 1), r = ((slot - kc) & 15) >> 1;
-        for (int q = q0 + wave; q < q1; q += NW) {
+        if (wave < w0) return;
+        for (int q = q0 + wave - w0; q < q1; q += nw) {
             const int R = 8 * q + r;
             unsigned voff = BAD;
             if (R < H.rows) {
-                const int f = R / H.hpos, pos = R - f * H.hpos;
-                const int par = pos / H.hpe, idx = pos - par * H.hpe;
+                // f = R / hpos by multiply-high (exact for every R < rows: host-checked);
+                // hmul <= 2, so the parity half is one compare
+                const int f = (int)__umulhi((unsigned)R, H.mhpos), pos = R - f * H.hpos;
+                const int par = pos >= H.hpe ? 1 : 0, idx = pos - par * H.hpe;
                 const int sh = idx * H.hmul + par - H.pad, t = tbase + f;
                 if ((unsigned)t < (unsigned)H.T && (unsigned)sh < (unsigned)H.hsrc)
                     voff = (unsigned)(((long long)t * H.ld + (long long)sh * H.pw + c * BK + kc * 8) * 2);
@@ -663,6 +674,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
     const int steps = H.nch * H.ntaps;
     auto issue_b = [&](int st1, char *dst) {
         const int c1 = st1 / H.ntaps, p1 = st1 - c1 * H.ntaps;
+        if (!bwave) return;
         if constexpr (BROW) {
             const h16 *bb = B.base + (long long)H.bshift[p1] * B.ld + c1 * BK;
             sb.issue(B, make_rsrc(bb), 0, BK, dst, wave, lane);
@@ -670,45 +682,26 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
             sb.issue(B, rb, p1 * H.pw + c1 * BK, K, dst, wave, lane);
         }
     };
-    // this wave's halo loads in the slice issued at step s (0 when none is issued)
-    auto halo_count = [&](int s) {
-        const int cs = s / H.ntaps, ps = s - cs * H.ntaps;
-        if (H.nbuf < 2 || cs + 1 >= H.nch) return 0;
-        const int q0 = ps * H.slice, q1 = min(H.npieces, q0 + H.slice);
-        return q1 - q0 > wave ? (q1 - q0 - wave + NW - 1) / NW : 0;
-    };
     const bool tr = H.trace && blockIdx.x == 300 && tid == 0;
 #define HALO_TP(slot) \
     if (tr && (slot) < 128) H.trace[slot] = wall_clock64();
     HALO_TP(0);
     const EpiPre epre = epi_params<BN, 64 * NW>(E, N, n0, tid);
-    halo_issue(0, 0, 0, H.npieces);
-    static_for<ST - 1>([&](auto I) {
-        constexpr int i = decltype(I)::value;
-        if (i < steps) issue_b(i, bring + i * B_STAGE);
-    });
-    // loads this wave issued in the last two steps (for the counted waits of ST = 3, 4)
-    int n1 = (ST >= 3 && ST - 2 < steps) ? SB::NC : 0, n2 = (ST >= 4 && ST - 3 < steps) ? SB::NC : 0;
+    halo_issue(0, 0, 0, H.npieces, 0, NW);
+    if (steps > 0) issue_b(0, bring);
     int sb_st = 0;  // B stage of step st
     for (int st = 0; st < steps; ++st) {
         const int c = st / H.ntaps, p = st - c * H.ntaps;
-        if constexpr (ST == 2) {
-            wait_vmcnt<0>();
-        } else {
-            // B(st) was issued ST - 1 steps ago; younger: everything of the last ST - 2
-            // steps. At a chunk start the halo of chunk c (its last slice issued first in
-            // step st - 1) must have landed too: younger than it, only step st - 1's B.
-            int younger = ST == 3 ? n1 : n1 + n2;
-            if (c > 0 && p == 0) younger = min(younger, st - 1 + ST - 1 < steps ? (int)SB::NC : 0);
-            wait_vmcnt_rt(younger);
-        }
+        // B waves: B(st), issued in step st - 1; halo waves: the whole halo of chunk c at
+        // its first step (its slices were issued over chunk c - 1's steps)
+        if (bwave || p == 0) wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         HALO_TP(1 + 2 * st);
         if (H.nbuf == 1 && c > 0 && p == 0) {
             // one halo image (two do not fit beside the B ring): every wave is past the
             // previous chunk's last fragment reads, so reload it in place and wait
-            halo_issue(c, 0, 0, H.npieces);
+            halo_issue(c, 0, 0, H.npieces, 0, NW);
             wait_vmcnt<0>();
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
@@ -716,17 +709,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         // the halo slice first, then the B stage (the order the waits above count)
         if (H.nbuf > 1 && c + 1 < H.nch) {
             const int q0 = p * H.slice;
-            halo_issue(c + 1, (c + 1) & 1, q0, min(H.npieces, q0 + H.slice));
+            halo_issue(c + 1, (c + 1) & 1, q0, min(H.npieces, q0 + H.slice), NWB, NW - NWB);
         }
-        const bool issue = st + ST - 1 < steps;
-        if (issue) {
-            const int sn = sb_st == 0 ? ST - 1 : sb_st - 1;  // (st + ST - 1) % ST
-            issue_b(st + ST - 1, bring + sn * B_STAGE);
-        }
-        if constexpr (ST >= 3) {
-            n2 = n1;
-            n1 = halo_count(st) + (issue ? SB::NC : 0);
-        }
+        if (st + 1 < steps) issue_b(st + 1, bring + (sb_st ^ 1) * B_STAGE);
         const char *ta = dsm + (H.nbuf > 1 ? (c & 1) : 0) * H.halo_bytes;
         const char *tb = bring + sb_st * B_STAGE;
         sb_st = sb_st + 1 == ST ? 0 : sb_st + 1;
@@ -1217,6 +1202,10 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     if (lds > 160 * 1024) return 0;
     H.rows = H.nf * H.hpos;
     H.npieces = (H.rows + 7) / 8;
+    H.mhpos = (unsigned)((0x100000000ULL + H.hpos - 1) / H.hpos);
+    if (a.hmul > 2) return 0;
+    for (unsigned R = 0; R < (unsigned)(8 * H.npieces); ++R)
+        if ((unsigned)(((unsigned long long)R * H.mhpos) >> 32) != R / (unsigned)H.hpos) return 0;
     H.slice = (H.npieces + H.ntaps - 1) / H.ntaps;
     for (int p = 0; p < a.nparts; ++p) {
         const int x = a.dh[p] + H.pad;

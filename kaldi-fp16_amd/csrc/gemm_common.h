@@ -151,8 +151,9 @@ __device__ __forceinline__ Rsrc make_rsrc(const void *base) {
 // the reads of a stage (cdna_hip_programming.md, "What hipcc does not do", LDS-DMA recipe).
 template <int BYTES>
 __device__ __forceinline__ void lds_dma(Rsrc rs, const void *lds_dst, unsigned voff) {
-    const unsigned m0v = (unsigned)__builtin_amdgcn_readfirstlane(
-        (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void *)lds_dst);
+    // the low dword of a flat pointer into LDS is the LDS offset (the shared aperture is the
+    // high dword); no address-space cast, which hipcc miscompiles inside some wave branches
+    const unsigned m0v = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds_dst);
     unsigned keep;
     if constexpr (BYTES == 16)
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"

@@ -1079,8 +1079,7 @@ extern "C" int nnet_forward_ivector(KfNet *net, const void *features, int T, con
 }
 // k-contiguous (transposed) copies of the short-K forward weights: the tiled GEMM's
 // k-contiguous B path beats its reduction-major one on these shapes (TDNN-F affine
-// forward with the full epilogue 243 -> 225 us, scripts/panel_bench.py), and the
-// panel GEMM (csrc/panel.hip, KF_PANEL=1) reads only B^T rows
+// forward with the full epilogue 243 -> 225 us, DESIGN.md §7 performance log, r2)
 static bool refresh_wt(KfNet *net) {
     if (!net->wt_dirty) return true;
     // one launch for every layer's copy (was one ops_transpose each: 18 x 9 us per step)

@@ -111,7 +111,7 @@ _sig(core, "kf_dp_join", _i, _vp)
 _sig(core, "kf_dp_allreduce_mean", _i, _vp, _vp, _sz)
 _sig(core, "kf_dp_allreduce_sum_f64", _i, _vp, _vp, _sz)
 _sig(core, "kf_dp_stats", _i, _vp, C.POINTER(_ll), C.POINTER(_ll))
-_sig(core, "kf_dp_debug", _i, _vp, _i, _vp, _vp)
+_sig(core, "kf_dp_debug", _i, _vp, _i, _vp, _vp, C.c_size_t)
 _sig(core, "kf_dp_plan", _i, _i, C.POINTER(_ll), C.POINTER(_ll), _ll, _ll, _i, C.POINTER(_i),
      C.POINTER(_ll), C.POINTER(_ll))
 _sig(core, "kf_prof_enable", None, _i)

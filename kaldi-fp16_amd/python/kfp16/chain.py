@@ -69,7 +69,7 @@ _sig("kf_chain_debug_spin_limit", None, _vp, C.c_uint)
 _sig("kf_chain_debug_exchange_sys", None, _vp, C.c_int)
 _sig("kf_chain_debug_den_pairs", None, _vp, C.c_int)
 _sig("kf_chain_debug_census", C.c_int, _vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
-     C.POINTER(C.c_int))
+     C.POINTER(C.c_int), C.POINTER(C.c_int))
 _sig("chain_forward_backward", _i, _vp, C.POINTER(ChainFstGPU), _i, _i, _vp, _vp, _fp)
 _sig("chain_compute_posteriors", _i, _vp, C.POINTER(ChainFstGPU), _i, _i, _vp, _vp, _f, _vp)
 _sig("chain_compute_loss", _i, _vp, C.POINTER(ChainFstGPU), C.POINTER(ChainFstGPU), _i, _i, _vp,
@@ -211,10 +211,11 @@ class Chain:
     def debug_census(self) -> dict:
         """The XCD census of the last compute's den launch: exchange units per direction,
         units whose workgroups all shared one XCD (L2-local exchange unless forced)."""
-        v = [C.c_int() for _ in range(4)]
+        v = [C.c_int() for _ in range(5)]
         if core.kf_chain_debug_census(self.h, *(C.byref(x) for x in v)) != 0:
             _raise("kf_chain_debug_census")
-        return {"units": v[0].value, "local_fwd": v[1].value, "local_bwd": v[2].value, "forced": bool(v[3].value)}
+        return {"units": v[0].value, "local_fwd": v[1].value, "local_bwd": v[2].value, "forced": bool(v[3].value),
+                "G": v[4].value}
 
     def seq_stats(self, nseq: int) -> np.ndarray:
         from . import read_f32, sync

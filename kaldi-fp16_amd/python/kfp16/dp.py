@@ -96,12 +96,13 @@ class Communicator:
 
     DEBUG_SNAPSHOT, DEBUG_PEER_MEAN = 1, 2
 
-    def debug(self, mode: int, grad_base=None, aux_base=None):
+    def debug(self, mode: int, grad_base=None, aux_base=None, count: int = 0):
         """kf_dp_debug test hooks: DEBUG_SNAPSHOT copies each bucket to aux (same offset
         from grad_base) as its exchange starts; DEBUG_PEER_MEAN averages each exchanged
-        bucket with aux, a second rank's gradient. 0 turns them off."""
+        bucket with aux, a second rank's gradient. 0 turns them off. count: fp32 values
+        of both buffers (buckets outside them then fail)."""
         core = _core()
-        if core.kf_dp_debug(self.h, int(mode), grad_base, aux_base) != 0:
+        if core.kf_dp_debug(self.h, int(mode), grad_base, aux_base, int(count)) != 0:
             raise RuntimeError("kf_dp_debug: " + _dp_err(core))
 
     def stats(self):

@@ -27,7 +27,8 @@ a = raw[:256].reshape(32, 8)
 w = raw[256:].reshape(32, 2, 16) - a[:, None, :1]  # per-wave arc end relative to the frame start
 d = np.diff(a, axis=1)
 names = ["arc", "publish", "prefetch", "wait", "psum", "consume", "tail+bar"]
-print("G", os.environ.get("KF_DEN_G", "auto"), "egs", egs)
+cen = ch.debug_census()
+print("G", cen["G"], "units", cen["units"], "XCD-local units", cen["local_fwd"], cen["local_bwd"], "egs", egs)
 print("mean us per phase:", {n: round(float(v), 2) for n, v in zip(names, d[1:].mean(0))})
 fr = np.diff(a[:, 0])
 print("frame period us: mean %.2f min %.2f max %.2f" % (fr.mean(), fr.min(), fr.max()))

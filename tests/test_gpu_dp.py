@@ -77,7 +77,7 @@ def test_exchange_starts_after_its_gradients(gpu, xconfig, T):
     plan = net.dp_plan(BUCKET)
     assert dp.covers_exactly(plan, P) and len(plan) > 4
     net.bind_dp(comm, BUCKET)
-    comm.debug(comm.DEBUG_SNAPSHOT, net.grad_ptr, snap.ptr)
+    comm.debug(comm.DEBUG_SNAPSHOT, net.grad_ptr, snap.ptr, P)
 
     def run(early):
         net.dp_debug_early(early)
@@ -137,7 +137,7 @@ def test_two_shard_mean_then_sgd(gpu, xconfig, T):
     peer = gpu.upload_f32(gb)
     comm = dp.Communicator(0, 1, dp.unique_id(), 0)
     net.bind_dp(comm, BUCKET)
-    comm.debug(comm.DEBUG_PEER_MEAN, net.grad_ptr, peer.ptr)
+    comm.debug(comm.DEBUG_PEER_MEAN, net.grad_ptr, peer.ptr, P)
 
     def bound_step(early):
         net.set_params(w0)
@@ -183,5 +183,17 @@ def test_debug_hook_arguments(gpu):
         comm.debug(3, 16, 16)          # exclusive modes
     with pytest.raises(RuntimeError):
         comm.debug(comm.DEBUG_SNAPSHOT)  # needs both buffers
+    with pytest.raises(RuntimeError):
+        comm.debug(comm.DEBUG_SNAPSHOT, 16, 16)  # and their length
+    # a bucket outside the registered gradient fails instead of writing past aux
+    g, aux = gpu.DeviceBuffer(64 * 4), gpu.DeviceBuffer(64 * 4)
+    other = gpu.DeviceBuffer(64 * 4)
+    comm.debug(comm.DEBUG_SNAPSHOT, g.ptr, aux.ptr, 64)
+    comm.allreduce_mean(g.ptr + 32 * 4, 32)          # inside: fine
+    with pytest.raises(RuntimeError):
+        comm.allreduce_mean(g.ptr + 48 * 4, 32)      # runs past the end
+    with pytest.raises(RuntimeError):
+        comm.allreduce_mean(other.ptr, 16)           # another buffer
+    gpu.sync()
     comm.debug(0)
     comm.close()
