@@ -227,6 +227,11 @@ int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
 int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes);
 void kf_prof_reset(void);
 
+/* test / A-B hook: 1 runs the short-K wide-N fused GEMMs (k-contiguous plain or two-part
+ * spliced A, plain k-contiguous B, 128 < K <= 640, N % 128 == 0, >= 1024 tiles, beta 0, no
+ * MXFP8 copy) on the persistent kernel with store waves; 0 (default) on the tiled kernel.
+ * Returns the previous setting. */
+int kf_gemm_debug_persist(int on);
 /* test hook: the fused GEMM's K-step interleave of a two-part spliced A with parts of
  * >= 512 columns (the TDNN-F linear forward / affine input gradient). 1 (default):
  * the K-steps alternate between the parts; 0: part order. Only the fp32 accumulation

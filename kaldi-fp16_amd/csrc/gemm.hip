@@ -1231,6 +1231,8 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     return 0;
 }
 
+int kf_gemm_persist_try(int M, int N, int K, const OpD &a, const OpD &b, int am, int bm, const KfEpilogue &E);
+
 // K-step interleave of two-part spliced A operands (WgradArgs::kil): 1 = on (default),
 // 0 = part order. Test hook: kf_gemm_debug_kil (kf_ops.h) compares the two orders.
 static int g_kil = 1;
@@ -1286,6 +1288,10 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
     if (!E.out8) {
         const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);
         if (hr != 0) return hr < 0 ? -1 : 0;
+    }
+    if (B->kcontig) {  // short K, wide N: the persistent kernel with store waves (gemm_persist.hip)
+        const int pr = kf_gemm_persist_try(M, N, K, a, b, am, bm, E);
+        if (pr != 0) return pr < 0 ? -1 : 0;
     }
     // Tiles: 384x160 8-wave for N = 160 / 320; 256x64 for N <= 64; for
     // N >= 256 192x128 8-wave tiles (80 KB of LDS: two workgroups share a CU and one's

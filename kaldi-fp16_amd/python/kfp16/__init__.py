@@ -439,5 +439,6 @@ _sig(core, "kf_gemm_fused", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOp
 _sig(core, "kf_gemm_wgrad", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i)
 _sig(core, "kf_rows_sum", _i, _vp, _vp, _ll, _i, _i, _i)
 _sig(core, "kf_gemm_debug_kil", None, _i)
+_sig(core, "kf_gemm_debug_persist", _i, _i)
 _sig(core, "kf_gemm_trace", None, _vp, _i, _i)
 _sig(core, "kf_quant_mxfp8", _i, _vp, _ll, _i, _i, _i, _vp, _ll, _vp, _ll)
