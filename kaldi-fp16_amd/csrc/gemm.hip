@@ -1530,13 +1530,12 @@ __global__ __launch_bounds__(256) void k_gemm_smallk_v8(int M, int ncv, int K, l
             for (int e = 0; e < 8; ++e) b[k][e] = (float)v[e];
         }
     }
-    for (long long m = g / ncv; m < M; m += R) {
+    // four rows in flight per thread: C's row loads are the HBM stream (AddBias: K = 1)
+    auto row = [&](long long m, const half8 &c0) {
         float a[kSmallK];
 #pragma unroll
         for (int k = 0; k < kSmallK; ++k) a[k] = k < K ? h2f(A[m * lda + k]) : 0.f;
-        h16 *c = C + m * ldc + 8 * cv;
         half8 out;
-        const half8 c0 = beta != 0.f ? *reinterpret_cast<const half8 *>(c) : half8{};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             float s = 0.f;
@@ -1547,8 +1546,18 @@ __global__ __launch_bounds__(256) void k_gemm_smallk_v8(int M, int ncv, int K, l
             if (beta != 0.f) v += beta * (float)c0[e];
             out[e] = f2h(v);
         }
-        *reinterpret_cast<half8 *>(c) = out;
+        *reinterpret_cast<half8 *>(C + m * ldc + 8 * cv) = out;
+    };
+    long long m = g / ncv;
+    for (; m + 3 * R < M; m += 4 * R) {
+        half8 c0[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            c0[u] = beta != 0.f ? *reinterpret_cast<const half8 *>(C + (m + u * R) * ldc + 8 * cv) : half8{};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) row(m + u * R, c0[u]);
     }
+    for (; m < M; m += R) row(m, beta != 0.f ? *reinterpret_cast<const half8 *>(C + m * ldc + 8 * cv) : half8{});
 }
 
 // ---------------------------------------------------------------------------

@@ -264,6 +264,17 @@ def test_copy_fill_fp16_to_fp32(gpu, ab, count):
     np.testing.assert_array_equal(gpu.read_f32(out.ptr + 4, (count,)), x.astype(np.float32))
 
 
+@pytest.mark.parametrize("count", [8, 1000, 4099, 8 * 1024 * 256 * 4 + 8 * 37])
+def test_copy_aligned_vector_path(gpu, count):
+    """16-byte aligned, count % 8 == 0: k_copy_v8 (four vectors per thread, then the tail
+    of whole vectors); otherwise the blit. Guards on both sides stay untouched."""
+    rng = rng_for("copyv", count)
+    x = f16(rng.standard_normal(count))
+    src, dst = Slot(gpu, x, 0), Slot(gpu, np.zeros(count), 0)
+    assert gpu.core.ops_copy(dst.ptr, src.ptr, count) == 0
+    np.testing.assert_array_equal(bits(dst.read()), bits(x))
+
+
 # ----------------------------------------------------------------- layout ops
 @pytest.mark.parametrize("T,src_cols,dst_cols,off,soff", [(1, 1, 3, 2, 1), (11, 40, 72, 32, 1), (37, 129, 300, 7, 1),
                                                            (11, 40, 72, 32, 0), (301, 160, 320, 160, 0),
