@@ -132,6 +132,21 @@ int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B, f
 int kf_quant_mxfp8(const void *src, long long ld_src, int rows, int cols, int transpose,
                    void *q, long long ldq, uint8_t *scales, long long lds);
 
+/* Up to KF_QUANT_MAX kf_quant_mxfp8 calls in one launch (the weight copies after each
+ * update: ~80 small matrices per step, each too small to fill the GPU on its own). Same
+ * arguments and results as kf_quant_mxfp8, per job. */
+#define KF_QUANT_MAX 32
+typedef struct KfQuantJob {
+    const void *src;
+    long long ld_src;
+    int rows, cols, transpose;
+    void *q;
+    long long ldq;
+    uint8_t *scales;
+    long long lds;
+} KfQuantJob;
+int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs);
+
 /* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols
  * (edge may be a spare row of src's own allocation) */
 int kf_rows_sum(void *edge, const void *src, long long ld, int r0, int r1, int cols);

@@ -1276,6 +1276,11 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
             return -1;
         }
         const int K2 = K / 2;  // the kernel counts the reduction in 2-byte units
+        if (N % 160 == 0 && N <= 320 && !E.out8) {  // TDNN-F linear (N = bottleneck): no idle columns
+            if (am == OP_SIMPLE)
+                return launch<384, 160, 4, 2, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
+            return launch<384, 160, 4, 2, true, true, false, 2, OP_P2, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
+        }
         if (N >= 256) {
             if (am == OP_SIMPLE)
                 return launch<256, 256, 2, 4, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
@@ -1285,7 +1290,7 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
             return launch<128, 128, 2, 2, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
         return launch<128, 128, 2, 2, true, true, false, 2, OP_P2, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
     }
-    if (!E.out8) {
+    {  // the halo kernel shares fused_epilogue, MXFP8 copy included (BN >= 64)
         const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);
         if (hr != 0) return hr < 0 ? -1 : 0;
     }
@@ -1515,32 +1520,32 @@ __global__ void k_gemm_small(int M, int N, int K, float alpha, const h16 *A, int
 // for every thread of that row (one cached line). Same arithmetic and order as
 // k_gemm_small: s = sum_k a*b in fp32, v = alpha * s (+ beta * C), one RNE store.
 constexpr int kSmallK = 8;
+template <int KS>
 __global__ __launch_bounds__(256) void k_gemm_smallk_v8(int M, int ncv, int K, long long R, float alpha,
                                                         const h16 *A, int lda, const h16 *B, int ldb,
                                                         float beta, h16 *C, int ldc) {
     const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= (long long)ncv * R) return;
     const int cv = (int)(g % ncv);
-    float b[kSmallK][8];
+    float b[KS][8];
 #pragma unroll
-    for (int k = 0; k < kSmallK; ++k) {
+    for (int k = 0; k < KS; ++k) {
         if (k < K) {
             const half8 v = *reinterpret_cast<const half8 *>(B + (long long)k * ldb + 8 * cv);
 #pragma unroll
             for (int e = 0; e < 8; ++e) b[k][e] = (float)v[e];
         }
     }
-    // four rows in flight per thread: C's row loads are the HBM stream (AddBias: K = 1)
-    auto row = [&](long long m, const half8 &c0) {
-        float a[kSmallK];
-#pragma unroll
-        for (int k = 0; k < kSmallK; ++k) a[k] = k < K ? h2f(A[m * lda + k]) : 0.f;
+    // four rows in flight per thread (AddBias: K = 1, C's rows are the HBM stream). Every
+    // load of a group is issued before its first store: vmcnt also counts stores, so a load
+    // issued behind a store would wait for that store's acknowledgement.
+    auto row = [&](long long m, const float (&a)[KS], const half8 &c0) {
         half8 out;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
             float s = 0.f;
 #pragma unroll
-            for (int k = 0; k < kSmallK; ++k)
+            for (int k = 0; k < KS; ++k)
                 if (k < K) s += a[k] * b[k][e];
             float v = alpha * s;
             if (beta != 0.f) v += beta * (float)c0[e];
@@ -1548,16 +1553,26 @@ __global__ __launch_bounds__(256) void k_gemm_smallk_v8(int M, int ncv, int K, l
         }
         *reinterpret_cast<half8 *>(C + m * ldc + 8 * cv) = out;
     };
+    auto load = [&](long long m, float (&a)[KS], half8 &c0) {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) a[k] = k < K ? h2f(A[m * lda + k]) : 0.f;
+        c0 = beta != 0.f ? *reinterpret_cast<const half8 *>(C + m * ldc + 8 * cv) : half8{};
+    };
     long long m = g / ncv;
     for (; m + 3 * R < M; m += 4 * R) {
+        float a[4][KS];
         half8 c0[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            c0[u] = beta != 0.f ? *reinterpret_cast<const half8 *>(C + (m + u * R) * ldc + 8 * cv) : half8{};
+        for (int u = 0; u < 4; ++u) load(m + u * R, a[u], c0[u]);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) row(m + u * R, c0[u]);
+        for (int u = 0; u < 4; ++u) row(m + u * R, a[u], c0[u]);
     }
-    for (; m < M; m += R) row(m, beta != 0.f ? *reinterpret_cast<const half8 *>(C + m * ldc + 8 * cv) : half8{});
+    for (; m < M; m += R) {
+        float a[KS];
+        half8 c0;
+        load(m, a, c0);
+        row(m, a, c0);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1570,7 +1585,16 @@ __global__ void k_quant_mxfp8(const h16 *src, long long ld_src, int rows, int co
     const long long total = (long long)rows * nblk;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
-        const int r = (int)(i / nblk), b = (int)(i - (long long)r * nblk);
+        // transposed source (weights): consecutive threads take consecutive rows r, so each
+        // of the 32 loads of a block is one coalesced source row; else consecutive blocks
+        int r, b;
+        if (transpose) {
+            b = (int)(i / rows);
+            r = (int)(i - (long long)b * rows);
+        } else {
+            r = (int)(i / nblk);
+            b = (int)(i - (long long)r * nblk);
+        }
         float v[32];
         float amax = 0.f;
 #pragma unroll
@@ -1592,6 +1616,123 @@ __global__ void k_quant_mxfp8(const h16 *src, long long ld_src, int rows, int co
     }
 }
 
+// Row quantisation on 16-byte vectors (source rows 16-byte aligned, cols % 8 == 0): four
+// lanes per 32-element block, eight elements each, the block's amax by two lane swaps as in
+// the GEMM epilogue's copy, so a wave reads 1 KB of contiguous row bytes per load.
+__global__ __launch_bounds__(256) void k_quant_mxfp8_rows_v8(const h16 *src, long long ld_src, int rows, int cols,
+                                                             int nblk, uint8_t *q, long long ldq, uint8_t *scales,
+                                                             long long lds) {
+    const long long total = (long long)rows * nblk * 4;
+    const long long S = (long long)gridDim.x * blockDim.x;
+    // total is a multiple of 4 and S of 64, so a block's four lanes are live together
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += S) {
+        const long long rb = i >> 2;
+        const int r = (int)(rb / nblk), b = (int)(rb - (long long)r * nblk), c0 = 32 * b + 8 * (int)(i & 3);
+        float v[8];
+        if (c0 < cols) {
+            const half8 x = *reinterpret_cast<const half8 *>(src + (long long)r * ld_src + c0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+        amax = fmaxf(amax, __shfl_xor(amax, 1));
+        amax = fmaxf(amax, __shfl_xor(amax, 2));
+        const int ex = mx_exponent(amax);
+        const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= inv;
+        *reinterpret_cast<uint2 *>(q + (long long)r * ldq + c0) = pack_e4m3x8(v);
+        if ((i & 3) == 0) scales[(long long)r * lds + b] = (uint8_t)(ex + 127);
+    }
+}
+
+// Weight quantisation of many matrices in one launch (kf_quant_mxfp8_batch): job j owns
+// threads [t0[j], t0[j+1]) of the grid, one per (row, 32-element block), rows fastest.
+struct QuantJobs {
+    KfQuantJob job[KF_QUANT_MAX];
+    long long t0[KF_QUANT_MAX + 1];
+    int n;
+};
+__global__ __launch_bounds__(256) void k_quant_mxfp8_batch(QuantJobs J) {
+    const long long S = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < J.t0[J.n]; i += S) {
+        int j = 0;
+        while (j + 1 < J.n && i >= J.t0[j + 1]) ++j;
+        const KfQuantJob &Q = J.job[j];
+        const long long l = i - J.t0[j];
+        const h16 *src = (const h16 *)Q.src;
+        int r, b;
+        if (Q.transpose) {
+            b = (int)(l / Q.rows);
+            r = (int)(l - (long long)b * Q.rows);
+        } else {
+            const int nblk = (Q.cols + 127) / 128 * 4;
+            r = (int)(l / nblk);
+            b = (int)(l - (long long)r * nblk);
+        }
+        float v[32];
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 32; ++e) {
+            const int c = 32 * b + e;
+            float x = 0.f;
+            if (c < Q.cols) x = h2f(Q.transpose ? src[(long long)c * Q.ld_src + r] : src[(long long)r * Q.ld_src + c]);
+            v[e] = x;
+            amax = fmaxf(amax, fabsf(x));
+        }
+        const int ex = mx_exponent(amax);
+        const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
+#pragma unroll
+        for (int e = 0; e < 32; ++e) v[e] *= inv;
+        uint8_t *qr = (uint8_t *)Q.q + (long long)r * Q.ldq + 32 * b;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) *reinterpret_cast<uint2 *>(qr + 8 * w) = pack_e4m3x8(v + 8 * w);
+        Q.scales[(long long)r * Q.lds + b] = (uint8_t)(ex + 127);
+    }
+}
+
+static bool quant_args_ok(const void *src, int rows, int cols, const void *q, long long ldq, const uint8_t *scales,
+                          long long lds) {
+    const int cols_pad = (cols + 127) / 128 * 128;
+    return src && q && scales && ldq >= cols_pad && ldq % 16 == 0 && lds >= cols_pad / 32 && !((uintptr_t)q & 7);
+}
+
+extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
+    if (n < 0 || n > KF_QUANT_MAX || (n && !jobs)) {
+        kf_set_error("kf_quant_mxfp8_batch: %d jobs (at most %d)", n, KF_QUANT_MAX);
+        return -1;
+    }
+    QuantJobs J{};
+    long long tot = 0;
+    for (int j = 0; j < n; ++j) {
+        const KfQuantJob &Q = jobs[j];
+        if (Q.rows < 0 || Q.cols < 0 || ((Q.rows && Q.cols) && !quant_args_ok(Q.src, Q.rows, Q.cols, Q.q, Q.ldq,
+                                                                                Q.scales, Q.lds))) {
+            kf_set_error("kf_quant_mxfp8_batch: bad job %d (rows=%d cols=%d ldq=%lld lds=%lld)", j, Q.rows, Q.cols,
+                         Q.ldq, Q.lds);
+            return -1;
+        }
+        J.job[j] = Q;
+        J.t0[j] = tot;
+        tot += (long long)Q.rows * ((Q.cols + 127) / 128 * 4);
+    }
+    J.t0[n] = tot;
+    J.n = n;
+    if (tot == 0) return 0;
+    k_quant_mxfp8_batch<<<kf_blocks(tot, 256, 16384), 256, 0, kf_stream()>>>(J);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        kf_set_error("kf_quant_mxfp8_batch: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
 extern "C" int kf_quant_mxfp8(const void *src, long long ld_src, int rows, int cols, int transpose,
                               void *q, long long ldq, uint8_t *scales, long long lds) {
     if (rows <= 0 || cols <= 0) return 0;
@@ -1603,8 +1744,12 @@ extern "C" int kf_quant_mxfp8(const void *src, long long ld_src, int rows, int c
         return -1;
     }
     const long long total = (long long)rows * (cols_pad / 32);
-    k_quant_mxfp8<<<kf_blocks(total, 256, 16384), 256, 0, kf_stream()>>>(
-        (const h16 *)src, ld_src, rows, cols, cols_pad, transpose, (uint8_t *)q, ldq, scales, lds);
+    if (!transpose && cols % 8 == 0 && ld_src % 8 == 0 && !((uintptr_t)src & 15))
+        k_quant_mxfp8_rows_v8<<<kf_blocks(4 * total, 256, 16384), 256, 0, kf_stream()>>>(
+            (const h16 *)src, ld_src, rows, cols, cols_pad / 32, (uint8_t *)q, ldq, scales, lds);
+    else
+        k_quant_mxfp8<<<kf_blocks(total, 256, 16384), 256, 0, kf_stream()>>>(
+            (const h16 *)src, ld_src, rows, cols, cols_pad, transpose, (uint8_t *)q, ldq, scales, lds);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         kf_set_error("kf_quant_mxfp8: %s", hipGetErrorString(e));
@@ -1629,11 +1774,16 @@ int kf_ops_gemm_impl(int M, int N, int K, float alpha, const void *A, int lda, c
                             !(((uintptr_t)B | (uintptr_t)C) & 15);
     if (smallk_vec) {
         const int ncv = N / 8;
-        long long R = 262144 / ncv;
+        long long R = 524288 / ncv;
         if (R < 1) R = 1;
         if (R > M) R = M;
-        k_gemm_smallk_v8<<<(unsigned)((ncv * R + 255) / 256), 256, 0, kf_stream()>>>(
-            M, ncv, K, R, alpha, (const h16 *)A, lda, (const h16 *)B, ldb, beta, (h16 *)C, ldc);
+        const unsigned grid = (unsigned)((ncv * R + 255) / 256);
+        if (K == 1)  // AddBias (ops.go:335-351): one column of B in registers
+            k_gemm_smallk_v8<1><<<grid, 256, 0, kf_stream()>>>(M, ncv, K, R, alpha, (const h16 *)A, lda,
+                                                                (const h16 *)B, ldb, beta, (h16 *)C, ldc);
+        else
+            k_gemm_smallk_v8<kSmallK><<<grid, 256, 0, kf_stream()>>>(M, ncv, K, R, alpha, (const h16 *)A, lda,
+                                                                      (const h16 *)B, ldb, beta, (h16 *)C, ldc);
     } else if (!fast || K == 0) {
         k_gemm_small<<<kf_blocks((long long)M * N, 256, 8192), 256, 0, kf_stream()>>>(
             M, N, K, alpha, (const h16 *)A, lda, (const h16 *)B, ldb, beta, (h16 *)C, ldc);

@@ -124,7 +124,7 @@ struct RowVec {
     long long R;  // row stride of the walk (threads = ncv * R)
 };
 static inline RowVec rowvec_plan(long long rows, int ncv, int &blocks) {
-    long long R = 262144 / ncv;  // ~256K threads in flight
+    long long R = 262144 / ncv;  // ~256K threads in flight, four 16-byte loads each
     if (R < 1) R = 1;
     if (R > rows) R = rows;
     blocks = (int)((ncv * R + 255) / 256);

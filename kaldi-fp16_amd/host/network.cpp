@@ -914,8 +914,10 @@ bool mx_alloc(KfNet *net, Mx &m, size_t rows, int width) {
     bridge_gpu_memset(m.s, 0, rows * (m.ld / 32) + 64);
     return true;
 }
-// W [nparts*rows x N] fp16 -> Mx [N x nparts*pad128(rows)]
-bool mx_weights(KfNet *net, Mx &m, int pi, int nparts, int rows, int N, bool alloc) {
+// W [nparts*rows x N] fp16 -> Mx [N x nparts*pad128(rows)]: one quantisation job per part
+// (run together by quantise_weights)
+bool mx_weights(KfNet *net, Mx &m, int pi, int nparts, int rows, int N, bool alloc,
+                std::vector<KfQuantJob> &jobs) {
     const int part = pad128(rows);
     if (alloc) {
         m.ld = nparts * part;
@@ -925,17 +927,22 @@ bool mx_weights(KfNet *net, Mx &m, int pi, int nparts, int rows, int N, bool all
     }
     const uint16_t *W = (const uint16_t *)wptr(net, pi);
     for (int p = 0; p < nparts; ++p)
-        if (!ck(kf_quant_mxfp8(W + (size_t)p * rows * N, N, N, rows, 1, m.q + p * part, m.ld,
-                               m.s + p * part / 32, m.ld / 32),
-                "quantise weights"))
-            return false;
+        jobs.push_back(KfQuantJob{W + (size_t)p * rows * N, N, N, rows, 1, m.q + p * part, m.ld, m.s + p * part / 32,
+                                  m.ld / 32});
     return true;
 }
 // the layer's output can carry an MXFP8 copy (its epilogue has 32-column blocks)
-bool f8_producer(const NetLayer &nl) {
+bool f8_producer(const KfNet *net, int idx) {
+    const NetLayer &nl = net->layers[idx];
     const Layer &L = nl.L;
-    // conv: the epilogue's [(t,h) x fout] view must be the consumer's [t x hout*fout]
-    if (L.type == LayerType::ConvReluBN) return L.fin != 1 && L.fout % 32 == 0 && L.out_dim % 128 == 0;
+    // conv: the epilogue's [(t,h) x fout] view must be the consumer's [t x hout*fout], and
+    // only a non-conv consumer reads the copy (a conv's input is the fp16 halo image)
+    if (L.type == LayerType::ConvReluBN) {
+        bool mx_consumer = false;
+        for (const auto &c : net->layers)
+            mx_consumer = mx_consumer || (c.input == idx && c.L.type != LayerType::ConvReluBN);
+        return mx_consumer && L.fin != 1 && L.fout % 32 == 0 && L.out_dim % 128 == 0;
+    }
     return L.type == LayerType::TDNNF || L.type == LayerType::Linear ||
            (L.type == LayerType::Prefinal && L.small_dim % 32 == 0);
 }
@@ -978,29 +985,34 @@ static const Mx *in8(KfNet *net, const NetLayer &nl) {
 }
 
 static bool quantise_weights(KfNet *net, bool alloc) {
+    std::vector<KfQuantJob> jobs;
     for (auto &nl : net->layers) {
         const Layer &L = nl.L;
         bool ok = true;
         switch (L.type) {
             case LayerType::TDNNF: {
                 const int np = L.time_stride > 0 ? 2 : 1;
-                ok = mx_weights(net, nl.w8, nl.pW, np, L.in_dim, L.bottleneck, alloc) &&
-                     mx_weights(net, nl.w8b, nl.pW2, np, L.bottleneck, L.out_dim, alloc);
+                ok = mx_weights(net, nl.w8, nl.pW, np, L.in_dim, L.bottleneck, alloc, jobs) &&
+                     mx_weights(net, nl.w8b, nl.pW2, np, L.bottleneck, L.out_dim, alloc, jobs);
                 break;
             }
             case LayerType::Linear:
             case LayerType::Output:
-                ok = mx_weights(net, nl.w8, nl.pW, 1, L.in_dim, L.out_dim, alloc);
+                ok = mx_weights(net, nl.w8, nl.pW, 1, L.in_dim, L.out_dim, alloc, jobs);
                 break;
             case LayerType::Prefinal:
-                ok = mx_weights(net, nl.w8, nl.pW, 1, L.in_dim, L.big_dim, alloc) &&
-                     mx_weights(net, nl.w8b, nl.pW2, 1, L.big_dim, L.small_dim, alloc);
+                ok = mx_weights(net, nl.w8, nl.pW, 1, L.in_dim, L.big_dim, alloc, jobs) &&
+                     mx_weights(net, nl.w8b, nl.pW2, 1, L.big_dim, L.small_dim, alloc, jobs);
                 break;
             default:
                 break;
         }
         if (!ok) return false;
     }
+    for (size_t j = 0; j < jobs.size(); j += KF_QUANT_MAX)
+        if (!ck(kf_quant_mxfp8_batch((int)std::min<size_t>(KF_QUANT_MAX, jobs.size() - j), jobs.data() + j),
+                "quantise weights"))
+            return false;
     return true;
 }
 
@@ -1014,9 +1026,10 @@ extern "C" int nnet_set_fp8(KfNet *net, int on) {
         const size_t T = (size_t)net->max_T;
         bool first = true;
         for (auto &nl : net->layers) first = first && !nl.w8.q;
-        for (auto &nl : net->layers) {
+        for (size_t i = 0; i < net->layers.size(); ++i) {
+            NetLayer &nl = net->layers[i];
             const Layer &L = nl.L;
-            if (first && f8_producer(nl) && !mx_alloc(net, nl.a8, T, L.out_dim)) {
+            if (first && f8_producer(net, (int)i) && !mx_alloc(net, nl.a8, T, L.out_dim)) {
                 set_err("fp8: alloc " + L.name);
                 return -1;
             }
@@ -1202,8 +1215,15 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 KfEpilogue E = epi0();
                 E.out = nl.aux;
                 E.ldo = bn;
-                if (net->fp8) set_out8(E, nl.x8);
+                // the bottleneck's MXFP8 copy is quantised after the GEMM rather than in its
+                // epilogue: out8 needs 32-column blocks inside one wave's tile, which would
+                // force 256x256 tiles onto N = bottleneck (320 of 512 columns used) instead of
+                // 384x160 (3072 model: 331 -> see DESIGN §7)
                 if (!ck(kf_gemm_fused(T, bn, x8 ? nl.w8.ld : klin, &A, &B, &E), "tdnnf linear")) return -1;
+                if (net->fp8 && nl.x8.q &&
+                    !ck(kf_quant_mxfp8(nl.aux, bn, T, bn, 0, nl.x8.q, nl.x8.ld, nl.x8.s, nl.x8.ld / 32),
+                        "quantise bottleneck"))
+                    return -1;
                 const bool f8b = net->fp8 && nl.x8.q;
                 KfOperand A2 = f8b ? op_mx(nl.x8, T, np, 0, s)
                                    : s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 1)

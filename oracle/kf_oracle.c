@@ -525,8 +525,10 @@ int orc_net_forward(OrcNet *net, const float *features) {
                 float *bott = (float *)xalloc(sizeof(float) * (size_t)T * bn);
                 orc_matmul(T, bn, klin, lin_in, Wl, bott);
                 free(tmp);
-                float *bott8 = MX ? mx_rows_new(bott, T, bn) : NULL;
                 if (mode) orc_round_f16(bott, (long long)T * bn);
+                /* the product quantises the stored fp16 bottleneck (network.cpp: kf_quant_mxfp8
+                   after the linear GEMM), so the copy is taken after the rounding */
+                float *bott8 = MX ? mx_rows_new(bott, T, bn) : NULL;
                 const float *aff_src = MX ? bott8 : bott, *Wa = L->W2;
                 if (MX) Wa = wq2 = mx_cols_new(L->W2, kaff, dout);
                 const float *aff_in = aff_src;

@@ -124,3 +124,36 @@ def test_conv_halo_wgrad(gpu, hin, fin, hout, sub, fout, T):
     # accumulate = 1 adds onto the existing gradient
     kf.check(kf.core.kf_gemm_wgrad(K, fout, M, C.byref(a), C.byref(b), gW.ptr, fout, gb.ptr, 1))
     _check(kf.read_f32(gW.ptr, (K, fout)), 2 * (P.T @ dz.astype(np.float64)), M)
+
+
+@pytest.mark.parametrize("hin,fin,hout,sub,fout,T", [SHAPES[0], SHAPES[3], SHAPES[4]])
+def test_conv_halo_out8_bit_exact(gpu, hin, fin, hout, sub, fout, T):
+    """The MXFP8 copy of a conv output (the [(t, h) x fout] rows the TDNN-F above reads as
+    [t x hout * fout], network.cpp) written by the halo kernel's epilogue: small-integer
+    inputs and weights keep every output exact in fp16 and fp32, so the codes and scales
+    must equal the numpy quantisation of the fp16 output (tests/mx_ref.py)."""
+    from mx_ref import mx_quantize
+    kf = gpu
+    rng = np.random.default_rng(3 * hin + fout + T)
+    x = _h(rng.integers(-1, 2, (T, hin * fin)))
+    W = _h(rng.integers(-1, 2, (9 * fin, fout)) * (rng.random((9 * fin, fout)) < 0.3))
+    dx, dW = kf.upload_fp16(x), kf.upload_fp16(W)
+    M, K = T * hout, 9 * fin
+    out = kf.DeviceBuffer(M * fout * 2)
+    q8, s8 = kf.DeviceBuffer(M * fout), kf.DeviceBuffer(M * fout // 32)
+    kf.core.bridge_gpu_memset(q8.ptr, 0, M * fout)
+    kf.core.bridge_gpu_memset(s8.ptr, 0, M * fout // 32)
+    a = kf.operand(dx.ptr, hin * fin, M, K, 1, nparts=9, part_width=fin, T=T, hout=hout, hsrc=hin,
+                   hmul=sub, hdiv=1, tpolicy=0, dt=[o[0] for o in OFFS], dh=[o[1] for o in OFFS])
+    b = kf.operand(dW.ptr, fout, K, fout, 0)
+    e = kf.KfEpilogue(out=out.ptr, ldo=fout, alpha=1.0, relu=1, out8=q8.ptr, ldo8=fout, scale8=s8.ptr)
+    kf.check(kf.core.kf_gemm_fused(M, fout, K, C.byref(a), C.byref(b), C.byref(e)))
+    kf.sync()
+    ref = np.maximum(im2col(x.astype(np.float64), T, hin, fin, hout, sub, OFFS) @ W.astype(np.float64), 0)
+    got = kf.read_fp16(out.ptr, (M, fout)).astype(np.float32)
+    np.testing.assert_array_equal(got, ref.astype(np.float32))
+    codes = np.frombuffer(kf.read_fp16(q8.ptr, (M * fout // 2,)).tobytes(), np.uint8).reshape(M, fout)
+    scales = np.frombuffer(kf.read_fp16(s8.ptr, (M * fout // 64,)).tobytes(), np.uint8).reshape(M, fout // 32)
+    rq, rs = mx_quantize(got)
+    np.testing.assert_array_equal(codes, rq)
+    np.testing.assert_array_equal(scales, rs)

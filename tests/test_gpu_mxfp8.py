@@ -161,3 +161,41 @@ def test_epilogue_out8_bit_exact(gpu, N):
     np.testing.assert_array_equal(codes[:, :N], rq)
     np.testing.assert_array_equal(scales[:, :N // 32], rs)
     assert not codes[:, N:].any() and not scales[:, N // 32:].any()  # padding untouched
+
+
+class _QuantJob(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("ld_src", C.c_longlong), ("rows", C.c_int), ("cols", C.c_int),
+                ("transpose", C.c_int), ("q", C.c_void_p), ("ldq", C.c_longlong), ("scales", C.c_void_p),
+                ("lds", C.c_longlong)]
+
+
+def test_quantiser_batch_matches_single_calls(gpu):
+    """kf_quant_mxfp8_batch (the weight copies after each update, several matrices per
+    launch) writes exactly what one kf_quant_mxfp8 call per job writes, for transposed
+    (weights) and row (activations) jobs of ragged sizes."""
+    kf = gpu
+    rng = np.random.default_rng(11)
+    shapes = [(96, 200, 1), (320, 256, 1), (37, 130, 0), (1, 8, 0), (160, 64, 1)]
+    jobs, refs, keep = [], [], []
+    for rows, cols, tr in shapes:
+        x = h(rng.standard_normal((rows, cols)) * np.exp(rng.uniform(-4, 4, (rows, 1))))
+        src = x.T.copy() if tr else x
+        codes, scales, _ = quant_gpu(kf, src, bool(tr))
+        refs.append((codes, scales))
+        cpad = (cols + 127) // 128 * 128
+        dsrc = kf.upload_fp16(src)
+        q, sc = kf.DeviceBuffer(rows * cpad), kf.DeviceBuffer(rows * cpad // 32)
+        kf.core.bridge_gpu_memset(q.ptr, 0x5A, rows * cpad)
+        keep += [dsrc, q, sc]
+        jobs.append(_QuantJob(dsrc.ptr, src.shape[1], rows, cols, tr, q.ptr, cpad, sc.ptr, cpad // 32))
+    arr = (_QuantJob * len(jobs))(*jobs)
+    kf.core.kf_quant_mxfp8_batch.argtypes = [C.c_int, C.c_void_p]
+    kf.check(kf.core.kf_quant_mxfp8_batch(len(jobs), C.cast(arr, C.c_void_p)), "quant batch")
+    kf.sync()
+    for j, ((rows, cols, tr), (rc, rs)) in enumerate(zip(shapes, refs)):
+        cpad = (cols + 127) // 128 * 128
+        q, sc = keep[3 * j + 1], keep[3 * j + 2]
+        codes = np.frombuffer(kf.read_fp16(q.ptr, (rows * cpad // 2,)).tobytes(), np.uint8).reshape(rows, cpad)
+        scales = np.frombuffer(kf.read_fp16(sc.ptr, (rows * cpad // 64,)).tobytes(), np.uint8).reshape(rows, cpad // 32)
+        np.testing.assert_array_equal(codes, rc)
+        np.testing.assert_array_equal(scales, rs)
