@@ -78,6 +78,8 @@ typedef struct {
  *   if resid: v += resid_alpha * resid[m][n]     (TDNN-F bypass / grad bypass)
  *   out[m][n] = rne_fp16(v)                       (when out != NULL)
  *   if out2: out2[m][n] = rne_fp16(v * scale2[n] * bit(mask_in, m*ldo2+n))
+ *   if out8: MXFP8 copy (kf_quant_mxfp8's rule, 32-column blocks) of the unrounded v, or
+ *            with out8_src = 1 of the unrounded out2 value
  * Masks are bit-packed in the linear element order of the tensor they describe
  * (bit i of byte i/8), so producer and consumer may tile differently.
  */
@@ -100,6 +102,7 @@ typedef struct {
     void *out8;            /* e4m3 [M x ldo8], or NULL */
     long long ldo8;
     uint8_t *scale8;       /* E8M0 [M x ldo8/32] (required with out8) */
+    int out8_src;          /* 0: out8 quantises v (out's value); 1: out2's value (needs out2) */
 } KfEpilogue;
 
 /* current stream for every launch made by this library on the calling thread
@@ -242,11 +245,6 @@ int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
 int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes);
 void kf_prof_reset(void);
 
-/* test / A-B hook: 1 runs the short-K wide-N fused GEMMs (k-contiguous plain or two-part
- * spliced A, plain k-contiguous B, 128 < K <= 640, N % 128 == 0, >= 1024 tiles, beta 0, no
- * MXFP8 copy) on the persistent kernel with store waves; 0 (default) on the tiled kernel.
- * Returns the previous setting. */
-int kf_gemm_debug_persist(int on);
 /* test hook: the fused GEMM's K-step interleave of a two-part spliced A with parts of
  * >= 512 columns (the TDNN-F linear forward / affine input gradient). 1 (default):
  * the K-steps alternate between the parts; 0: part order. Only the fp32 accumulation

@@ -1231,7 +1231,6 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     return 0;
 }
 
-int kf_gemm_persist_try(int M, int N, int K, const OpD &a, const OpD &b, int am, int bm, const KfEpilogue &E);
 
 // K-step interleave of two-part spliced A operands (WgradArgs::kil): 1 = on (default),
 // 0 = part order. Test hook: kf_gemm_debug_kil (kf_ops.h) compares the two orders.
@@ -1256,6 +1255,10 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
     if ((E.out && E.ldo % 8) || (E.out2 && E.ldo2 % 8) || (E.resid && E.ldr % 8) ||
         (E.mask_out && E.ldo % 8)) {
         kf_set_error("kf_gemm_fused: leading dimensions must be multiples of 8");
+        return -1;
+    }
+    if (E.out8 && E.out8_src && !E.out2) {
+        kf_set_error("kf_gemm_fused: out8_src = 1 needs out2");
         return -1;
     }
     if (E.out8 && (N % 32 || E.ldo8 % 32 || !E.scale8)) {
@@ -1294,22 +1297,17 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);
         if (hr != 0) return hr < 0 ? -1 : 0;
     }
-    if (B->kcontig) {  // short K, wide N: the persistent kernel with store waves (gemm_persist.hip)
-        const int pr = kf_gemm_persist_try(M, N, K, a, b, am, bm, E);
-        if (pr != 0) return pr < 0 ? -1 : 0;
-    }
     // Tiles: 384x160 8-wave for N = 160 / 320; 256x64 for N <= 64; for
     // N >= 256 192x128 8-wave tiles (80 KB of LDS: two workgroups share a CU and one's
     // epilogue overlaps the other's MFMA loop; the wide K = 320 products write 2-3
-    // full-width fp16 tensors), 256x256 when the epilogue writes an MXFP8 copy (32-column
-    // blocks inside one wave's tile); 128x128 otherwise.
+    // full-width fp16 tensors; their 32-column wave tiles hold the MXFP8 copy's blocks);
+    // 128x128 otherwise.
     int tile = 0;
     if (N % 160 == 0 && N <= 320 && !E.out8) tile = 5;
     else if (N <= 64) tile = 2;
-    else if (N >= 256) tile = E.out8 ? 3 : 6;
+    else if (N >= 256) tile = 6;  // 192x128: 32-column wave tiles, so out8 blocks fit
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
-        if (tile == 3) return launch<256, 256, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 6) return launch<192, 128, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 5) return launch<384, 160, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 2) return launch<256, 64, 4, 1, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);  \

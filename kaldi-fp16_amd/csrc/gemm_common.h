@@ -380,6 +380,7 @@ __device__ __forceinline__ void epilogue8(const KfEpilogue &E, const EpiCols &P,
             if (E.scale2) w *= P.scale2[nl + e];
             if (E.mask_in && !((mbits >> e) & 1u)) w = 0.f;
             o[e] = f2h(w);
+            if (E.out8_src) v[e] = w;  // the MXFP8 copy after this call quantises out2's value
         }
         store_h8((h16 *)E.out2 + (long long)m * E.ldo2 + n, o);
     }

@@ -573,7 +573,7 @@ int ops_copy(void *dst, const void *src, int count) {
     if (count <= 0) return 0;
     if (count % 8 == 0 && aligned16(dst) && aligned16(src)) {
         const long long n8 = count / 8;
-        k_copy_v8<<<(int)std::min<long long>((n8 + 255) / 256, 1024), 256, 0, kf_stream()>>>((h16 *)dst, (const h16 *)src, n8);
+        k_copy_v8<<<kf_blocks(n8, 256, 8192), 256, 0, kf_stream()>>>((h16 *)dst, (const h16 *)src, n8);
         return ops_check("copy");
     }
     hipError_t e = hipMemcpyAsync(dst, src, (size_t)count * 2, hipMemcpyDeviceToDevice, kf_stream());

@@ -74,8 +74,12 @@ struct NetLayer {
     // MXFP8 forward (nnet_set_fp8): output / aux copies written by the producing
     // GEMM epilogue, and the weights quantised [N][K] with each splice part padded
     Mx a8, x8, w8, w8b;
+    // MXFP8 train step, TDNN-F with a time stride: the affine weight rows for the input
+    // gradient, [bottleneck x 2 * pad128(out_dim)] (part p = rows p*bn .. of W2, blocks of 32
+    // along out_dim), quantised with the forward copies
+    Mx w8d;
     // k-contiguous (transposed) fp16 copy of a short-K forward weight, [N x K], for the
-    // panel GEMM (csrc/panel.hip); refreshed from w16 before a forward after any change
+    // fused GEMM's k-contiguous B; refreshed from w16 before a forward after any change
     void *wt = nullptr;
     int wt_pi = -1, wt_K = 0, wt_N = 0;
 };
@@ -206,6 +210,10 @@ struct KfNet {
     void *dbott = nullptr, *edge = nullptr;
     size_t edge_half = 0;
     int fp8 = 0;
+    // MXFP8 copies of dz[0] / dz[1] written by the producing input-gradient epilogue
+    // (out8_src = 1) for a TDNN-F layer's affine input gradient, and the layer each holds
+    Mx dz8[2];
+    int dz8_layer[2] = {-1, -1};
     bool wt_dirty = true;  // the transposed weight copies need a refresh (NetLayer::wt)
     // data parallel (kf_dp.h): gradient buckets exchanged during the backward
     KfDp *dp = nullptr;
@@ -931,6 +939,23 @@ bool mx_weights(KfNet *net, Mx &m, int pi, int nparts, int rows, int N, bool all
                                   m.ld / 32});
     return true;
 }
+// W2 [2*bn x dout] -> w8d [bn x 2*pad128(dout)]: row j holds W2 rows j and bn + j, each
+// quantised in 32-element blocks along dout (the reduction of the affine input gradient)
+bool mx_dgrad_weights(KfNet *net, NetLayer &nl, bool alloc, std::vector<KfQuantJob> &jobs) {
+    const int bn = nl.L.bottleneck, dout = nl.L.out_dim, part = pad128(dout);
+    Mx &m = nl.w8d;
+    if (alloc) {
+        m.ld = 2 * part;
+        m.q = (uint8_t *)net->dalloc((size_t)bn * m.ld + 64);
+        m.s = (uint8_t *)net->dalloc((size_t)bn * (m.ld / 32) + 64);
+        if (!m.q || !m.s) return false;
+    }
+    const uint16_t *W2 = (const uint16_t *)wptr(net, nl.pW2);
+    for (int p = 0; p < 2; ++p)
+        jobs.push_back(KfQuantJob{W2 + (size_t)p * bn * dout, dout, bn, dout, 0, m.q + p * part, m.ld,
+                                  m.s + p * part / 32, m.ld / 32});
+    return true;
+}
 // the layer's output can carry an MXFP8 copy (its epilogue has 32-column blocks)
 bool f8_producer(const KfNet *net, int idx) {
     const NetLayer &nl = net->layers[idx];
@@ -993,7 +1018,8 @@ static bool quantise_weights(KfNet *net, bool alloc) {
             case LayerType::TDNNF: {
                 const int np = L.time_stride > 0 ? 2 : 1;
                 ok = mx_weights(net, nl.w8, nl.pW, np, L.in_dim, L.bottleneck, alloc, jobs) &&
-                     mx_weights(net, nl.w8b, nl.pW2, np, L.bottleneck, L.out_dim, alloc, jobs);
+                     mx_weights(net, nl.w8b, nl.pW2, np, L.bottleneck, L.out_dim, alloc, jobs) &&
+                     (np == 1 || mx_dgrad_weights(net, nl, alloc, jobs));
                 break;
             }
             case LayerType::Linear:
@@ -1039,6 +1065,15 @@ extern "C" int nnet_set_fp8(KfNet *net, int on) {
                 return -1;
             }
         }
+        // dz copies for the TDNN-F affine input gradients: as wide as the widest such layer
+        int dzw = 0;
+        for (auto &nl : net->layers)
+            if (nl.L.type == LayerType::TDNNF && nl.L.time_stride > 0) dzw = std::max(dzw, nl.L.out_dim);
+        for (int i = 0; first && dzw > 0 && i < 2; ++i)
+            if (!mx_alloc(net, net->dz8[i], T, dzw)) {
+                set_err("fp8: alloc dz copies");
+                return -1;
+            }
         if (!quantise_weights(net, first)) return -1;
     }
     net->fp8 = 1;
@@ -1364,14 +1399,24 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
     E.ldo2 = w;
     E.out2 = dz_out;
     switch (L.type) {
-        case LayerType::TDNNF:
+        case LayerType::TDNNF: {
             E.scale2 = pl.bn_scale;
             E.mask_in = pl.mask;
             if (pl.bypass) {
                 E.out = g_out;
                 E.ldo = w;
             }
+            // MXFP8 train step: also the e4m3 copy of dz_P for P's affine input gradient
+            const int i = dz_out == net->dz[0] ? 0 : dz_out == net->dz[1] ? 1 : -1;
+            if (net->fp8 && i >= 0 && w % 32 == 0 && pl.w8d.q && net->dz8[i].q && net->dz8[i].ld == pad128(w)) {
+                E.out8 = net->dz8[i].q;
+                E.ldo8 = net->dz8[i].ld;
+                E.scale8 = net->dz8[i].s;
+                E.out8_src = 1;
+                net->dz8_layer[i] = P;
+            }
             return true;
+        }
         case LayerType::ConvReluBN:
         case LayerType::Attention:
             E.scale2 = pl.bn_scale;
@@ -1457,6 +1502,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         const void *x = act_of(net, nl.input);
         bool want_dx = nl.needs_dx && nl.input >= 0;
         void *dz_next = net->dz[flip], *g_next = net->g[flip];
+        net->dz8_layer[flip] = -1;
         KfEpilogue E;
         if (want_dx && !dx_epilogue(net, nl.input, dz_next, g_next, E)) return -1;
         if (nl.bypass) {
@@ -1543,17 +1589,45 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 KfEpilogue E1 = epi0();
                 E1.out = dbott;
                 E1.ldo = bn;
+                const int i8 = dz == net->dz[0] ? 0 : dz == net->dz[1] ? 1 : -1;
                 if (s > 0) {
                     // spare row T of dz holds sum_{t >= T-1-s} dz[t] (clamped-splice transpose)
                     void *edge = (char *)dz + (size_t)T * dout * 2;
                     if (!ck(kf_rows_sum(edge, dz, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout), "edge"))
                         return -1;
-                    KfOperand A1 = op_splice(dz, T, dout, 0, -s, KF_ZERO, 1);
-                    A1.edge_t[1] = T - 1;
-                    A1.edge_row[1] = T;
                     KfOperand B1 = op_wrows(wptr(net, nl.pW2), 2, bn, dout);
-                    if (!ck(kf_gemm_fused(T, bn, 2 * dout, &A1, &B1, &E1), "tdnnf affine dgrad"))
-                        return -1;
+                    if (net->fp8 && i8 >= 0 && net->dz8_layer[i8] == li && T > 1) {
+                        // MXFP8 (the one MFMA-bound backward product, K = 2 x dout): rows
+                        // 0 .. T-2 from dz's e4m3 copy [dz(t) | dz(t-s)] against the e4m3
+                        // weight rows; row T-1, whose second part is the clamped-edge sum,
+                        // again in fp16 below (the MXFP8 operand has no edge rows)
+                        const Mx &d8 = net->dz8[i8];
+                        const int pw = pad128(dout);
+                        KfOperand A1 = op_base(d8.q, d8.ld, T, 2 * pw, 1);
+                        A1.nparts = 2;
+                        A1.part_width = pw;
+                        A1.dt[1] = -s;
+                        A1.tpolicy = KF_ZERO;
+                        A1.fmt = KF_FMT_MXFP8;
+                        A1.scales = d8.s;
+                        A1.lds = d8.ld / 32;
+                        KfOperand B8 = op_mxw(nl.w8d, bn);
+                        if (!ck(kf_gemm_fused(T, bn, 2 * pw, &A1, &B8, &E1), "tdnnf affine dgrad mxfp8")) return -1;
+                        KfOperand Ae = op_splice((const char *)dz + (size_t)(T - 1) * dout * 2, 1, dout, 0, -s,
+                                                 KF_ZERO, 1);
+                        Ae.edge_t[1] = 0;
+                        Ae.edge_row[1] = 1;
+                        KfEpilogue Ee = E1;
+                        Ee.out = (char *)dbott + (size_t)(T - 1) * bn * 2;
+                        if (!ck(kf_gemm_fused(1, bn, 2 * dout, &Ae, &B1, &Ee), "tdnnf affine dgrad edge row"))
+                            return -1;
+                    } else {
+                        KfOperand A1 = op_splice(dz, T, dout, 0, -s, KF_ZERO, 1);
+                        A1.edge_t[1] = T - 1;
+                        A1.edge_row[1] = T;
+                        if (!ck(kf_gemm_fused(T, bn, 2 * dout, &A1, &B1, &E1), "tdnnf affine dgrad"))
+                            return -1;
+                    }
                 } else {
                     KfOperand A1 = op_base(dz, dout, T, dout, 1);
                     KfOperand B1 = op_base(wptr(net, nl.pW2), dout, bn, dout, 1);

@@ -410,7 +410,7 @@ class KfEpilogue(C.Structure):
     _fields_ = [("out", _vp), ("ldo", _ll), ("alpha", _f), ("beta", _f), ("bias", _vp), ("relu", _i),
                 ("mask_out", _vp), ("scale", _vp), ("shift", _vp), ("resid", _vp), ("ldr", _ll),
                 ("resid_alpha", _f), ("out2", _vp), ("ldo2", _ll), ("scale2", _vp), ("mask_in", _vp),
-                ("out8", _vp), ("ldo8", _ll), ("scale8", _vp)]
+                ("out8", _vp), ("ldo8", _ll), ("scale8", _vp), ("out8_src", _i)]
 
 
 def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, hout=1, hsrc=1,
@@ -439,6 +439,5 @@ _sig(core, "kf_gemm_fused", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOp
 _sig(core, "kf_gemm_wgrad", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i)
 _sig(core, "kf_rows_sum", _i, _vp, _vp, _ll, _i, _i, _i)
 _sig(core, "kf_gemm_debug_kil", None, _i)
-_sig(core, "kf_gemm_debug_persist", _i, _i)
 _sig(core, "kf_gemm_trace", None, _vp, _i, _i)
 _sig(core, "kf_quant_mxfp8", _i, _vp, _ll, _i, _i, _i, _vp, _ll, _vp, _ll)

@@ -640,6 +640,19 @@ static float *colsum(const float *g, int rows, int D) {
     return s;
 }
 
+/* the layers whose affine input gradient the MXFP8 train step runs in e4m3: strided
+   TDNN-F layers with out_dim % 32 == 0 and as wide (padded to 128) as the widest strided
+   TDNN-F layer (network.cpp: the dz copies are allocated that wide) */
+static int mx_dgrad_layer(const OrcNet *net, int li) {
+    const OrcLayer *L = &net->layers[li];
+    if (L->type != ORC_TDNNF || L->stride <= 0 || L->out_dim % 32) return 0;
+    int w = 0;
+    for (int j = 0; j < net->nlayers; ++j)
+        if (net->layers[j].type == ORC_TDNNF && net->layers[j].stride > 0 && net->layers[j].out_dim > w)
+            w = net->layers[j].out_dim;
+    return (L->out_dim + 127) / 128 == (w + 127) / 128;
+}
+
 /*
  * Exact backward. v[li] is the fp32 (unrounded) gradient w.r.t. layer li's
  * output; the MI355X build stores g = rne(v) and dz = rne(v * bnscale * mask),
@@ -735,6 +748,11 @@ int orc_net_backward_top(OrcNet *net, const float *features, const float *out_gr
                     int d = (int)(i % dout);
                     dz[i] = net->mask[li][i] ? g[i] * bn_scale(&L->bn, d) : 0.f;
                 }
+                /* MXFP8 train step (network.cpp backward_impl): the affine input gradient of a
+                   strided layer reads the e4m3 copy of the unrounded dz and of W2's rows, except
+                   for row T-1 (the clamped-edge row), which stays fp16 */
+                float *dz8 = NULL;
+                if (net->mx8 && s > 0 && T > 1 && mx_dgrad_layer(net, li)) dz8 = mx_rows_new(dz, T, dout);
                 if (mode) orc_round_f16(dz, (long long)T * dout);
                 const float *bott = net->aux[li];
                 const int kaff = s > 0 ? 2 * bn : bn, klin = s > 0 ? 2 * din : din;
@@ -745,15 +763,27 @@ int orc_net_backward_top(OrcNet *net, const float *features, const float *out_gr
                 net->gb2[li] = colsum(dz, T, dout);
                 float *daff = (float *)xalloc(sizeof(float) * (size_t)T * kaff);
                 matmul_nt(T, kaff, dout, dz, L->W2, daff);
+                float *daff8 = daff;
+                if (dz8) {
+                    float *w8 = mx_rows_new(L->W2, kaff, dout);
+                    daff8 = (float *)xalloc(sizeof(float) * (size_t)T * kaff);
+                    matmul_nt(T, kaff, dout, dz8, w8, daff8);
+                    free(w8);
+                    free(dz8);
+                }
                 float *dbott = (float *)xalloc(sizeof(float) * (size_t)T * bn);
-                for (int t = 0; t < T; ++t)
-                    for (int c = 0; c < bn; ++c) dbott[(size_t)t * bn + c] += daff[(size_t)t * kaff + c];
+                for (int t = 0; t < T; ++t) {
+                    const float *da = t == T - 1 ? daff : daff8;
+                    for (int c = 0; c < bn; ++c) dbott[(size_t)t * bn + c] += da[(size_t)t * kaff + c];
+                }
                 if (s > 0)
                     for (int t = 0; t < T; ++t) {
                         int tp = t + s > T - 1 ? T - 1 : t + s;
+                        const float *da = tp == T - 1 ? daff : daff8;
                         for (int c = 0; c < bn; ++c)
-                            dbott[(size_t)tp * bn + c] += daff[(size_t)t * kaff + bn + c];
+                            dbott[(size_t)tp * bn + c] += da[(size_t)t * kaff + bn + c];
                     }
+                if (daff8 != daff) free(daff8);
                 free(daff);
                 if (mode) orc_round_f16(dbott, (long long)T * bn);
                 float *lin_in = s > 0 ? splice_minus(x, T, din, s) : (float *)x;
