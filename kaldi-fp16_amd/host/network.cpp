@@ -1465,12 +1465,21 @@ extern "C" const void *nnet_debug_tensor(KfNet *net, const char *what, int layer
     if (w == "g0") return net->g[0];
     if (w == "g1") return net->g[1];
     if (w == "dbott") return net->dbott;
+    // the MXFP8 copies of dz[layer] (layer = buffer 0 / 1) and the layer whose affine input
+    // gradient reads it (as an int, through the pointer's low bits: -1 none), MXFP8 train step
+    if ((w == "dz8q" || w == "dz8s" || w == "dz8layer") && (layer == 0 || layer == 1)) {
+        if (w == "dz8layer") return (const void *)(intptr_t)(net->dz8_layer[layer] + 1);
+        return w == "dz8q" ? (const void *)net->dz8[layer].q : (const void *)net->dz8[layer].s;
+    }
     if (layer < 0 || layer >= (int)net->layers.size()) return nullptr;
     if (w == "aux") return net->layers[layer].aux;
     if (w == "dproj") return net->layers[layer].dproj;
     if (w == "mask") return net->layers[layer].mask;
     if (w == "bn_scale") return net->layers[layer].bn_scale;
     if (w == "bn2_scale") return net->layers[layer].bn2_scale;
+    // the e4m3 affine weight rows of the MXFP8 input gradient, [bn x 2*pad128(out)]
+    if (w == "w8dq") return net->layers[layer].w8d.q;
+    if (w == "w8ds") return net->layers[layer].w8d.s;
     // the MXFP8 copy this layer's GEMM reads (e4m3 [T x pad128(in)], E8M0 [T x pad128(in)/32])
     if (w == "x8q" || w == "x8s") {
         const Mx *m = in8(net, net->layers[layer]);
