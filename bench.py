@@ -571,10 +571,18 @@ def main():
         r, _ = run_workload(a, "cnn_tdnn_17f.xconfig", "forward", False, rank, world, None, ks, kw, prof_on)
         extra["configs[1]_forward_1536"] = dict(
             workload="cnn_tdnn_17f forward only, fp16", **describe(r, a, world, "forward", False, "", PEAK_FP16_TFLOPS))
+        r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "train", False, rank, world, None, ks, kw, prof_on)
+        extra["configs[4]_train_3072_fp16"] = dict(
+            workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), fp16 (the MXFP8 step's reference point)",
+            **describe(r, a, world, "train", False, "", PEAK_FP16_TFLOPS))
+        ms16 = extra["configs[4]_train_3072_fp16"]["ms_per_step"]
         r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "train", True, rank, world, None, ks, kw, prof_on)
         extra["configs[4]_train_3072_mxfp8"] = dict(
-            workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), MXFP8 forward GEMMs, fp16 backward",
+            workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD): MXFP8 forward GEMMs and strided TDNN-F "
+                     "affine input gradients, the rest fp16",
             **describe(r, a, world, "train", True, "", PEAK_FP8_TFLOPS))
+        m8 = extra["configs[4]_train_3072_mxfp8"]
+        m8["speedup_vs_fp16_step"] = round(ms16 / m8["ms_per_step"], 4) if m8.get("ms_per_step") else None
         r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "forward", True, rank, world, None, ks, kw, prof_on)
         extra["configs[4]_forward_3072_mxfp8"] = dict(
             workload="cnn_tdnn_17f_3072 forward only, MXFP8 GEMMs",

@@ -150,6 +150,11 @@ typedef struct KfQuantJob {
 } KfQuantJob;
 int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs);
 
+/* out[j] = rne_fp16(sum_c x0[c] W[j][c] + x1[c] W[rows + j][c]), j < rows, W [2*rows x cols]
+ * fp16 row-major, fp32 accumulation; cols % 8 == 0, 16-byte aligned pointers (out is not
+ * required to be: it is written per element). One row of a two-part product. */
+int kf_dot2_rows(void *out, const void *x0, const void *x1, const void *W, int rows, int cols);
+
 /* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols
  * (edge may be a spare row of src's own allocation) */
 int kf_rows_sum(void *edge, const void *src, long long ld, int r0, int r1, int cols);

@@ -1461,6 +1461,44 @@ extern "C" int kf_rows_sum(void *edge, const void *src, long long ld, int r0, in
     return 0;
 }
 
+// out[j] = rne_fp16(x0 . W[j] + x1 . W[rows + j]) for j < rows (W [2*rows x cols], fp32
+// accumulation): one row of a two-part product, e.g. the clamped-edge row T-1 of the MXFP8
+// affine input gradient (network.cpp). A workgroup per output element: a one-row GEMM would
+// walk K on two workgroups.
+__global__ __launch_bounds__(256) void k_dot2_rows(h16 *out, const h16 *x0, const h16 *x1, const h16 *W, int rows,
+                                                   int cols) {
+    __shared__ float part[4];
+    const int j = blockIdx.x;
+    const h16 *w0 = W + (long long)j * cols, *w1 = W + (long long)(rows + j) * cols;
+    float acc = 0.f;
+    for (int c = 8 * threadIdx.x; c < cols; c += 8 * blockDim.x) {
+        const half8 a = load_h8(x0 + c), b = load_h8(x1 + c), u = load_h8(w0 + c), v = load_h8(w1 + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc = fmaf((float)a[e], (float)u[e], fmaf((float)b[e], (float)v[e], acc));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) out[j] = f2h(part[0] + part[1] + part[2] + part[3]);
+}
+
+extern "C" int kf_dot2_rows(void *out, const void *x0, const void *x1, const void *W, int rows, int cols) {
+    if (rows <= 0) return 0;
+    if (cols % 8 || ((uintptr_t)x0 | (uintptr_t)x1 | (uintptr_t)W) & 15) {
+        kf_set_error("kf_dot2_rows: cols %% 8 and 16-byte aligned operands required (cols=%d)", cols);
+        return -1;
+    }
+    k_dot2_rows<<<rows, 256, 0, kf_stream()>>>((h16 *)out, (const h16 *)x0, (const h16 *)x1, (const h16 *)W, rows,
+                                              cols);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        kf_set_error("kf_dot2_rows: %s", hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
 // helpers for plain operands (used by the ABI GEMM below and by the host layer)
 static KfOperand plain_operand(const void *p, long long ld, int rows, int cols, int kcontig) {
     KfOperand d;
@@ -1694,6 +1732,62 @@ __global__ __launch_bounds__(256) void k_quant_mxfp8_batch(QuantJobs J) {
     }
 }
 
+// Transposed jobs (weights W[K][N] -> W8[N][K]) through LDS: a workgroup owns 64 output rows
+// r (source columns) x 256 k (8 blocks): the source tile is read as 256 row segments of 128
+// bytes, and each output row's 256 bytes are written by 32 consecutive lanes (4 per block,
+// the block amax by two lane swaps), so both sides are coalesced.
+struct QuantTJobs {
+    KfQuantJob job[KF_QUANT_MAX];
+    int wg0[KF_QUANT_MAX + 1];  // first workgroup of each job
+    int rt[KF_QUANT_MAX];       // 64-row tiles of each job
+    int n;
+};
+__global__ __launch_bounds__(256) void k_quant_mxfp8_tbatch(QuantTJobs J) {
+    __shared__ float tile[256][65];
+    int j = 0;
+    while (j + 1 < J.n && (int)blockIdx.x >= J.wg0[j + 1]) ++j;
+    const KfQuantJob &Q = J.job[j];
+    const int w = blockIdx.x - J.wg0[j];
+    const int r0 = (w % J.rt[j]) * 64, k0 = (w / J.rt[j]) * 256;
+    const h16 *src = (const h16 *)Q.src;
+    // 2048 16-byte source vectors (8 per 64-row tile row), all loads issued before the LDS
+    // writes (rows % 8 == 0, ld_src % 8 == 0, 16-byte aligned source: host-checked)
+    half8 xs[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int i = threadIdx.x + 256 * u, k = k0 + (i >> 3), r = r0 + 8 * (i & 7);
+        xs[u] = (k < Q.cols && r < Q.rows) ? load_h8(src + (long long)k * Q.ld_src + r) : half8{};
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int i = threadIdx.x + 256 * u, kk = i >> 3, rr = 8 * (i & 7);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tile[kk][rr + e] = (float)xs[u][e];
+    }
+    __syncthreads();
+    const int kpad = (Q.cols + 127) / 128 * 128;
+    for (int i = threadIdx.x; i < 64 * 32; i += 256) {  // i = output row * 32 + block * 4 + quarter
+        const int rr = i >> 5, b = (i >> 2) & 7, qq = i & 3, r = r0 + rr, c0 = 32 * b + 8 * qq;
+        float v[8];
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            v[e] = tile[c0 + e][rr];
+            amax = fmaxf(amax, fabsf(v[e]));
+        }
+        amax = fmaxf(amax, __shfl_xor(amax, 1));
+        amax = fmaxf(amax, __shfl_xor(amax, 2));
+        const int ex = mx_exponent(amax);
+        const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= inv;
+        if (r < Q.rows && k0 + c0 < kpad) {
+            *reinterpret_cast<uint2 *>((uint8_t *)Q.q + (long long)r * Q.ldq + k0 + c0) = pack_e4m3x8(v);
+            if (qq == 0) Q.scales[(long long)r * Q.lds + (k0 >> 5) + b] = (uint8_t)(ex + 127);
+        }
+    }
+}
+
 static bool quant_args_ok(const void *src, int rows, int cols, const void *q, long long ldq, const uint8_t *scales,
                           long long lds) {
     const int cols_pad = (cols + 127) / 128 * 128;
@@ -1706,7 +1800,9 @@ extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
         return -1;
     }
     QuantJobs J{};
+    QuantTJobs TJ{};
     long long tot = 0;
+    int twg = 0;
     for (int j = 0; j < n; ++j) {
         const KfQuantJob &Q = jobs[j];
         if (Q.rows < 0 || Q.cols < 0 || ((Q.rows && Q.cols) && !quant_args_ok(Q.src, Q.rows, Q.cols, Q.q, Q.ldq,
@@ -1715,14 +1811,25 @@ extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
                          Q.ldq, Q.lds);
             return -1;
         }
-        J.job[j] = Q;
-        J.t0[j] = tot;
-        tot += (long long)Q.rows * ((Q.cols + 127) / 128 * 4);
+        if (!Q.rows || !Q.cols) continue;
+        if (Q.transpose && Q.rows % 8 == 0 && Q.ld_src % 8 == 0 && !((uintptr_t)Q.src & 15)) {
+            // LDS-tiled: 64 rows x 256 k per workgroup
+            TJ.job[TJ.n] = Q;
+            TJ.wg0[TJ.n] = twg;
+            TJ.rt[TJ.n] = (Q.rows + 63) / 64;
+            twg += TJ.rt[TJ.n] * ((Q.cols + 127) / 128 * 128 + 255) / 256;
+            ++TJ.n;
+        } else {
+            J.job[J.n] = Q;
+            J.t0[J.n] = tot;
+            tot += (long long)Q.rows * ((Q.cols + 127) / 128 * 4);
+            ++J.n;
+        }
     }
-    J.t0[n] = tot;
-    J.n = n;
-    if (tot == 0) return 0;
-    k_quant_mxfp8_batch<<<kf_blocks(tot, 256, 16384), 256, 0, kf_stream()>>>(J);
+    J.t0[J.n] = tot;
+    TJ.wg0[TJ.n] = twg;
+    if (tot > 0) k_quant_mxfp8_batch<<<kf_blocks(tot, 256, 16384), 256, 0, kf_stream()>>>(J);
+    if (twg > 0) k_quant_mxfp8_tbatch<<<twg, 256, 0, kf_stream()>>>(TJ);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         kf_set_error("kf_quant_mxfp8_batch: %s", hipGetErrorString(e));

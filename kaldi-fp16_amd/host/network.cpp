@@ -1622,13 +1622,10 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         A1.lds = d8.ld / 32;
                         KfOperand B8 = op_mxw(nl.w8d, bn);
                         if (!ck(kf_gemm_fused(T, bn, 2 * pw, &A1, &B8, &E1), "tdnnf affine dgrad mxfp8")) return -1;
-                        KfOperand Ae = op_splice((const char *)dz + (size_t)(T - 1) * dout * 2, 1, dout, 0, -s,
-                                                 KF_ZERO, 1);
-                        Ae.edge_t[1] = 0;
-                        Ae.edge_row[1] = 1;
-                        KfEpilogue Ee = E1;
-                        Ee.out = (char *)dbott + (size_t)(T - 1) * bn * 2;
-                        if (!ck(kf_gemm_fused(1, bn, 2 * dout, &Ae, &B1, &Ee), "tdnnf affine dgrad edge row"))
+                        if (!ck(kf_dot2_rows((char *)dbott + (size_t)(T - 1) * bn * 2,
+                                             (const char *)dz + (size_t)(T - 1) * dout * 2, edge,
+                                             wptr(net, nl.pW2), bn, dout),
+                                "tdnnf affine dgrad edge row"))
                             return -1;
                     } else {
                         KfOperand A1 = op_splice(dz, T, dout, 0, -s, KF_ZERO, 1);

@@ -340,7 +340,7 @@ def _isolated_dgrad_errors(kfp16, xcfg, T, seed=3):
         rq, rs = mx_quantize(np.pad(dz[:T].astype(np.float32), ((0, 0), (0, pw - dout))))
         code_agree = float((dzq == rq).mean())
         dbott = kfp16.read_fp16(kfp16.nnet.nnet_debug_tensor(net.h, b"dbott", 0), (T, bn)).astype(np.float64)
-        a0, a1 = dz8[:, :dout], dz8[:, pw:pw + dout]
+        a0 = a1 = dz8[:, :dout]   # both parts read dz's copy: rows t and t - s
         b0, b1 = w8[:, :dout], w8[:, pw:pw + dout]
         ref = a0 @ b0.T
         mag = np.abs(a0) @ np.abs(b0).T
