@@ -1732,6 +1732,41 @@ __global__ __launch_bounds__(256) void k_quant_mxfp8_batch(QuantJobs J) {
     }
 }
 
+// Row jobs on 16-byte vectors (cols % 8 == 0, ld_src % 8 == 0, aligned source: host-checked),
+// as k_quant_mxfp8_rows_v8: four lanes per 32-element block; J.t0 counts lanes
+__global__ __launch_bounds__(256) void k_quant_mxfp8_vbatch(QuantJobs J) {
+    const long long S = (long long)gridDim.x * blockDim.x;
+    // every job's lane count is a multiple of 4 and S of 64: a block's four lanes are live together
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < J.t0[J.n]; i += S) {
+        int j = 0;
+        while (j + 1 < J.n && i >= J.t0[j + 1]) ++j;
+        const KfQuantJob &Q = J.job[j];
+        const long long l = i - J.t0[j], rb = l >> 2;
+        const int nblk = (Q.cols + 127) / 128 * 4;
+        const int r = (int)(rb / nblk), b = (int)(rb - (long long)r * nblk), c0 = 32 * b + 8 * (int)(l & 3);
+        float v[8];
+        if (c0 < Q.cols) {
+            const half8 x = load_h8((const h16 *)Q.src + (long long)r * Q.ld_src + c0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (float)x[e];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        }
+        float amax = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(v[e]));
+        amax = fmaxf(amax, __shfl_xor(amax, 1));
+        amax = fmaxf(amax, __shfl_xor(amax, 2));
+        const int ex = mx_exponent(amax);
+        const float inv = __uint_as_float((unsigned)(127 - ex) << 23);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= inv;
+        *reinterpret_cast<uint2 *>((uint8_t *)Q.q + (long long)r * Q.ldq + c0) = pack_e4m3x8(v);
+        if ((l & 3) == 0) Q.scales[(long long)r * Q.lds + b] = (uint8_t)(ex + 127);
+    }
+}
+
 // Transposed jobs (weights W[K][N] -> W8[N][K]) through LDS: a workgroup owns 64 output rows
 // r (source columns) x 256 k (8 blocks): the source tile is read as 256 row segments of 128
 // bytes, and each output row's 256 bytes are written by 32 consecutive lanes (4 per block,
@@ -1799,9 +1834,9 @@ extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
         kf_set_error("kf_quant_mxfp8_batch: %d jobs (at most %d)", n, KF_QUANT_MAX);
         return -1;
     }
-    QuantJobs J{};
+    QuantJobs J{}, VJ{};
     QuantTJobs TJ{};
-    long long tot = 0;
+    long long tot = 0, vtot = 0;
     int twg = 0;
     for (int j = 0; j < n; ++j) {
         const KfQuantJob &Q = jobs[j];
@@ -1819,6 +1854,11 @@ extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
             TJ.rt[TJ.n] = (Q.rows + 63) / 64;
             twg += TJ.rt[TJ.n] * ((Q.cols + 127) / 128 * 128 + 255) / 256;
             ++TJ.n;
+        } else if (!Q.transpose && Q.cols % 8 == 0 && Q.ld_src % 8 == 0 && !((uintptr_t)Q.src & 15)) {
+            VJ.job[VJ.n] = Q;  // row jobs on 16-byte vectors
+            VJ.t0[VJ.n] = vtot;
+            vtot += (long long)Q.rows * ((Q.cols + 127) / 128 * 4) * 4;
+            ++VJ.n;
         } else {
             J.job[J.n] = Q;
             J.t0[J.n] = tot;
@@ -1827,8 +1867,10 @@ extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
         }
     }
     J.t0[J.n] = tot;
+    VJ.t0[VJ.n] = vtot;
     TJ.wg0[TJ.n] = twg;
     if (tot > 0) k_quant_mxfp8_batch<<<kf_blocks(tot, 256, 16384), 256, 0, kf_stream()>>>(J);
+    if (vtot > 0) k_quant_mxfp8_vbatch<<<kf_blocks(vtot, 256, 16384), 256, 0, kf_stream()>>>(VJ);
     if (twg > 0) k_quant_mxfp8_tbatch<<<twg, 256, 0, kf_stream()>>>(TJ);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

@@ -175,7 +175,7 @@ def test_quantiser_batch_matches_single_calls(gpu):
     (weights) and row (activations) jobs of ragged sizes."""
     kf = gpu
     rng = np.random.default_rng(11)
-    shapes = [(96, 200, 1), (320, 256, 1), (37, 130, 0), (1, 8, 0), (160, 64, 1)]
+    shapes = [(96, 200, 1), (320, 256, 1), (37, 130, 0), (1, 8, 0), (160, 64, 1), (50, 264, 0), (9, 3072, 0)]
     jobs, refs, keep = [], [], []
     for rows, cols, tr in shapes:
         x = h(rng.standard_normal((rows, cols)) * np.exp(rng.uniform(-4, 4, (rows, 1))))
