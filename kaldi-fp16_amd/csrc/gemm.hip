@@ -1298,7 +1298,7 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         if (hr != 0) return hr < 0 ? -1 : 0;
     }
     // Tiles: 384x160 8-wave for N = 160 / 320; 256x64 for N <= 64; for
-    // N >= 256 192x128 8-wave tiles (80 KB of LDS: two workgroups share a CU and one's
+    // N >= 256 192x128 (or 128x192, below) 8-wave tiles (80 KB of LDS: two workgroups share a CU and one's
     // epilogue overlaps the other's MFMA loop; the wide K = 320 products write 2-3
     // full-width fp16 tensors; their 32-column wave tiles hold the MXFP8 copy's blocks);
     // 128x128 otherwise.
@@ -1306,8 +1306,14 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
     if (N % 160 == 0 && N <= 320 && !E.out8) tile = 5;
     else if (N <= 64) tile = 2;
     else if (N >= 256) tile = 6;  // 192x128: 32-column wave tiles, so out8 blocks fit
+    // short-K wide products with N % 192 == 0: 128x192 tiles (same 80 KB, two per CU; 12 -> 8
+    // column tiles per row block): TDNN-F linear input gradient 281 -> 257 us, affine forward
+    // 215 -> 207 us (rocprof A/B/A/B). Not with an MXFP8 copy: its 48-column wave tiles do
+    // not hold whole 32-column blocks (and 32x96 wave tiles overflow the epilogue's LDS).
+    if (tile == 6 && K <= 640 && N % 192 == 0 && !E.out8) tile = 7;
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
+        if (tile == 7) return launch<128, 192, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 6) return launch<192, 128, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 5) return launch<384, 160, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 2) return launch<256, 64, 4, 1, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1);  \
