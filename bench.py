@@ -7,8 +7,9 @@ LF-MMI objective + derivative (numerator and leaky-HMM denominator per eg,
 backward.go:224-371), backward with the gradient all-reduce overlapped (N > 1,
 kf_dp over RCCL), and SGD, over one minibatch of 64 synthetic egs (96,000 frames)
 per GPU, on the pinned synthetic 17-TDNN-F model (configs/cnn_tdnn_17f.xconfig)
-with the synthetic den graph and numerator FSTs of SURVEY §8d. Inputs are
-resident in HBM before the timed region.
+with the synthetic den graph and numerator FSTs of SURVEY §8d. Every timed step
+also uploads its minibatch (fp32 features, numerator FSTs) on a copy stream, as
+TrainStep's TransferBatch does (--no-h2d: inputs resident in HBM before timing).
 
 Launch:
   python bench.py [--gpus N --steps K --warmup W]
@@ -79,6 +80,10 @@ def parse(argv=None):
     p.add_argument("--gt-frames", type=int, default=48, help="frames of the gotorch-style float64 CPU leg")
     p.add_argument("--cpu-threads", type=int, default=0, help="0: every host core")
     p.add_argument("--no-prof", action="store_true")
+    p.add_argument("--no-h2d", action="store_true",
+                   help="upload the step's inputs once before timing (default: TrainStep's per-minibatch "
+                        "feature and numerator upload inside every step, overlapped on a copy stream)")
+    p.add_argument("--input-pool", type=int, default=2, help="distinct host minibatches cycled through (h2d)")
     p.add_argument("--fp8", action="store_true",
                    help="MXFP8 forward GEMMs (configs[4]; use with --xconfig cnn_tdnn_17f_3072.xconfig)")
     p.add_argument("--mode", choices=("train", "forward"), default="train",
@@ -426,16 +431,19 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
     if comm is not None and mode == "train":
         net.bind_dp(comm, bucket_bytes)                    # bucketed all-reduce inside backward
 
-    feats = synth.make_features(T, 40, seed=1234 + rank)   # this rank's shard of egs
-    fbuf = torch.from_numpy(feats.view(np.int16)).to("cuda")
     P = net.layers[-1][3]
     # chain supervision: shared den graph, one numerator FST per eg
     # (seed 7 + global eg index); the objective writes the output gradient on the
     # subsampled rows (leftCtx 30, stride 3) — every other row stays zero
     den_g = synth.make_den_graph(num_pdfs=P)
     dgraph = chain.DenGraph(den_g)
-    fsts = [synth.make_num_fst(dp.eg_index(rank, a.egs, e), num_pdfs=P) for e in range(a.egs)]
-    nbatch = chain.NumBatch(fsts)
+    h2d = mode == "train" and not a.no_h2d
+    npool = max(1, a.input_pool) if h2d else 1
+    # this rank's shards of egs: features (fp32, as the loader holds them) and numerator FSTs
+    # of `npool` distinct host minibatches (pool 0 is the r4 bench's minibatch)
+    feats_pool = [synth.make_features(T, 40, seed=1234 + rank + 7919 * b) for b in range(npool)]
+    packs = [chain.pack_num_fsts([synth.make_num_fst(dp.eg_index(rank, a.egs, e) + 104729 * b, num_pdfs=P)
+                                  for e in range(a.egs)]) for b in range(npool)]
     row0, nfr, stride = synth.chain_layout(a.egs, FRAMES_PER_EG)
     objective = chain.Chain(dgraph, max_seqs=a.egs, max_frames=int(nfr.max()))
     out_ptr = net.activation("output")[0]
@@ -448,14 +456,64 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         ibuf = torch.from_numpy(ivecs.view(np.int16)).to("cuda")
         seq_off = np.arange(a.egs + 1, dtype=np.int32) * FRAMES_PER_EG
 
+    comp = torch.cuda.current_stream()
+    if h2d:
+        # TrainStep's input stage (train_step.go:155 TransferBatch -> bridge.cu:206-267, and the
+        # per-sequence FST uploads of chain_loss.go:44-97) inside every timed step: step i+1's
+        # fp32 features (pinned host) and numerator FSTs (kf_num_batch_refill) go up on a copy
+        # stream while step i computes; the step then rounds its features to fp16 (RNE,
+        # fp16.go:12-70) on the GPU. Two device slots; events order reuse.
+        copy = torch.cuda.Stream()
+        host = [torch.from_numpy(f).pin_memory() for f in feats_pool]
+        f32 = [torch.empty((T, 40), dtype=torch.float32, device="cuda") for _ in range(2)]
+        fbufs = [torch.empty((T, 40), dtype=torch.float16, device="cuda") for _ in range(2)]
+        nums = [chain.NumBatch(packs[0]), chain.NumBatch(packs[min(1, npool - 1)])]
+        ev_copied = [torch.cuda.Event() for _ in range(2)]
+        ev_conv = [torch.cuda.Event() for _ in range(2)]
+        ev_obj = [torch.cuda.Event() for _ in range(2)]
+        for nb in nums:   # the first refill frees the create-time upload (one device sync), untimed
+            nb.refill(packs[0], copy.cuda_stream)
+        torch.cuda.synchronize()
+        state = {"i": 0}
+
+        def stage(i):
+            """step i's inputs into slot i % 2, on the copy stream"""
+            sl = i % 2
+            copy.wait_event(ev_conv[sl])    # the slot's fp32 features were converted (step i - 2)
+            copy.wait_event(ev_obj[sl])     # the slot's numerator was used (step i - 2)
+            with torch.cuda.stream(copy):
+                f32[sl].copy_(host[i % npool], non_blocking=True)
+                ev_copied[sl].record(copy)
+            nums[sl].refill(packs[i % npool], copy.cuda_stream)
+
+        stage(0)
+    else:
+        feats = feats_pool[0]
+        fbuf = torch.from_numpy(feats.view(np.int16)).to("cuda")
+        nbatch = chain.NumBatch(packs[0])
+
     def step():
-        if ivd:
-            net.forward_ivector(fbuf.data_ptr(), T, ibuf.data_ptr(), seq_off)
+        if h2d:
+            i = state["i"]
+            sl = i % 2
+            comp.wait_event(ev_copied[sl])
+            kfp16.check(kfp16.core.bridge_fp32_to_fp16_gpu(fbufs[sl].data_ptr(), f32[sl].data_ptr(), T * 40),
+                        "bridge_fp32_to_fp16_gpu")
+            ev_conv[sl].record(comp)
+            fptr, num = fbufs[sl].data_ptr(), nums[sl]
         else:
-            net.forward(fbuf.data_ptr(), T)
+            fptr, num = fbuf.data_ptr(), nbatch
+        if ivd:
+            net.forward_ivector(fptr, T, ibuf.data_ptr(), seq_off)
+        else:
+            net.forward(fptr, T)
         if mode == "forward":
             return
-        objective.compute(nbatch, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
+        objective.compute(num, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
+        if h2d:
+            ev_obj[sl].record(comp)
+            stage(i + 1)                    # the next step's inputs, overlapped with this backward
+            state["i"] = i + 1
         net.backward(gbuf.data_ptr())       # + the overlapped gradient all-reduce (N > 1)
         net.sgd(a.lr, a.momentum)
 
@@ -471,15 +529,23 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         kfp16.core.kf_prof_reset()
         kfp16.core.kf_prof_enable(1)
     dp0 = comm.stats() if comm is not None else (0, 0)
+    # per-step HIP events on the launch stream (the library runs on torch's current stream):
+    # the median step beside the wall-clock mean (median of the timed steps)
+    st = torch.cuda.current_stream()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
+        evs[i].record(st)
         step()
+    evs[steps].record(st)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kfp16.core.kf_prof_enable(0)
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    median_ms = dp.max_over_ranks(float(np.median(step_ms)), "cuda")
     elapsed = dp.max_over_ranks(elapsed, "cuda")
     dp1 = comm.stats() if comm is not None else (0, 0)
 
@@ -502,25 +568,35 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         res = objective.result()
         stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
                                   "cuda")
-    out = {"T": T, "elapsed": elapsed, "steps": steps, "prof": prof, "chain_prof": chain_prof, "classes": classes,
-           "xconfig": xconfig, "mode": mode,
+    out = {"T": T, "elapsed": elapsed, "median_ms": median_ms, "step_ms": step_ms, "steps": steps, "prof": prof, "chain_prof": chain_prof, "classes": classes,
+           "xconfig": xconfig, "mode": mode, "h2d": h2d, "input_pool": npool,
            "stats": stats, "ivd": ivd, "dp": (dp1[0] - dp0[0], dp1[1] - dp0[1]),
            "buckets": len(net.dp_plan(bucket_bytes)) if comm is not None else 0}
     ctx = (xcfg, params, bns, den_g, P) if keep else None
+    torch.cuda.synchronize()
+    for nb in (nums if h2d else [nbatch]):
+        nb.close()
     objective.close()
     net.close()
     return out, ctx
 
 
 def describe(r, a, world, mode, fp8, xconfig, peak):
-    ms_step = r["elapsed"] / r["steps"] * 1e3
+    # ms_per_step: median of the timed steps (max over ranks); value: whole-job frames over
+    # the wall clock of all timed steps, whose mean step is reported beside the median
+    mean_ms = r["elapsed"] / r["steps"] * 1e3
     value = r["T"] * world * r["steps"] / r["elapsed"]
-    d = {"value": round(value, 1), "ms_per_step": round(ms_step, 3)}
+    d = {"value": round(value, 1), "ms_per_step": round(r["median_ms"], 3), "ms_per_step_mean": round(mean_ms, 3),
+         "ms_per_step_min_max": [round(min(r["step_ms"]), 3), round(max(r["step_ms"]), 3)]}
     mf = MODEL_MFLOP_PER_FRAME.get(r["xconfig"])
     if mf is not None:
-        # whole step against the dense MFMA roofline: frames/s x algorithmic FLOPs per frame
+        # whole step against the dense FP16 MFMA roofline: frames/s x algorithmic FLOPs per
+        # frame / 2.5 PF. Also for the MXFP8 step, whose backward stays mostly fp16 (its
+        # fp8 share is in roofline.classes): against the 5 PF fp8 peak it would read ~2x
+        # low and not compare with the fp16 step
         fpf = mf[1] if r["mode"] == "train" else mf[0]
-        d["step_mfma_frac"] = round(value * fpf * 1e6 / (peak * 1e12), 4)
+        d["step_mfma_frac"] = round(value * fpf * 1e6 / (PEAK_FP16_TFLOPS * 1e12), 4)
+        d["step_mfma_peak"] = "fp16 dense 2.5 PF"
         d["step_mflop_per_frame"] = fpf
     if r["prof"]:
         d["roofline"] = roofline(r["prof"], r["steps"], peak)
@@ -619,9 +695,18 @@ def main():
             "config": {"workload": workload,
                        "xconfig": a.xconfig, "egs_per_gpu": a.egs, "frames_per_eg": FRAMES_PER_EG,
                        "global_batch_egs": a.egs * world, "parallelism": f"dp{world}",
+                       "h2d_in_step": bool(head["h2d"]),
+                       "inputs": ("per step: fp32 features from pinned host memory and the minibatch's "
+                                  "numerator FSTs (kf_num_batch_refill) uploaded on a copy stream during the "
+                                  "previous step, RNE to fp16 on the GPU inside the step; "
+                                  f"{head['input_pool']} distinct host minibatches cycled")
+                                 if head["h2d"] else "resident in HBM before timing",
                        "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)"},
         }
-        for k in ("step_mfma_frac", "step_mflop_per_frame", "objf_per_frame", "objective_finite_seqs"):
+        out["ms_per_step_mean"] = d["ms_per_step_mean"]
+        out["ms_per_step_min_max"] = d["ms_per_step_min_max"]
+        for k in ("step_mfma_frac", "step_mfma_peak", "step_mflop_per_frame", "objf_per_frame",
+                  "objective_finite_seqs"):
             if k in d:
                 out[k] = d[k]
         if not fwd_only:

@@ -80,6 +80,16 @@ KfNumBatch *kf_num_batch_create(int nseq, const int32_t *state_off, const int32_
                                 const int32_t *row_ptr, const int32_t *dst, const int32_t *pdf1,
                                 const float *logw, const int32_t *final_off,
                                 const int32_t *final_state, const float *final_logw);
+/* Re-fill an existing batch with the next minibatch's FSTs (same arrays as
+ * kf_num_batch_create), TrainStep's per-minibatch upload (chain_loss.go:44-97) without a
+ * device-wide stall: host preparation into pinned staging and one asynchronous copy on
+ * `stream` (NULL: kf_get_stream()) into device buffers that only grow (a growth waits for
+ * the device once). The caller orders the copy after every kernel still reading the batch's
+ * previous contents; kf_chain_compute waits for the copy itself. 0 / -1. */
+int kf_num_batch_refill(KfNumBatch *b, int nseq, const int32_t *state_off, const int32_t *arc_off,
+                        const int32_t *row_ptr, const int32_t *dst, const int32_t *pdf1,
+                        const float *logw, const int32_t *final_off, const int32_t *final_state,
+                        const float *final_logw, void *stream);
 void kf_num_batch_free(KfNumBatch *b);
 
 /* Workspace for up to max_seqs sequences of up to max_frames frames each. */

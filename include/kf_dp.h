@@ -56,9 +56,9 @@ int kf_dp_allreduce_sum_f64(KfDp *dp, double *buf, size_t count);
 /* number of all-reduce launches and fp32 values exchanged since kf_dp_create */
 int kf_dp_stats(const KfDp *dp, long long *launches, long long *values);
 
-/* Test hooks (one GPU can then check what N ranks depend on). Each bucket issued by
- * kf_dp_allreduce_mean_async whose address lies at or above grad_base also does, on the
- * communication stream:
+/* Test hooks (one GPU can then check what N ranks depend on). While a mode is on, every
+ * bucket issued by kf_dp_allreduce_mean_async must lie inside [grad_base, grad_base + count)
+ * and also does, on the communication stream:
  *   KF_DP_DEBUG_SNAPSHOT:  before the all-reduce, copies the bucket to the same offset
  *                          of aux_base: the values the exchange started from, so a test
  *                          can compare them with the finished gradient (a bucket issued

@@ -526,7 +526,8 @@ static size_t den_rec_fixed_bytes(int P, int nsl, int spg, int ns) {
 // posteriors: the alpha' and beta rows of `pair` frames in the f / b tables' slice orders
 // (rs = nsl * 64 entries each), the gamma rows and the q table's perm / len / off
 static size_t den_post_lds_bytes(int rs, int P, int nslq, int pair = 1) {
-    return (size_t)4 * (64 + 2 * (size_t)pair * rs + (size_t)pair * P + (size_t)nslq * 66);
+    (void)nslq;  // (the q-table metadata is read from global memory)
+    return (size_t)4 * (64 + 2 * (size_t)pair * rs + (size_t)pair * P);
 }
 
 // ---------------------------------------------------------------------------
@@ -781,6 +782,73 @@ __device__ __forceinline__ void sell_slice(const uint2 *arcs, int len, int off, 
     }
 }
 
+// The wave's slices of a SELL table (slots k = wave, wave + DEN_WAVES, ... of `slot`),
+// gather-summed in slot order with the same per-slice arithmetic as sell_slice. PIPE = 0:
+// sell_slice per slice (8 records loaded, then gathered). PIPE = 1: 4-record batches, the
+// next batch (the slice's rest, else the next slice's first) loaded before the current one
+// is gathered, so the L2 round trip of the record stream opens only the wave's first batch
+// (same registers: 2 x 4 records in flight instead of 8). pre(j) runs when slice j starts
+// (its result is handed to post), post(j, pre, acc) after its last record.
+template <int NS, int PIPE, class Pre, class Post>
+__device__ __forceinline__ void sell_walk(const uint2 *arcs, const int *len, const int *off, const int *slot,
+                                          int spg, int lane, int wave, const unsigned char *sv,
+                                          const unsigned char *sx, Pre pre, Post post) {
+    if constexpr (PIPE == 0) {
+        for (int k = wave; k < spg; k += DEN_WAVES) {
+            const int j = slot[k];
+            if (j < 0) continue;
+            const float pv = pre(j);
+            float acc[NS];
+            sell_slice<NS>(arcs, len[j], off[j], lane, sv, sx, acc);
+            post(j, pv, acc);
+        }
+    } else {
+#pragma clang fp contract(off)  // (a * tp) * x + acc rounded as the oracle does, any NS
+        auto nxt_slot = [&](int k) {
+            while (k < spg && slot[k] < 0) k += DEN_WAVES;
+            return k;
+        };
+        auto ld4 = [&](uint2 (&r)[4], int o, int k) {
+            const uint2 *e = arcs + ((size_t)o * 64 + lane) + (size_t)k * 64;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[i] = e[i * 64];
+        };
+        int k = nxt_slot(wave);
+        uint2 cur[4];
+        if (k < spg) ld4(cur, off[slot[k]], 0);
+        while (k < spg) {
+            const int j = slot[k];
+            const int n = len[j], o = off[j];
+            const int kn = nxt_slot(k + DEN_WAVES);
+            const float pv = pre(j);
+            float acc[NS];
+#pragma unroll
+            for (int q = 0; q < NS; ++q) acc[q] = 0.f;
+            for (int b = 0; b < n; b += 4) {
+                uint2 nx[4];
+                if (b + 4 < n) ld4(nx, o, b + 4);
+                else if (kn < spg) ld4(nx, off[slot[kn]], 0);
+                DenV<NS> a[4], x[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    a[i] = lds_v<NS>(sv, cur[i].x & 0xFFFF);
+                    x[i] = lds_v<NS>(sx, cur[i].x >> 16);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float tp = __uint_as_float(cur[i].y);
+#pragma unroll
+                    for (int q = 0; q < NS; ++q) acc[q] += a[i].x[q] * tp * x[i].x[q];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cur[i] = nx[i];
+            }
+            post(j, pv, acc);
+            k = kn;
+        }
+    }
+}
+
 // Per-block SELL state: len / off of every slice and this block's slot list (slot k is
 // processed by wave k % DEN_WAVES; -1 = empty) in LDS; initp stays in global memory
 // (L2-resident, read once per position per frame), which keeps the NS = 2 recursion small
@@ -848,7 +916,7 @@ __device__ __forceinline__ void den_put_exp(float *xe, int P, const RowPre<XT> (
 // the exchange: all blocks rebuild the full alpha'[t+1] in LDS from those rows. The store
 // keeps the slices before the leaky term: alpha'[t] = row[t] + asum[t] * leaky * init,
 // which k_den_post applies when it loads the row (one write per frame, not two).
-template <typename XT, bool LOC, int NS>
+template <typename XT, bool LOC, int NS, int PIPE = 0>
 __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
                                              unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -925,19 +993,16 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         }
         const int buf = (t + 1) & 1;
         float *tail = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
-        for (int k = wave; k < spg; k += DEN_WAVES) {
-            const int j = F.slot[k];
-            if (j < 0) continue;
-            const bool real = j * 64 + lane < S;  // padding positions stay 0
-            float acc[NS];
-            sell_slice<NS>(arcs, F.len[j], F.off[j], lane, sv, sx, acc);
+        sell_walk<NS, PIPE>(arcs, F.len, F.off, F.slot, spg, lane, wave, sv, sx, [&](int) { return 0.f; },
+                            [&](int j, float, const float (&acc)[NS]) {
+                                const bool real = j * 64 + lane < S;  // padding positions stay 0
 #pragma unroll
-            for (int q = 0; q < NS; ++q) {
-                const float v = real ? acc[q] * inv[q] : 0.0f;
-                if (live[q]) x_st<LOC>(arow[q], j * 64 + lane, v);
-                pq[q] += v;
-            }
-        }
+                                for (int q = 0; q < NS; ++q) {
+                                    const float v = real ? acc[q] * inv[q] : 0.0f;
+                                    if (live[q]) x_st<LOC>(arow[q], j * 64 + lane, v);
+                                    pq[q] += v;
+                                }
+                            });
         if (r.trace && unit == 0 && gi < 2 && lane == 0 && t >= 16 && t < 48)  // per-wave arc end, blocks 0, 1
             r.trace[256 + ((t - 16) * 2 + gi) * DEN_WAVES + wave] = wall_clock64();
         DEN_TP(1);
@@ -1026,7 +1091,7 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
 // frame (the den posteriors of a frame sum to one: they are d log p / d x_t), so this
 // pass scales by 1/<init, beta'[t+1]> and starts from ones — it needs nothing from the
 // forward pass and runs beside it. Iteration `it` is frame T_q - 1 - it of sequence q.
-template <typename XT, bool LOC, int NS>
+template <typename XT, bool LOC, int NS, int PIPE = 0>
 __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, const DenX &X,
                                              unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1097,20 +1162,18 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
         }
         const int buf = it & 1;
         float *tail = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
-        for (int k = wave; k < spg; k += DEN_WAVES) {  // kernel_den_backward_transitions
-            const int j = B.slot[k];
-            if (j < 0) continue;
-            const bool real = j * 64 + lane < S;  // padding positions stay 0
-            const float ip = B.initp[j * 64 + lane];
-            float acc[NS];
-            sell_slice<NS>(arcs, B.len[j], B.off[j], lane, sv, sx, acc);
+        // kernel_den_backward_transitions
+        sell_walk<NS, PIPE>(arcs, B.len, B.off, B.slot, spg, lane, wave, sv, sx,
+                            [&](int j) { return B.initp[j * 64 + lane]; },
+                            [&](int j, float ip, const float (&acc)[NS]) {
+                                const bool real = j * 64 + lane < S;  // padding positions stay 0
 #pragma unroll
-            for (int q = 0; q < NS; ++q) {
-                const float bd = real ? acc[q] * inv[q] : 0.0f;
-                if (live[q]) x_st<LOC>(brow[q], j * 64 + lane, bd);
-                pq[q] += ip * bd;
-            }
-        }
+                                for (int q = 0; q < NS; ++q) {
+                                    const float bd = real ? acc[q] * inv[q] : 0.0f;
+                                    if (live[q]) x_st<LOC>(brow[q], j * 64 + lane, bd);
+                                    pq[q] += ip * bd;
+                                }
+                            });
         float ws[NS];
 #pragma unroll
         for (int q = 0; q < NS; ++q) ws[q] = wave_sum(pq[q]);
@@ -1149,7 +1212,7 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
 // independent, see den_bwd_body). One launch keeps all 2*units*G blocks co-resident,
 // which the bounded exchange polls rely on; the XCD grouping of den_map is kept (G
 // consecutive ids share an XCD).
-template <typename XT, int NS>
+template <typename XT, int NS, int PIPE = 0>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const DenRun r, const DenX XF,
                                                         const DenX XB) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1165,11 +1228,11 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
     const int loc = den_xcd_local(bwd ? XB : XF, unit, reinterpret_cast<int *>(smem) + 32);
     if (loc < 0) return;  // timed out (reported through the timeout words)
     if (bwd) {
-        if (loc) den_bwd_body<XT, true, NS>(g, r, XB, smem, unit, gi);
-        else den_bwd_body<XT, false, NS>(g, r, XB, smem, unit, gi);
+        if (loc) den_bwd_body<XT, true, NS, PIPE>(g, r, XB, smem, unit, gi);
+        else den_bwd_body<XT, false, NS, PIPE>(g, r, XB, smem, unit, gi);
     } else {
-        if (loc) den_fwd_body<XT, true, NS>(g, r, XF, smem, unit, gi);
-        else den_fwd_body<XT, false, NS>(g, r, XF, smem, unit, gi);
+        if (loc) den_fwd_body<XT, true, NS, PIPE>(g, r, XF, smem, unit, gi);
+        else den_fwd_body<XT, false, NS, PIPE>(g, r, XF, smem, unit, gi);
     }
 }
 
@@ -1182,24 +1245,34 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
 #define POST_FRAMES 2  // frames per block (one two-frame pass: 1.82 -> 1.76 ms against 4)
 // records carry LDS byte offsets into the PAIR-interleaved alpha' / beta rows (one
 // 8-byte gather per operand serves both frames)
+// Record pipeline of one wave over its slices of a SELL table: the next 8 records (the
+// rest of this slice, else the first of the wave's next slice) are loaded before the
+// current 8 are gathered and summed, so an L2 round trip hides under a batch's work instead
+// of opening every batch (k_den_post was bound by those round trips: ~30 batches per wave,
+// one exposed L2 latency each).
+struct RecBatch {
+    uint2 r[8];
+    __device__ __forceinline__ void load(const uint2 *arcs, int off, int k, int lane) {
+        const uint2 *e = arcs + ((size_t)off * 64 + lane) + (size_t)k * 64;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = e[i * 64];
+    }
+};
+// slot list walk of one wave: the next non-empty slot at or after k (stride DEN_WAVES)
+__device__ __forceinline__ int next_slot(const int *slot, int k, int spg) {
+    while (k < spg && slot[k] < 0) k += DEN_WAVES;
+    return k;
+}
 template <int PAIR>
-__device__ __forceinline__ void post_slice(const uint2 *arcs, int len, int off, int lane,
-                                           const unsigned char *sva, const unsigned char *svb, float acc[PAIR]) {
+__device__ __forceinline__ void post_batch(const RecBatch &b, const unsigned char *sva, const unsigned char *svb,
+                                           float acc[PAIR]) {
 #pragma clang fp contract(off)  // (alpha * tp) * beta + acc, as the oracle rounds
-    const uint2 *e = arcs + (size_t)off * 64 + lane;
 #pragma unroll
-    for (int f = 0; f < PAIR; ++f) acc[f] = 0.f;
-    for (int k = 0; k < len; k += 8) {
-        uint2 rr[8];
+    for (int i = 0; i < 8; ++i) {
+        const DenV<PAIR> a = lds_v<PAIR>(sva, b.r[i].x & 0xFFFF), v = lds_v<PAIR>(svb, b.r[i].x >> 16);
+        const float tp = __uint_as_float(b.r[i].y);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const DenV<PAIR> a = lds_v<PAIR>(sva, rr[i].x & 0xFFFF), b = lds_v<PAIR>(svb, rr[i].x >> 16);
-            const float tp = __uint_as_float(rr[i].y);
-#pragma unroll
-            for (int f = 0; f < PAIR; ++f) acc[f] += a.x[f] * tp * b.x[f];
-        }
+        for (int f = 0; f < PAIR; ++f) acc[f] += a.x[f] * tp * v.x[f];
     }
 }
 template <typename XT, int MODE, int PAIR>
@@ -1213,13 +1286,10 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     float *va = reinterpret_cast<float *>(smem) + 64;  // [rsf][PAIR] alpha'[t+f], f-table slice order
     float *vb = va + PAIR * rsf;                       // [rsb][PAIR] beta[t+f+1], b-table slice order
     float *gam = vb + PAIR * rsb;                      // [PAIR][P] den, then the gradient
-    int *metaq = reinterpret_cast<int *>(gam + PAIR * P);
-    const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
-    for (int i = tid; i < nslq * 64; i += DEN_THREADS) metaq[i] = g.q.perm[i];
-    for (int i = tid; i < nslq; i += DEN_THREADS) {
-        metaq[nslq * 64 + i] = g.q.len[i];
-        metaq[nslq * 65 + i] = g.q.off[i];
-    }
+    // the q table's slice metadata stays in global memory (L2): one load per slice per wave
+    // (copying it to LDS cost every block 13 KB of L2 reads and LDS writes)
+    const int *permq = g.q.perm, *lenq = g.q.len, *offq = g.q.off;
+    (void)nslq;
 
     const int T = r.frames[seq];
     const int t0 = fb * POST_FRAMES, t1 = min(T, t0 + POST_FRAMES);
@@ -1273,39 +1343,69 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
         // stage alpha'[t+f], beta[t+f+1] (a missing second frame computes zeros); the
         // stored rows lack the leaky terms (den_fwd_body, den_bwd_body), added here as the
         // recursions add them
+        // both frames' rows are loaded before the first LDS store, which then writes each
+        // position's PAIR values as one vector (a PAIR-strided scalar store is 2-way conflicted)
+        float va_[PAIR][DEN_MAXS], vb_[PAIR][DEN_MAXS], as1[PAIR], tb[PAIR];
 #pragma unroll
         for (int f = 0; f < PAIR; ++f) {
             const bool live = f < nf2;
             // (a missing frame reads frame t's rows, which exist, and stores zeros)
             const int tf = live ? t + f : t;
             const float *ar = astore + (size_t)tf * rsf, *br = bstore + (size_t)(tf + 1) * rsb;
-            const float as1 = live ? asum[t + f] : 0.f;
-            const float tb = live ? leaky * bsum[t + f + 1] : 0.f;
-            float va_[DEN_MAXS], vb_[DEN_MAXS];
+            as1[f] = live ? asum[t + f] : 0.f;
+            tb[f] = live ? leaky * bsum[t + f + 1] : 0.f;
 #pragma unroll
             for (int m = 0; m < DEN_MAXS; ++m) {  // unconditional loads (index clamped)
                 const int c = tid + m * DEN_THREADS;
-                va_[m] = __builtin_nontemporal_load(ar + min(c, rsf - 1));
-                vb_[m] = __builtin_nontemporal_load(br + min(c, rsb - 1));
+                va_[f][m] = __builtin_nontemporal_load(ar + min(c, rsf - 1));
+                vb_[f][m] = __builtin_nontemporal_load(br + min(c, rsb - 1));
             }
+        }
 #pragma unroll
-            for (int m = 0; m < DEN_MAXS; ++m) {
-                const int c = tid + m * DEN_THREADS;
-                if (c < rsf) va[PAIR * c + f] = live ? va_[m] + as1 * leaky * ipf[m] : 0.f;
-                if (c < rsb) vb[PAIR * c + f] = live ? vb_[m] + tb : 0.f;
+        for (int m = 0; m < DEN_MAXS; ++m) {
+            const int c = tid + m * DEN_THREADS;
+            DenV<PAIR> a, b;
+#pragma unroll
+            for (int f = 0; f < PAIR; ++f) {
+                const bool live = f < nf2;
+                a.x[f] = live ? va_[f][m] + as1[f] * leaky * ipf[m] : 0.f;
+                b.x[f] = live ? vb_[f][m] + tb[f] : 0.f;
+            }
+            if constexpr (PAIR == 2) {
+                if (c < rsf) reinterpret_cast<float2 *>(va)[c] = make_float2(a.x[0], a.x[1]);
+                if (c < rsb) reinterpret_cast<float2 *>(vb)[c] = make_float2(b.x[0], b.x[1]);
+            } else {
+                if (c < rsf) va[c] = a.x[0];
+                if (c < rsb) vb[c] = b.x[0];
             }
         }
         __syncthreads();
         float gpart[PAIR];
 #pragma unroll
         for (int f = 0; f < PAIR; ++f) gpart[f] = 0.f;
-        for (int k = wave; k < g.q.spg[0]; k += DEN_WAVES) {
-            const int j = g.q.slot[0][k];
-            if (j < 0) continue;
+        const int *slotq = g.q.slot[0];
+        const int spgq = g.q.spg[0];
+        const uint2 *arcs = g.q.arc_p[PAIR - 1];
+        int k = next_slot(slotq, wave, spgq);
+        RecBatch cur;
+        if (k < spgq) cur.load(arcs, offq[slotq[k]], 0, lane);
+        while (k < spgq) {
+            const int j = slotq[k];
+            const int len = lenq[j], off = offq[j];
+            const int kn = next_slot(slotq, k + DEN_WAVES, spgq);
             const int pdf = permq[j * 64 + lane];
             float acc[PAIR];
-            post_slice<PAIR>(g.q.arc_p[PAIR - 1], lenq[j], offq[j], lane, reinterpret_cast<const unsigned char *>(va),
-                             reinterpret_cast<const unsigned char *>(vb), acc);
+#pragma unroll
+            for (int f = 0; f < PAIR; ++f) acc[f] = 0.f;
+            for (int b = 0; b < len; b += 8) {  // len is a multiple of 8
+                RecBatch nxt;
+                if (b + 8 < len) nxt.load(arcs, off, b + 8, lane);
+                else if (kn < spgq) nxt.load(arcs, offq[slotq[kn]], 0, lane);
+                post_batch<PAIR>(cur, reinterpret_cast<const unsigned char *>(va),
+                                 reinterpret_cast<const unsigned char *>(vb), acc);
+                cur = nxt;
+            }
+            k = kn;
             if (pdf < 0) continue;
 #pragma unroll
             for (int f = 0; f < PAIR; ++f) {
@@ -1797,6 +1897,8 @@ void launch_den_fb(const DenDev &g, const DenRun &r, const DenX &XF, DenXBuf &xf
     dim3 grid(2 * XF.nseq * XF.G);
     const size_t lds = std::max(XF.lds_f, XB.lds_b);
     if (fp32_in) hipLaunchKernelGGL((k_den_fb<float, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
+    else if (XF.ns == 2 && (kf_expt() & 4))
+        hipLaunchKernelGGL((k_den_fb<h16, 2, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
     else if (XF.ns == 2) hipLaunchKernelGGL((k_den_fb<h16, 2>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
     else hipLaunchKernelGGL((k_den_fb<h16, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
 }
@@ -1928,9 +2030,12 @@ void append(std::vector<int32_t> &blob, const std::vector<T> &v, std::vector<siz
     if (!v.empty()) memcpy(blob.data() + n, v.data(), v.size() * 4);
 }
 
-NumDevice *upload_nums(std::vector<NumHost> &hs, const char **why) {
-    std::vector<int32_t> blob;
-    std::vector<std::vector<size_t>> offs(hs.size());
+// the numerator tables of a minibatch as one int32 blob; offs[i] = the 19 table offsets of
+// FST i inside it
+static void pack_nums(std::vector<NumHost> &hs, std::vector<int32_t> &blob,
+                      std::vector<std::vector<size_t>> &offs) {
+    blob.clear();
+    offs.assign(hs.size(), {});
     for (size_t i = 0; i < hs.size(); ++i) {
         NumHost &h = hs[i];
         auto &o = offs[i];
@@ -1954,13 +2059,14 @@ NumDevice *upload_nums(std::vector<NumHost> &hs, const char **why) {
         append(blob, h.in_w, o);
         append(blob, h.gw, o);
     }
-    auto *nd = new NumDevice();
-    int32_t *d = dev_upload(blob, nd->owned);
-    if (!d) {
-        delete nd;
-        *why = "hipMalloc failed for numerator FSTs";
-        return nullptr;
-    }
+}
+
+// descriptors of the FSTs packed at device address d
+static void num_descs(const std::vector<NumHost> &hs, const std::vector<std::vector<size_t>> &offs,
+                      const int32_t *d, NumDevice *nd) {
+    nd->desc.clear();
+    nd->G.clear();
+    nd->Ag.clear();
     for (size_t i = 0; i < hs.size(); ++i) {
         const auto &o = offs[i];
         LogFstDev f{};
@@ -1992,6 +2098,20 @@ NumDevice *upload_nums(std::vector<NumHost> &hs, const char **why) {
         nd->G.push_back(f.G);
         nd->Ag.push_back((int)hs[i].grp_arc.size());
     }
+}
+
+NumDevice *upload_nums(std::vector<NumHost> &hs, const char **why) {
+    std::vector<int32_t> blob;
+    std::vector<std::vector<size_t>> offs;
+    pack_nums(hs, blob, offs);
+    auto *nd = new NumDevice();
+    int32_t *d = dev_upload(blob, nd->owned);
+    if (!d) {
+        delete nd;
+        *why = "hipMalloc failed for numerator FSTs";
+        return nullptr;
+    }
+    num_descs(hs, offs, d, nd);
     return nd;
 }
 
@@ -2542,7 +2662,22 @@ struct KfDenGraph {
 struct KfNumBatch {
     NumDevice *nd = nullptr;
     std::vector<int> S;
-    ~KfNumBatch() { delete nd; }
+    unsigned gen = 0;                  // bumped by every refill (kf_chain_compute's layout cache)
+    // kf_num_batch_refill: device blob and its pinned host staging (grow only)
+    int32_t *d_blob = nullptr;
+    size_t d_cap = 0;                  // int32 entries
+    int32_t *h_blob = nullptr;
+    size_t h_cap = 0;
+    hipEvent_t ev_copy = nullptr;      // the last refill's copy (h_blob is reused after it)
+    ~KfNumBatch() {
+        delete nd;
+        if (ev_copy) {
+            hipEventSynchronize(ev_copy);
+            hipEventDestroy(ev_copy);
+        }
+        if (d_blob) hipFree(d_blob);
+        if (h_blob) hipHostFree(h_blob);
+    }
 };
 
 struct KfChain {
@@ -2561,6 +2696,11 @@ struct KfChain {
     float *d_num_total = nullptr;
     // cache of the last run's layout (re-uploaded only when it changes)
     const KfNumBatch *last_num = nullptr;
+    unsigned last_gen = 0;
+    // pinned staging of the layout upload: two slots, each reused after its copy's event
+    char *h_stage[2] = {nullptr, nullptr};
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
+    int stage_slot = 0;
     std::vector<int> last_row0, last_frames;
     int last_stride = -1, last_nseq = 0;
     const void *last_nnet = nullptr;
@@ -2574,6 +2714,13 @@ struct KfChain {
     unsigned long long *trace = nullptr;  // kf_chain_trace (diagnostics)
     int den_pairs = 1;                     // kf_chain_debug_den_pairs (tests)
     ~KfChain() {
+        for (int i = 0; i < 2; ++i) {
+            if (ev_stage[i]) {
+                hipEventSynchronize(ev_stage[i]);
+                hipEventDestroy(ev_stage[i]);
+            }
+            if (h_stage[i]) hipHostFree(h_stage[i]);
+        }
         if (side) hipStreamDestroy(side);
         if (ev_in) hipEventDestroy(ev_in);
         if (ev_num) hipEventDestroy(ev_num);
@@ -2632,17 +2779,17 @@ extern "C" int kf_den_graph_initial_probs(const KfDenGraph *g, float *out) {
 }
 extern "C" void kf_den_graph_free(KfDenGraph *g) { delete g; }
 
-extern "C" KfNumBatch *kf_num_batch_create(int nseq, const int32_t *state_off,
-                                           const int32_t *arc_off, const int32_t *row_ptr,
-                                           const int32_t *dst, const int32_t *pdf1,
-                                           const float *logw, const int32_t *final_off,
-                                           const int32_t *final_state, const float *final_logw) {
+// host CSR arrays (kf_chain.h layout) -> prepared numerator FSTs
+static bool num_hosts(const char *fn, int nseq, const int32_t *state_off, const int32_t *arc_off,
+                      const int32_t *row_ptr, const int32_t *dst, const int32_t *pdf1, const float *logw,
+                      const int32_t *final_off, const int32_t *final_state, const float *final_logw,
+                      std::vector<NumHost> &hs) {
     const char *why = nullptr;
     if (nseq <= 0 || !state_off || !arc_off || !row_ptr || !final_off) {
-        kfc_set_error("kf_num_batch_create: invalid arguments");
-        return nullptr;
+        kfc_set_error("%s: invalid arguments", fn);
+        return false;
     }
-    std::vector<NumHost> hs(nseq);
+    hs.assign(nseq, NumHost());
     for (int i = 0; i < nseq; ++i) {
         NumHost &h = hs[i];
         h.S = state_off[i + 1] - state_off[i];
@@ -2650,8 +2797,8 @@ extern "C" KfNumBatch *kf_num_batch_create(int nseq, const int32_t *state_off,
         h.nfinal = final_off[i + 1] - final_off[i];
         h.start = 0;
         if (h.S <= 0 || h.A < 0 || h.nfinal < 0) {
-            kfc_set_error("kf_num_batch_create: sequence %d has an empty FST", i);
-            return nullptr;
+            kfc_set_error("%s: sequence %d has an empty FST", fn, i);
+            return false;
         }
         const int32_t *rp = row_ptr + state_off[i] + i;
         h.row_ptr.assign(rp, rp + h.S + 1);
@@ -2661,10 +2808,23 @@ extern "C" KfNumBatch *kf_num_batch_create(int nseq, const int32_t *state_off,
         h.fin_state.assign(final_state + final_off[i], final_state + final_off[i + 1]);
         h.fin_w.assign(final_logw + final_off[i], final_logw + final_off[i + 1]);
         if (!prepare_num(h, &why)) {
-            kfc_set_error("kf_num_batch_create: sequence %d: %s", i, why);
-            return nullptr;
+            kfc_set_error("%s: sequence %d: %s", fn, i, why);
+            return false;
         }
     }
+    return true;
+}
+
+extern "C" KfNumBatch *kf_num_batch_create(int nseq, const int32_t *state_off,
+                                           const int32_t *arc_off, const int32_t *row_ptr,
+                                           const int32_t *dst, const int32_t *pdf1,
+                                           const float *logw, const int32_t *final_off,
+                                           const int32_t *final_state, const float *final_logw) {
+    const char *why = nullptr;
+    std::vector<NumHost> hs;
+    if (!num_hosts("kf_num_batch_create", nseq, state_off, arc_off, row_ptr, dst, pdf1, logw, final_off,
+                   final_state, final_logw, hs))
+        return nullptr;
     NumDevice *nd = upload_nums(hs, &why);
     if (!nd) {
         kfc_set_error("kf_num_batch_create: %s", why);
@@ -2674,6 +2834,74 @@ extern "C" KfNumBatch *kf_num_batch_create(int nseq, const int32_t *state_off,
     b->nd = nd;
     for (auto &h : hs) b->S.push_back(h.S);
     return b;
+}
+
+// TrainStep's per-minibatch numerator upload (chain_loss.go:44-97) without a device-wide
+// stall: host preparation into pinned staging, one asynchronous copy on `stream` into
+// buffers that only grow. The caller orders the copy after every kernel that still reads
+// the batch's previous contents (e.g. `stream` waits for an event recorded after the
+// kf_chain_compute that used it).
+extern "C" int kf_num_batch_refill(KfNumBatch *b, int nseq, const int32_t *state_off,
+                                   const int32_t *arc_off, const int32_t *row_ptr, const int32_t *dst,
+                                   const int32_t *pdf1, const float *logw, const int32_t *final_off,
+                                   const int32_t *final_state, const float *final_logw, void *stream) {
+    if (!b) {
+        kfc_set_error("kf_num_batch_refill: NULL batch");
+        return -1;
+    }
+    std::vector<NumHost> hs;
+    if (!num_hosts("kf_num_batch_refill", nseq, state_off, arc_off, row_ptr, dst, pdf1, logw, final_off,
+                   final_state, final_logw, hs))
+        return -1;
+    std::vector<int32_t> blob;
+    std::vector<std::vector<size_t>> offs;
+    pack_nums(hs, blob, offs);
+    const size_t n = std::max<size_t>(blob.size(), 4);
+    hipStream_t st = stream ? (hipStream_t)stream : kf_stream();
+    if (b->ev_copy) hipEventSynchronize(b->ev_copy);  // h_blob may still feed the last copy
+    else if (hipEventCreateWithFlags(&b->ev_copy, hipEventDisableTiming) != hipSuccess) {
+        kfc_set_error("kf_num_batch_refill: hipEventCreate failed");
+        return -1;
+    }
+    if (n > b->h_cap) {
+        if (b->h_blob) hipHostFree(b->h_blob);
+        b->h_blob = nullptr;
+        b->h_cap = 0;
+        if (hipHostMalloc((void **)&b->h_blob, n * 4, 0) != hipSuccess) {
+            kfc_set_error("kf_num_batch_refill: hipHostMalloc failed");
+            return -1;
+        }
+        b->h_cap = n;
+    }
+    if (n > b->d_cap) {
+        // growing: the old blob (this batch's own, or the create-time one) may still be
+        // read by queued kernels; hipFree waits for the device
+        if (b->d_blob) hipFree(b->d_blob);
+        b->d_blob = nullptr;
+        b->d_cap = 0;
+        if (hipMalloc((void **)&b->d_blob, n * 4) != hipSuccess) {
+            kfc_set_error("kf_num_batch_refill: hipMalloc failed");
+            return -1;
+        }
+        b->d_cap = n;
+    }
+    if (b->nd && !b->nd->owned.empty()) {  // the create-time upload is no longer referenced
+        hipDeviceSynchronize();
+        for (void *p : b->nd->owned) hipFree(p);
+        b->nd->owned.clear();
+    }
+    if (!b->nd) b->nd = new NumDevice();
+    memcpy(b->h_blob, blob.data(), blob.size() * 4);
+    if (hipMemcpyAsync(b->d_blob, b->h_blob, blob.size() * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(b->ev_copy, st) != hipSuccess) {
+        kfc_set_error("kf_num_batch_refill: copy failed");
+        return -1;
+    }
+    num_descs(hs, offs, b->d_blob, b->nd);
+    b->S.clear();
+    for (auto &h : hs) b->S.push_back(h.S);
+    ++b->gen;
+    return 0;
 }
 extern "C" void kf_num_batch_free(KfNumBatch *b) { delete b; }
 
@@ -2701,6 +2929,11 @@ extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max
     ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&c->ev_num, hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < 2; ++i) {
+        ok = ok && hipEventCreateWithFlags(&c->ev_stage[i], hipEventDisableTiming) == hipSuccess;
+        ok = ok && hipHostMalloc((void **)&c->h_stage[i], (size_t)max_seqs * (sizeof(LogFstDev) + 12), 0) ==
+                       hipSuccess;
+    }
     if (!ok) {
         delete c;
         kfc_set_error("kf_chain_create: hipMalloc failed");
@@ -2727,7 +2960,9 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
         return -1;
     }
     hipStream_t st = kf_stream();
-    bool same = c->last_num == num && c->last_nseq == nseq && c->last_stride == stride &&
+    // a refilled numerator batch (kf_num_batch_refill): its copy lands before anything reads it
+    if (num->ev_copy) hipStreamWaitEvent(st, num->ev_copy, 0);
+    bool same = c->last_num == num && c->last_gen == num->gen && c->last_nseq == nseq && c->last_stride == stride &&
                 c->last_nnet == nnet_output && c->last_ld == ld && c->last_rows == num_rows &&
                 std::equal(seq_row0, seq_row0 + nseq, c->last_row0.begin(), c->last_row0.end()) &&
                 std::equal(seq_frames, seq_frames + nseq, c->last_frames.begin(),
@@ -2742,12 +2977,13 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
                               seq_row0[i], stride, num_rows);
                 return -1;
             }
-        hipStreamSynchronize(st);  // the staging vectors may still feed a copy
         size_t ab = 0, ps = 0;
         for (int i = 0; i < nseq; ++i) {
             ab += 2 * (size_t)(seq_frames[i] + 1) * num->S[i];
             ps += (size_t)seq_frames[i] * num->nd->G[i];
         }
+        if ((ab > c->num_ab_cap && c->num_ab) || (ps > c->num_post_cap && c->num_post))
+            hipDeviceSynchronize();  // growing: queued numerator kernels may still use the old buffers
         if (ab > c->num_ab_cap) {
             if (c->num_ab) hipFree(c->num_ab);
             c->num_ab = nullptr;
@@ -2796,10 +3032,29 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
             fits = fits && f.S <= NUM_PRE * NUM_THREADS && f.G <= NUM_PRE * NUM_THREADS;
         }
         c->num_lds = (fits && lds <= 64 * 1024) ? lds : 0;
-        hipMemcpy(c->d_desc, c->host_desc.data(), nseq * sizeof(LogFstDev), hipMemcpyHostToDevice);
-        hipMemcpy(c->d_row0, r0.data(), nseq * 8, hipMemcpyHostToDevice);
-        hipMemcpy(c->d_frames, seq_frames, nseq * 4, hipMemcpyHostToDevice);
+        // asynchronous on st (every earlier reader of d_desc / d_row0 / d_frames is ahead of it
+        // on st: the den kernels, and the numerator kernels through ev_num), from a pinned slot
+        // whose previous copy has retired: no host stall when the batch changes every step
+        const int slot = c->stage_slot;
+        c->stage_slot ^= 1;
+        hipEventSynchronize(c->ev_stage[slot]);
+        char *hs_ = c->h_stage[slot];
+        memcpy(hs_, c->host_desc.data(), nseq * sizeof(LogFstDev));
+        memcpy(hs_ + (size_t)c->max_seqs * sizeof(LogFstDev), r0.data(), nseq * 8);
+        memcpy(hs_ + (size_t)c->max_seqs * (sizeof(LogFstDev) + 8), seq_frames, nseq * 4);
+        bool cp = hipMemcpyAsync(c->d_desc, hs_, nseq * sizeof(LogFstDev), hipMemcpyHostToDevice, st) == hipSuccess;
+        cp = cp && hipMemcpyAsync(c->d_row0, hs_ + (size_t)c->max_seqs * sizeof(LogFstDev), nseq * 8,
+                                  hipMemcpyHostToDevice, st) == hipSuccess;
+        cp = cp && hipMemcpyAsync(c->d_frames, hs_ + (size_t)c->max_seqs * (sizeof(LogFstDev) + 8), nseq * 4,
+                                  hipMemcpyHostToDevice, st) == hipSuccess;
+        cp = cp && hipEventRecord(c->ev_stage[slot], st) == hipSuccess;
+        if (!cp) {
+            c->last_num = nullptr;
+            kfc_set_error("kf_chain_compute: layout upload failed");
+            return -1;
+        }
         c->last_num = num;
+        c->last_gen = num->gen;
         c->last_nseq = nseq;
         c->last_stride = stride;
         c->last_nnet = nnet_output;

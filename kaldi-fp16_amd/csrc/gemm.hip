@@ -169,7 +169,7 @@ __device__ __forceinline__ int mx_exponent(float amax) {
 // parameters go to LDS once per workgroup; then every wave stages its
 // accumulators through its own LDS region 32 rows at a time and each lane owns 8
 // consecutive columns of a row (16-byte global I/O). `smem` must hold
-// 4*BN + 32*(BN/WN + 4)*WM*WN floats; every LDS-DMA into it must have landed.
+// 4*BN + 32*EpiMap<BN/WN>::LDT*WM*WN floats; every LDS-DMA into it must have landed.
 // ---------------------------------------------------------------------------
 // the epilogue's per-column parameters of column n0 + tid, loaded before the K loop so
 // their latency hides under it (KF_EPI_EARLY=0: loaded in the epilogue)
@@ -191,6 +191,34 @@ __device__ __forceinline__ EpiPre epi_params(const KfEpilogue &E, int N, int n0,
     }
     return p;
 }
+
+// Epilogue item map and fp32 staging layout of a wave's 32-row chunk. Item k of a lane is
+// (row r, 8-column group cg); the lane reads columns 8cg .. 8cg+7 of row r as two 16-byte
+// LDS reads and owns them for the global I/O (CG consecutive lanes cover a row's 16 * CG
+// contiguous bytes). Rows of WTN + 4 dwords, except for WTN = 64 (the conv halo tiles and
+// the 256x256 / 128x128 / 256x64 GEMM tiles): rows of 64 dwords with 16-byte unit u of row r
+// at u ^ xr(r), which makes both the accumulator stores and the 16-byte reads bank-conflict
+// free (scripts/epi_lds_check.py; the padded rows are 2-way conflicted on the reads: with
+// 8-column items a row covers only every other 16-byte unit). For WTN = 32 / 48 (the 80 KB
+// 192x128 / 128x192 tiles) the conflicts stay: r5 measured a conflict-free form (the MFMAs
+// producing C^T, one 16-byte store per accumulator, rows of 48 dwords, 4-lane row runs) at
+// +6 % on the TDNN-F input gradient (257 -> 272 us: its 32-byte global row runs for the last
+// 16 columns cost more than the LDS cycles saved), and an XOR mixing lane and loop-index
+// bits at 18 more VGPRs (the second workgroup per CU lost, +50 %).
+template <int WTN>
+struct EpiMap {
+    static constexpr int CG = WTN / 8;
+    static constexpr bool SWZ = WTN == 64;
+    static constexpr int LDT = SWZ ? 64 : WTN + 4;
+    __device__ __forceinline__ static int row(int k, int lane) { return (lane + 64 * k) / CG; }
+    __device__ __forceinline__ static int cg(int k, int lane) { return (lane + 64 * k) % CG; }
+    __device__ __forceinline__ static int xr(int r) { return ((r >> 1) & 1) | (((r >> 2) & 1) << 2); }
+    // dword offset of column c of row r
+    __device__ __forceinline__ static int off(int r, int c) {
+        if constexpr (SWZ) return r * LDT + 4 * ((c >> 2) ^ xr(r)) + (c & 3);
+        else return r * LDT + c;
+    }
+};
 
 template <int BM, int BN, int WM, int WN>
 __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN / WN / 16], char *smem,
@@ -214,7 +242,8 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
     }
     __syncthreads();
     const EpiCols P{prm, prm + BN, prm + 2 * BN, prm + 3 * BN};
-    constexpr int LDT = WTN + 4;
+    using EM = EpiMap<WTN>;
+    constexpr int LDT = EM::LDT;
     float *st = prm + 4 * BN + wave * 32 * LDT;
     constexpr int CG = WTN / 8;
     constexpr int ITEMS = 32 * CG / 64;
@@ -234,7 +263,7 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
         constexpr int icp = decltype(ICc)::value, sl = icp % NSL;
         static_for<ITEMS>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+            const int r = EM::row(k, lane), cg = EM::cg(k, lane);
             const int m = m0 + wm * WTM + icp * 32 + r, n = n0 + wn * WTN + 8 * cg;
             rres[sl][k] = half8{};
             if (m < M && n < N && E.resid) rres[sl][k] = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
@@ -244,7 +273,7 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
         constexpr int icp = decltype(ICc)::value, sl = icp & 1;
         static_for<ITEMS>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+            const int r = EM::row(k, lane), cg = EM::cg(k, lane);
             const int m = m0 + wm * WTM + icp * 32 + r, n = n0 + wn * WTN + 8 * cg;
             const bool ok = m < M && n < N;
             cold[sl][k] = half8{};
@@ -264,7 +293,7 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
                 const int c = J * 16 + (lane & 15);
                 static_for<4>([&](auto EI) {
                     const int r = I2 * 16 + 4 * (lane >> 4) + EI;
-                    st[r * LDT + c] = acc[2 * ic + I2][J][decltype(EI)::value];
+                    st[EM::off(r, c)] = acc[2 * ic + I2][J][decltype(EI)::value];
                 });
             });
         });
@@ -273,14 +302,14 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         static_for<ITEMS>([&](auto K) {
             constexpr int k = decltype(K)::value;
-            const int it = lane + 64 * k, r = it / CG, cg = it - r * CG;
+            const int r = EM::row(k, lane), cg = EM::cg(k, lane);
             const int nl = wn * WTN + 8 * cg;
             const int m = m0 + wm * WTM + ic * 32 + r, n = n0 + nl;
             const bool live = m < M && n < N;
             float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             if (live) {
-                float4v x0 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg);
-                float4v x1 = *reinterpret_cast<const float4v *>(st + r * LDT + 8 * cg + 4);
+                float4v x0 = *reinterpret_cast<const float4v *>(st + EM::off(r, 8 * cg));
+                float4v x1 = *reinterpret_cast<const float4v *>(st + EM::off(r, 8 * cg + 4));
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     v[e] = x0[e];
@@ -336,7 +365,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     constexpr int LPT = SA::NC + SB::NC + (F8 ? SCS::SPW : 0);  // LDS-DMA per thread per stage
     static_assert((SA::EVEN && SB::EVEN) || ST == 2, "uneven stagers need the vmcnt(0) ring");
     static_assert(ST >= 2 && ST <= 4, "stages");
-    static_assert(4 * BN * 4 + (32 * (WTN + 4) * 4) * NW <= SmemSize<BM, BN, ST, SCB>::bytes,
+    static_assert(WGRAD || 4 * BN * 4 + (32 * EpiMap<WTN>::LDT * 4) * NW <= SmemSize<BM, BN, ST, SCB>::bytes,
                   "epilogue staging");
 
     __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, ST, SCB>::bytes];
@@ -1170,7 +1199,7 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     const int BM_ = residue ? 128 : 256;
     H.nf = (BM_ - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
     const int nw = BN_ == 64 ? 4 : 8;
-    const size_t epi = 16 * BN_ + 32 * (64 + 4) * 4 * nw;
+    const size_t epi = 16 * BN_ + 32 * EpiMap<64>::LDT * 4 * nw;
     // LDS of a halo geometry: two images when there are several channel chunks, else one
     // (two too large, e.g. cnn5's stride-2 forward: 80 KB each beside a 64 KB B ring: one
     // image, reloaded between channel chunks)
@@ -1188,11 +1217,13 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     const size_t lds0 = geometry(hpe0, nb0, hb0);
     // hpos = hout (mod 8): conflict-free fragment reads across frame boundaries (halo_off),
     // taken when it keeps the image count and the workgroups per CU (80 KB: two)
+    // (bounded: with hmul = 2 and an odd hout no pitch qualifies, so no pad is taken)
     int hpe = hpe0;
-    while ((hpe * a.hmul - a.hout) % 8) ++hpe;
-    int nb1, hb1;
-    const size_t lds1 = geometry(hpe, nb1, hb1);
-    const bool pad8 = lds1 <= 160 * 1024 && nb1 == nb0 && (lds0 > 80 * 1024 || lds1 <= 80 * 1024);
+    while (hpe < hpe0 + 8 && (hpe * a.hmul - a.hout) % 8) ++hpe;
+    const bool found8 = (hpe * a.hmul - a.hout) % 8 == 0;
+    int nb1 = nb0, hb1 = hb0;
+    const size_t lds1 = found8 ? geometry(hpe, nb1, hb1) : lds0;
+    const bool pad8 = found8 && lds1 <= 160 * 1024 && nb1 == nb0 && (lds0 > 80 * 1024 || lds1 <= 80 * 1024);
     if (!pad8) hpe = hpe0;
     H.hpe = hpe;
     H.hpos = hpe * a.hmul;
@@ -1365,6 +1396,16 @@ void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int 
 int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
                            float *bias_grad, int accumulate);
 
+// A/B experiment bits (KF_EXPT in the environment, read once; 0 = the measured default)
+int kf_expt() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("KF_EXPT");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
 extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              float *dW, long long ldw, float *bias_grad, int accumulate) {
     if (M <= 0 || N <= 0) return 0;
@@ -1393,6 +1434,13 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
             if (w < bw) bw = w, BMc = c;
         }
     }
+    // experiments: two workgroups per CU (74 KB of LDS each) for the TDNN-F weight gradients,
+    // a quarter of the splits per tile count -> a quarter of the fp32 slab bytes
+    if ((kf_expt() & 1) && BNc == 256 && M % 160 == 0 && M <= 320 && N % 128 == 0) {
+        BMc = 160;
+        BNc = 128;
+    }
+    if ((kf_expt() & 2) && BNc == 160) BMc = 128;
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
     // workgroups per launch: every split writes an M x N fp32 slab that the reduce
     // reads back, so the target trades CU fill against slab traffic
@@ -1435,6 +1483,10 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
             rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BMc == 256 && BNc == 128)                                                       \
             rc = launch<256, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 160 && BNc == 128)                                                       \
+            rc = launch<160, 128, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 128 && BNc == 160)                                                       \
+            rc = launch<128, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 160)                                                                     \
             rc = launch<384, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else                                                                                     \

@@ -1406,9 +1406,11 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
                 E.out = g_out;
                 E.ldo = w;
             }
-            // MXFP8 train step: also the e4m3 copy of dz_P for P's affine input gradient
+            // MXFP8 train step: also the e4m3 copy of dz_P for P's affine input gradient; only
+            // when the copy's row is exactly w wide (w % 128 == 0), so the dgrad GEMM's K range
+            // holds no stale codes from a wider layer's copy
             const int i = dz_out == net->dz[0] ? 0 : dz_out == net->dz[1] ? 1 : -1;
-            if (net->fp8 && i >= 0 && w % 32 == 0 && pl.w8d.q && net->dz8[i].q && net->dz8[i].ld == pad128(w)) {
+            if (net->fp8 && i >= 0 && w % 128 == 0 && pl.w8d.q && net->dz8[i].q && net->dz8[i].ld == w) {
                 E.out8 = net->dz8[i].q;
                 E.ldo8 = net->dz8[i].ld;
                 E.scale8 = net->dz8[i].s;

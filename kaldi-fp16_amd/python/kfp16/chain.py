@@ -59,6 +59,7 @@ _sig("kf_den_graph_create", _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp)
 _sig("kf_den_graph_initial_probs", _i, _vp, _vp)
 _sig("kf_den_graph_free", None, _vp)
 _sig("kf_num_batch_create", _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp)
+_sig("kf_num_batch_refill", _i, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp)
 _sig("kf_num_batch_free", None, _vp)
 _sig("kf_chain_create", _vp, _vp, _i, _i)
 _sig("kf_chain_free", None, _vp)
@@ -147,16 +148,29 @@ def pack_num_fsts(fsts) -> dict:
                 final_w=_a(np.concatenate(fw), np.float32))
 
 
+_NUM_KEYS = ("state_off", "arc_off", "row_ptr", "dst", "pdf1", "logw", "final_off", "final_state", "final_w")
+
+
 class NumBatch:
+    """Numerator FSTs of one minibatch on the device. `fsts`: per-eg CSR dicts, or the
+    arrays of pack_num_fsts."""
+
     def __init__(self, fsts):
-        p = pack_num_fsts(fsts)
+        p = fsts if isinstance(fsts, dict) else pack_num_fsts(fsts)
         self.nseq = p["nseq"]
         self._keep = p
-        self.h = core.kf_num_batch_create(
-            self.nseq, *[p[k].ctypes.data for k in ("state_off", "arc_off", "row_ptr", "dst", "pdf1",
-                                                      "logw", "final_off", "final_state", "final_w")])
+        self.h = core.kf_num_batch_create(self.nseq, *[p[k].ctypes.data for k in _NUM_KEYS])
         if not self.h:
             _raise("kf_num_batch_create")
+
+    def refill(self, fsts, stream=None):
+        """The next minibatch's FSTs into this batch (kf_num_batch_refill): asynchronous on
+        `stream` (a HIP stream handle, None: the library stream), no device-wide stall."""
+        p = fsts if isinstance(fsts, dict) else pack_num_fsts(fsts)
+        if core.kf_num_batch_refill(self.h, p["nseq"], *[p[k].ctypes.data for k in _NUM_KEYS], stream) != 0:
+            _raise("kf_num_batch_refill")
+        self.nseq = p["nseq"]
+        self._keep = p   # the host arrays were staged (pinned copy) before the call returned
 
     def close(self):
         if self.h:

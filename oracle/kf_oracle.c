@@ -641,16 +641,16 @@ static float *colsum(const float *g, int rows, int D) {
 }
 
 /* the layers whose affine input gradient the MXFP8 train step runs in e4m3: strided
-   TDNN-F layers with out_dim % 32 == 0 and as wide (padded to 128) as the widest strided
-   TDNN-F layer (network.cpp: the dz copies are allocated that wide) */
+   TDNN-F layers with out_dim % 128 == 0 and as wide as the widest strided TDNN-F layer
+   (network.cpp: the dz copies are allocated that wide; no padding columns) */
 static int mx_dgrad_layer(const OrcNet *net, int li) {
     const OrcLayer *L = &net->layers[li];
-    if (L->type != ORC_TDNNF || L->stride <= 0 || L->out_dim % 32) return 0;
+    if (L->type != ORC_TDNNF || L->stride <= 0 || L->out_dim % 128) return 0;
     int w = 0;
     for (int j = 0; j < net->nlayers; ++j)
         if (net->layers[j].type == ORC_TDNNF && net->layers[j].stride > 0 && net->layers[j].out_dim > w)
             w = net->layers[j].out_dim;
-    return (L->out_dim + 127) / 128 == (w + 127) / 128;
+    return L->out_dim == (w + 127) / 128 * 128;
 }
 
 /*
