@@ -471,6 +471,7 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         ev_copied = [torch.cuda.Event() for _ in range(2)]
         ev_conv = [torch.cuda.Event() for _ in range(2)]
         ev_obj = [torch.cuda.Event() for _ in range(2)]
+        ev_fwd = torch.cuda.Event()   # this step's forward done: the den recursion runs next
         for nb in nums:   # the first refill frees the create-time upload (one device sync), untimed
             nb.refill(packs[0], copy.cuda_stream)
         torch.cuda.synchronize()
@@ -481,6 +482,10 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
             sl = i % 2
             copy.wait_event(ev_conv[sl])    # the slot's fp32 features were converted (step i - 2)
             copy.wait_event(ev_obj[sl])     # the slot's numerator was used (step i - 2)
+            # and not before step i - 1's forward has finished: the copies then run under its
+            # den recursion (latency-bound, ~5 ms). Issued whenever the host got there, they
+            # sometimes landed under the den posteriors, which then took ~0.9 ms longer.
+            copy.wait_event(ev_fwd)
             with torch.cuda.stream(copy):
                 f32[sl].copy_(host[i % npool], non_blocking=True)
                 ev_copied[sl].record(copy)
@@ -507,6 +512,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
             net.forward_ivector(fptr, T, ibuf.data_ptr(), seq_off)
         else:
             net.forward(fptr, T)
+        if h2d:
+            ev_fwd.record(comp)
         if mode == "forward":
             return
         objective.compute(num, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)

@@ -93,10 +93,13 @@ void *nnet_weight_buffer(KfNet *net);
  * copies at the next forward, MXFP8 copies now) */
 int nnet_weights_changed(KfNet *net);
 int nnet_sgd(KfNet *net, float lr, float momentum);
-/* MXFP8 forward (BASELINE configs[4]): 1 = every TDNN-F / linear / prefinal / output
+/* MXFP8 train step (BASELINE configs[4]): 1 = every TDNN-F / linear / prefinal / output
  * GEMM whose input has an MXFP8 copy runs on the fp8 MFMA (kf_ops.h MXFP8 operands);
  * the producing epilogues write those copies, weights are re-quantised on every
- * parameter change. Backward stays fp16 (it reads the fp16 activations). 0 = off. */
+ * parameter change; in the backward the strided TDNN-F affine input gradients run on
+ * e4m3 copies of dz (written by the layer above's input-gradient epilogue) and of W2,
+ * everything else stays fp16. 2 = the same forward with an all-fp16 backward (a test
+ * knob). 0 = off. */
 int nnet_set_fp8(KfNet *net, int on);
 
 /* Data parallel (kf_dp.h). nnet_bind_dp: nnet_backward exchanges the

@@ -526,8 +526,7 @@ static size_t den_rec_fixed_bytes(int P, int nsl, int spg, int ns) {
 // posteriors: the alpha' and beta rows of `pair` frames in the f / b tables' slice orders
 // (rs = nsl * 64 entries each), the gamma rows and the q table's perm / len / off
 static size_t den_post_lds_bytes(int rs, int P, int nslq, int pair = 1) {
-    (void)nslq;  // (the q-table metadata is read from global memory)
-    return (size_t)4 * (64 + 2 * (size_t)pair * rs + (size_t)pair * P);
+    return (size_t)4 * (64 + 2 * (size_t)pair * rs + (size_t)pair * P + (size_t)nslq * 66);
 }
 
 // ---------------------------------------------------------------------------
@@ -782,73 +781,6 @@ __device__ __forceinline__ void sell_slice(const uint2 *arcs, int len, int off, 
     }
 }
 
-// The wave's slices of a SELL table (slots k = wave, wave + DEN_WAVES, ... of `slot`),
-// gather-summed in slot order with the same per-slice arithmetic as sell_slice. PIPE = 0:
-// sell_slice per slice (8 records loaded, then gathered). PIPE = 1: 4-record batches, the
-// next batch (the slice's rest, else the next slice's first) loaded before the current one
-// is gathered, so the L2 round trip of the record stream opens only the wave's first batch
-// (same registers: 2 x 4 records in flight instead of 8). pre(j) runs when slice j starts
-// (its result is handed to post), post(j, pre, acc) after its last record.
-template <int NS, int PIPE, class Pre, class Post>
-__device__ __forceinline__ void sell_walk(const uint2 *arcs, const int *len, const int *off, const int *slot,
-                                          int spg, int lane, int wave, const unsigned char *sv,
-                                          const unsigned char *sx, Pre pre, Post post) {
-    if constexpr (PIPE == 0) {
-        for (int k = wave; k < spg; k += DEN_WAVES) {
-            const int j = slot[k];
-            if (j < 0) continue;
-            const float pv = pre(j);
-            float acc[NS];
-            sell_slice<NS>(arcs, len[j], off[j], lane, sv, sx, acc);
-            post(j, pv, acc);
-        }
-    } else {
-#pragma clang fp contract(off)  // (a * tp) * x + acc rounded as the oracle does, any NS
-        auto nxt_slot = [&](int k) {
-            while (k < spg && slot[k] < 0) k += DEN_WAVES;
-            return k;
-        };
-        auto ld4 = [&](uint2 (&r)[4], int o, int k) {
-            const uint2 *e = arcs + ((size_t)o * 64 + lane) + (size_t)k * 64;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) r[i] = e[i * 64];
-        };
-        int k = nxt_slot(wave);
-        uint2 cur[4];
-        if (k < spg) ld4(cur, off[slot[k]], 0);
-        while (k < spg) {
-            const int j = slot[k];
-            const int n = len[j], o = off[j];
-            const int kn = nxt_slot(k + DEN_WAVES);
-            const float pv = pre(j);
-            float acc[NS];
-#pragma unroll
-            for (int q = 0; q < NS; ++q) acc[q] = 0.f;
-            for (int b = 0; b < n; b += 4) {
-                uint2 nx[4];
-                if (b + 4 < n) ld4(nx, o, b + 4);
-                else if (kn < spg) ld4(nx, off[slot[kn]], 0);
-                DenV<NS> a[4], x[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    a[i] = lds_v<NS>(sv, cur[i].x & 0xFFFF);
-                    x[i] = lds_v<NS>(sx, cur[i].x >> 16);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float tp = __uint_as_float(cur[i].y);
-#pragma unroll
-                    for (int q = 0; q < NS; ++q) acc[q] += a[i].x[q] * tp * x[i].x[q];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) cur[i] = nx[i];
-            }
-            post(j, pv, acc);
-            k = kn;
-        }
-    }
-}
-
 // Per-block SELL state: len / off of every slice and this block's slot list (slot k is
 // processed by wave k % DEN_WAVES; -1 = empty) in LDS; initp stays in global memory
 // (L2-resident, read once per position per frame), which keeps the NS = 2 recursion small
@@ -916,7 +848,7 @@ __device__ __forceinline__ void den_put_exp(float *xe, int P, const RowPre<XT> (
 // the exchange: all blocks rebuild the full alpha'[t+1] in LDS from those rows. The store
 // keeps the slices before the leaky term: alpha'[t] = row[t] + asum[t] * leaky * init,
 // which k_den_post applies when it loads the row (one write per frame, not two).
-template <typename XT, bool LOC, int NS, int PIPE = 0>
+template <typename XT, bool LOC, int NS>
 __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, const DenX &X,
                                              unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -993,16 +925,19 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         }
         const int buf = (t + 1) & 1;
         float *tail = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
-        sell_walk<NS, PIPE>(arcs, F.len, F.off, F.slot, spg, lane, wave, sv, sx, [&](int) { return 0.f; },
-                            [&](int j, float, const float (&acc)[NS]) {
-                                const bool real = j * 64 + lane < S;  // padding positions stay 0
+        for (int k = wave; k < spg; k += DEN_WAVES) {
+            const int j = F.slot[k];
+            if (j < 0) continue;
+            const bool real = j * 64 + lane < S;  // padding positions stay 0
+            float acc[NS];
+            sell_slice<NS>(arcs, F.len[j], F.off[j], lane, sv, sx, acc);
 #pragma unroll
-                                for (int q = 0; q < NS; ++q) {
-                                    const float v = real ? acc[q] * inv[q] : 0.0f;
-                                    if (live[q]) x_st<LOC>(arow[q], j * 64 + lane, v);
-                                    pq[q] += v;
-                                }
-                            });
+            for (int q = 0; q < NS; ++q) {
+                const float v = real ? acc[q] * inv[q] : 0.0f;
+                if (live[q]) x_st<LOC>(arow[q], j * 64 + lane, v);
+                pq[q] += v;
+            }
+        }
         if (r.trace && unit == 0 && gi < 2 && lane == 0 && t >= 16 && t < 48)  // per-wave arc end, blocks 0, 1
             r.trace[256 + ((t - 16) * 2 + gi) * DEN_WAVES + wave] = wall_clock64();
         DEN_TP(1);
@@ -1091,7 +1026,7 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fwd(const DenDev g, const D
 // frame (the den posteriors of a frame sum to one: they are d log p / d x_t), so this
 // pass scales by 1/<init, beta'[t+1]> and starts from ones — it needs nothing from the
 // forward pass and runs beside it. Iteration `it` is frame T_q - 1 - it of sequence q.
-template <typename XT, bool LOC, int NS, int PIPE = 0>
+template <typename XT, bool LOC, int NS>
 __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, const DenX &X,
                                              unsigned char *smem, int unit, int gi) {
     const int S = g.S, P = g.P, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1162,18 +1097,20 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
         }
         const int buf = it & 1;
         float *tail = X.buf + (((size_t)unit * 2 + buf) * G + gi) * X.blk;
-        // kernel_den_backward_transitions
-        sell_walk<NS, PIPE>(arcs, B.len, B.off, B.slot, spg, lane, wave, sv, sx,
-                            [&](int j) { return B.initp[j * 64 + lane]; },
-                            [&](int j, float ip, const float (&acc)[NS]) {
-                                const bool real = j * 64 + lane < S;  // padding positions stay 0
+        for (int k = wave; k < spg; k += DEN_WAVES) {  // kernel_den_backward_transitions
+            const int j = B.slot[k];
+            if (j < 0) continue;
+            const bool real = j * 64 + lane < S;  // padding positions stay 0
+            const float ip = B.initp[j * 64 + lane];
+            float acc[NS];
+            sell_slice<NS>(arcs, B.len[j], B.off[j], lane, sv, sx, acc);
 #pragma unroll
-                                for (int q = 0; q < NS; ++q) {
-                                    const float bd = real ? acc[q] * inv[q] : 0.0f;
-                                    if (live[q]) x_st<LOC>(brow[q], j * 64 + lane, bd);
-                                    pq[q] += ip * bd;
-                                }
-                            });
+            for (int q = 0; q < NS; ++q) {
+                const float bd = real ? acc[q] * inv[q] : 0.0f;
+                if (live[q]) x_st<LOC>(brow[q], j * 64 + lane, bd);
+                pq[q] += ip * bd;
+            }
+        }
         float ws[NS];
 #pragma unroll
         for (int q = 0; q < NS; ++q) ws[q] = wave_sum(pq[q]);
@@ -1212,7 +1149,7 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
 // independent, see den_bwd_body). One launch keeps all 2*units*G blocks co-resident,
 // which the bounded exchange polls rely on; the XCD grouping of den_map is kept (G
 // consecutive ids share an XCD).
-template <typename XT, int NS, int PIPE = 0>
+template <typename XT, int NS>
 __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const DenRun r, const DenX XF,
                                                         const DenX XB) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1228,11 +1165,11 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
     const int loc = den_xcd_local(bwd ? XB : XF, unit, reinterpret_cast<int *>(smem) + 32);
     if (loc < 0) return;  // timed out (reported through the timeout words)
     if (bwd) {
-        if (loc) den_bwd_body<XT, true, NS, PIPE>(g, r, XB, smem, unit, gi);
-        else den_bwd_body<XT, false, NS, PIPE>(g, r, XB, smem, unit, gi);
+        if (loc) den_bwd_body<XT, true, NS>(g, r, XB, smem, unit, gi);
+        else den_bwd_body<XT, false, NS>(g, r, XB, smem, unit, gi);
     } else {
-        if (loc) den_fwd_body<XT, true, NS, PIPE>(g, r, XF, smem, unit, gi);
-        else den_fwd_body<XT, false, NS, PIPE>(g, r, XF, smem, unit, gi);
+        if (loc) den_fwd_body<XT, true, NS>(g, r, XF, smem, unit, gi);
+        else den_fwd_body<XT, false, NS>(g, r, XF, smem, unit, gi);
     }
 }
 
@@ -1245,34 +1182,25 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_fb(const DenDev g, const De
 #define POST_FRAMES 2  // frames per block (one two-frame pass: 1.82 -> 1.76 ms against 4)
 // records carry LDS byte offsets into the PAIR-interleaved alpha' / beta rows (one
 // 8-byte gather per operand serves both frames)
-// Record pipeline of one wave over its slices of a SELL table: the next 8 records (the
-// rest of this slice, else the first of the wave's next slice) are loaded before the
-// current 8 are gathered and summed, so an L2 round trip hides under a batch's work instead
-// of opening every batch (k_den_post was bound by those round trips: ~30 batches per wave,
-// one exposed L2 latency each).
-struct RecBatch {
-    uint2 r[8];
-    __device__ __forceinline__ void load(const uint2 *arcs, int off, int k, int lane) {
-        const uint2 *e = arcs + ((size_t)off * 64 + lane) + (size_t)k * 64;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = e[i * 64];
-    }
-};
-// slot list walk of one wave: the next non-empty slot at or after k (stride DEN_WAVES)
-__device__ __forceinline__ int next_slot(const int *slot, int k, int spg) {
-    while (k < spg && slot[k] < 0) k += DEN_WAVES;
-    return k;
-}
 template <int PAIR>
-__device__ __forceinline__ void post_batch(const RecBatch &b, const unsigned char *sva, const unsigned char *svb,
-                                           float acc[PAIR]) {
+__device__ __forceinline__ void post_slice(const uint2 *arcs, int len, int off, int lane,
+                                           const unsigned char *sva, const unsigned char *svb, float acc[PAIR]) {
 #pragma clang fp contract(off)  // (alpha * tp) * beta + acc, as the oracle rounds
+    const uint2 *e = arcs + (size_t)off * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const DenV<PAIR> a = lds_v<PAIR>(sva, b.r[i].x & 0xFFFF), v = lds_v<PAIR>(svb, b.r[i].x >> 16);
-        const float tp = __uint_as_float(b.r[i].y);
+    for (int f = 0; f < PAIR; ++f) acc[f] = 0.f;
+    // (16 records in flight instead of 8: 1738 -> 1812 us per launch, r5)
+    for (int k = 0; k < len; k += 8) {
+        uint2 rr[8];
 #pragma unroll
-        for (int f = 0; f < PAIR; ++f) acc[f] += a.x[f] * tp * v.x[f];
+        for (int i = 0; i < 8; ++i) rr[i] = e[(k + i) * 64];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const DenV<PAIR> a = lds_v<PAIR>(sva, rr[i].x & 0xFFFF), b = lds_v<PAIR>(svb, rr[i].x >> 16);
+            const float tp = __uint_as_float(rr[i].y);
+#pragma unroll
+            for (int f = 0; f < PAIR; ++f) acc[f] += a.x[f] * tp * b.x[f];
+        }
     }
 }
 template <typename XT, int MODE, int PAIR>
@@ -1286,10 +1214,13 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
     float *va = reinterpret_cast<float *>(smem) + 64;  // [rsf][PAIR] alpha'[t+f], f-table slice order
     float *vb = va + PAIR * rsf;                       // [rsb][PAIR] beta[t+f+1], b-table slice order
     float *gam = vb + PAIR * rsb;                      // [PAIR][P] den, then the gradient
-    // the q table's slice metadata stays in global memory (L2): one load per slice per wave
-    // (copying it to LDS cost every block 13 KB of L2 reads and LDS writes)
-    const int *permq = g.q.perm, *lenq = g.q.len, *offq = g.q.off;
-    (void)nslq;
+    int *metaq = reinterpret_cast<int *>(gam + PAIR * P);
+    const int *permq = metaq, *lenq = metaq + nslq * 64, *offq = metaq + nslq * 65;
+    for (int i = tid; i < nslq * 64; i += DEN_THREADS) metaq[i] = g.q.perm[i];
+    for (int i = tid; i < nslq; i += DEN_THREADS) {
+        metaq[nslq * 64 + i] = g.q.len[i];
+        metaq[nslq * 65 + i] = g.q.off[i];
+    }
 
     const int T = r.frames[seq];
     const int t0 = fb * POST_FRAMES, t1 = min(T, t0 + POST_FRAMES);
@@ -1383,29 +1314,13 @@ __global__ __launch_bounds__(DEN_THREADS) void k_den_post(const DenDev g, const 
         float gpart[PAIR];
 #pragma unroll
         for (int f = 0; f < PAIR; ++f) gpart[f] = 0.f;
-        const int *slotq = g.q.slot[0];
-        const int spgq = g.q.spg[0];
-        const uint2 *arcs = g.q.arc_p[PAIR - 1];
-        int k = next_slot(slotq, wave, spgq);
-        RecBatch cur;
-        if (k < spgq) cur.load(arcs, offq[slotq[k]], 0, lane);
-        while (k < spgq) {
-            const int j = slotq[k];
-            const int len = lenq[j], off = offq[j];
-            const int kn = next_slot(slotq, k + DEN_WAVES, spgq);
+        for (int k = wave; k < g.q.spg[0]; k += DEN_WAVES) {
+            const int j = g.q.slot[0][k];
+            if (j < 0) continue;
             const int pdf = permq[j * 64 + lane];
             float acc[PAIR];
-#pragma unroll
-            for (int f = 0; f < PAIR; ++f) acc[f] = 0.f;
-            for (int b = 0; b < len; b += 8) {  // len is a multiple of 8
-                RecBatch nxt;
-                if (b + 8 < len) nxt.load(arcs, off, b + 8, lane);
-                else if (kn < spgq) nxt.load(arcs, offq[slotq[kn]], 0, lane);
-                post_batch<PAIR>(cur, reinterpret_cast<const unsigned char *>(va),
-                                 reinterpret_cast<const unsigned char *>(vb), acc);
-                cur = nxt;
-            }
-            k = kn;
+            post_slice<PAIR>(g.q.arc_p[PAIR - 1], lenq[j], offq[j], lane, reinterpret_cast<const unsigned char *>(va),
+                             reinterpret_cast<const unsigned char *>(vb), acc);
             if (pdf < 0) continue;
 #pragma unroll
             for (int f = 0; f < PAIR; ++f) {
@@ -1897,8 +1812,6 @@ void launch_den_fb(const DenDev &g, const DenRun &r, const DenX &XF, DenXBuf &xf
     dim3 grid(2 * XF.nseq * XF.G);
     const size_t lds = std::max(XF.lds_f, XB.lds_b);
     if (fp32_in) hipLaunchKernelGGL((k_den_fb<float, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
-    else if (XF.ns == 2 && (kf_expt() & 4))
-        hipLaunchKernelGGL((k_den_fb<h16, 2, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
     else if (XF.ns == 2) hipLaunchKernelGGL((k_den_fb<h16, 2>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
     else hipLaunchKernelGGL((k_den_fb<h16, 1>), grid, dim3(DEN_THREADS), lds, st, g, r, XF, XB);
 }
@@ -2727,8 +2640,7 @@ struct KfChain {
         if (den_out) hipFree(den_out);
         for (void *p : {(void *)alpha_store, (void *)beta_store, (void *)asum_store, (void *)bsum_store,
                         (void *)stats, (void *)num_ab,
-                        (void *)num_post, (void *)d_desc, (void *)d_row0, (void *)d_frames,
-                        (void *)d_num_total})
+                        (void *)num_post, (void *)d_desc, (void *)d_num_total})
             if (p) hipFree(p);
     }
 };
@@ -2921,9 +2833,13 @@ extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max
     ok = ok && hipMalloc(&c->asum_store, (size_t)max_seqs * (max_frames + 1) * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->bsum_store, (size_t)max_seqs * (max_frames + 1) * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->stats, (size_t)max_seqs * 8 * 4) == hipSuccess;
-    ok = ok && hipMalloc(&c->d_desc, (size_t)max_seqs * sizeof(LogFstDev)) == hipSuccess;
-    ok = ok && hipMalloc(&c->d_row0, (size_t)max_seqs * 8) == hipSuccess;
-    ok = ok && hipMalloc(&c->d_frames, (size_t)max_seqs * 4) == hipSuccess;
+    // descriptors, row offsets and frame counts in one allocation, laid out as the pinned
+    // staging slot, so a layout change is one copy
+    ok = ok && hipMalloc(&c->d_desc, (size_t)max_seqs * (sizeof(LogFstDev) + 12)) == hipSuccess;
+    if (ok) {
+        c->d_row0 = reinterpret_cast<long long *>(reinterpret_cast<char *>(c->d_desc) + (size_t)max_seqs * sizeof(LogFstDev));
+        c->d_frames = reinterpret_cast<int *>(reinterpret_cast<char *>(c->d_row0) + (size_t)max_seqs * 8);
+    }
     ok = ok && hipMalloc(&c->d_num_total, (size_t)max_seqs * 4) == hipSuccess;
     ok = ok && hipMalloc(&c->den_out, (size_t)max_seqs * 8) == hipSuccess;
     ok = ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess;
@@ -3042,11 +2958,8 @@ extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChain
         memcpy(hs_, c->host_desc.data(), nseq * sizeof(LogFstDev));
         memcpy(hs_ + (size_t)c->max_seqs * sizeof(LogFstDev), r0.data(), nseq * 8);
         memcpy(hs_ + (size_t)c->max_seqs * (sizeof(LogFstDev) + 8), seq_frames, nseq * 4);
-        bool cp = hipMemcpyAsync(c->d_desc, hs_, nseq * sizeof(LogFstDev), hipMemcpyHostToDevice, st) == hipSuccess;
-        cp = cp && hipMemcpyAsync(c->d_row0, hs_ + (size_t)c->max_seqs * sizeof(LogFstDev), nseq * 8,
-                                  hipMemcpyHostToDevice, st) == hipSuccess;
-        cp = cp && hipMemcpyAsync(c->d_frames, hs_ + (size_t)c->max_seqs * (sizeof(LogFstDev) + 8), nseq * 4,
-                                  hipMemcpyHostToDevice, st) == hipSuccess;
+        bool cp = hipMemcpyAsync(c->d_desc, hs_, (size_t)c->max_seqs * (sizeof(LogFstDev) + 12),
+                                 hipMemcpyHostToDevice, st) == hipSuccess;
         cp = cp && hipEventRecord(c->ev_stage[slot], st) == hipSuccess;
         if (!cp) {
             c->last_num = nullptr;

@@ -1434,13 +1434,9 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
             if (w < bw) bw = w, BMc = c;
         }
     }
-    // experiments: two workgroups per CU (74 KB of LDS each) for the TDNN-F weight gradients,
-    // a quarter of the splits per tile count -> a quarter of the fp32 slab bytes
-    if ((kf_expt() & 1) && BNc == 256 && M % 160 == 0 && M <= 320 && N % 128 == 0) {
-        BMc = 160;
-        BNc = 128;
-    }
-    if ((kf_expt() & 2) && BNc == 160) BMc = 128;
+    // (r5: two workgroups per CU for the TDNN-F weight gradients, 160x128 / 128x160 tiles at
+    // 72 KB, a quarter of the fp32 slab bytes: affine 121 -> 311 us, linear 126 -> 171 us per
+    // launch, the reduce 25 -> 13 us; the bigger tiles' operand reuse is worth more)
     const int tiles = ((M + BMc - 1) / BMc) * ((N + BNc - 1) / BNc);
     // workgroups per launch: every split writes an M x N fp32 slab that the reduce
     // reads back, so the target trades CU fill against slab traffic
@@ -1483,10 +1479,6 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
             rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BMc == 256 && BNc == 128)                                                       \
             rc = launch<256, 128, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
-        else if (BMc == 160 && BNc == 128)                                                       \
-            rc = launch<160, 128, 2, 4, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
-        else if (BMc == 128 && BNc == 160)                                                       \
-            rc = launch<128, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else if (BNc == 160)                                                                     \
             rc = launch<384, 160, 4, 2, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
         else                                                                                     \

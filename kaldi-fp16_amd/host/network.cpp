@@ -210,6 +210,7 @@ struct KfNet {
     void *dbott = nullptr, *edge = nullptr;
     size_t edge_half = 0;
     int fp8 = 0;
+    int fp8_dgrad = 1;  // nnet_set_fp8(net, 2): MXFP8 forward, fp16 affine input gradients (tests)
     // MXFP8 copies of dz[0] / dz[1] written by the producing input-gradient epilogue
     // (out8_src = 1) for a TDNN-F layer's affine input gradient, and the layer each holds
     Mx dz8[2];
@@ -1048,6 +1049,7 @@ extern "C" int nnet_set_fp8(KfNet *net, int on) {
         net->fp8 = 0;
         return 0;
     }
+    net->fp8_dgrad = on != 2;
     if (!net->fp8) {
         const size_t T = (size_t)net->max_T;
         bool first = true;
@@ -1410,7 +1412,8 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
             // when the copy's row is exactly w wide (w % 128 == 0), so the dgrad GEMM's K range
             // holds no stale codes from a wider layer's copy
             const int i = dz_out == net->dz[0] ? 0 : dz_out == net->dz[1] ? 1 : -1;
-            if (net->fp8 && i >= 0 && w % 128 == 0 && pl.w8d.q && net->dz8[i].q && net->dz8[i].ld == w) {
+            if (net->fp8 && net->fp8_dgrad && i >= 0 && w % 128 == 0 && pl.w8d.q && net->dz8[i].q &&
+                net->dz8[i].ld == w) {
                 E.out8 = net->dz8[i].q;
                 E.ldo8 = net->dz8[i].ld;
                 E.scale8 = net->dz8[i].s;

@@ -645,7 +645,7 @@ static float *colsum(const float *g, int rows, int D) {
    (network.cpp: the dz copies are allocated that wide; no padding columns) */
 static int mx_dgrad_layer(const OrcNet *net, int li) {
     const OrcLayer *L = &net->layers[li];
-    if (L->type != ORC_TDNNF || L->stride <= 0 || L->out_dim % 128) return 0;
+    if (net->mx8 == 2 || L->type != ORC_TDNNF || L->stride <= 0 || L->out_dim % 128) return 0;
     int w = 0;
     for (int j = 0; j < net->nlayers; ++j)
         if (net->layers[j].type == ORC_TDNNF && net->layers[j].stride > 0 && net->layers[j].out_dim > w)

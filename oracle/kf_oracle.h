@@ -100,7 +100,9 @@ typedef struct {
     /* MXFP8 emulation of the GPU's nnet_set_fp8 forward (kf_nnet.h): the dense GEMMs
      * of TDNN-F / linear / prefinal / output layers read quantise-dequantised
      * (OCP MX, blocks of 32 along K) inputs and weights; act8 holds the
-     * quantised copies of producer outputs (taken before the fp16 rounding). */
+     * quantised copies of producer outputs (taken before the fp16 rounding). 1 also
+     * emulates the MXFP8 affine input gradients of the strided TDNN-F layers in the
+     * backward (mx_dgrad_layer), 2 does not (nnet_set_fp8(net, 2)). */
     int mx8;
     float **act8;
     /* ivector input: [B x ivec_dim] rows, frames of sequence s = [seq_off[s], seq_off[s+1]) */

@@ -282,7 +282,7 @@ class OracleNet:
         self.arr = arr
         self.index = index
         self.round_mode = round_mode
-        self.mx8 = bool(mx8)   # emulate the GPU's MXFP8 forward GEMMs (kf_nnet.h nnet_set_fp8)
+        self.mx8 = int(mx8)    # emulate the GPU's MXFP8 step (kf_nnet.h nnet_set_fp8: 1, or 2 = fp16 backward)
         if threads:
             lib().orc_set_threads(int(threads))
         self.net = None
@@ -322,7 +322,7 @@ class OracleNet:
         self.net.T = x.shape[0]
         self.net.feat_dim = x.shape[1]
         self.net.round_mode = self.round_mode
-        self.net.mx8 = int(self.mx8)
+        self.net.mx8 = int(self.mx8)   # 1: MX forward + MX strided affine dgrad; 2: MX forward only
         if ivectors is not None:
             iv = np.ascontiguousarray(ivectors, dtype=np.float32)
             so = np.ascontiguousarray(seq_off, dtype=np.int32)

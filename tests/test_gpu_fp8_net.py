@@ -210,17 +210,21 @@ def test_config5_fp8_layers_isolated(gpu):
     _check_isolated(_isolated_fp8_errors(gpu, synth.load_xconfig("cnn_tdnn_17f_3072.xconfig"), 1500))
 
 
-FP8_GRAD_TOL = 0.15    # weight gradients vs the oracle's MXFP8 emulation (chaotic e4m3 flips, as above)
+# weight gradients vs the oracle's MXFP8 emulation (chaotic e4m3 flips, as above); measured
+# at most 6.3 % (tiny) and 7.2 % (3072 model) with the MXFP8 affine input gradients on (r4)
+FP8_GRAD_TOL = 0.10
 
 
-def _fp8_backward_errors(kfp16, xcfg, T, seed=7):
-    """MXFP8 forward, fp16 backward of a fixed output gradient on the GPU; the oracle
-    replays the GPU's ReLU decisions in its fp16 and its MXFP8-emulating forward and
-    back-propagates the same gradient. Returns ({param: err vs MX emulation},
-    {param: err vs fp16}, the params of layers up to the first fp8 layer)."""
+def _fp8_backward_errors(kfp16, xcfg, T, seed=7, mode=1):
+    """MXFP8 train step on the GPU (nnet_set_fp8 `mode`: 1 = MXFP8 forward and strided
+    TDNN-F affine input gradients, 2 = MXFP8 forward, all-fp16 backward) back-propagating a
+    fixed output gradient; the oracle replays the GPU's ReLU decisions in its fp16 and its
+    MX-emulating step (the same mode) and back-propagates the same gradient. Returns
+    ({param: err vs MX emulation}, {param: err vs fp16}, the params of layers up to the
+    first fp8 layer that no e4m3 backward product reaches)."""
     from kfp16 import synth
     net, params, bns, feats, fbuf = _net(kfp16, xcfg, T)
-    net.set_fp8(True)
+    net.set_fp8(mode)
     net.forward(fbuf.ptr, T)
     masks = net.relu_masks()
     P = net.layers[-1][3]
@@ -232,12 +236,13 @@ def _fp8_backward_errors(kfp16, xcfg, T, seed=7):
     # layers up to the first fp8 layer see no e4m3 flip in the forward, and none in the
     # backward unless an MXFP8 affine input gradient (strided TDNN-F) sits above them: then
     # the chaotic divergence starts there and they get the deep layers' bars
-    mx_dgrad = [i for i, L in enumerate(net.layers) if kfp16.nnet.nnet_debug_tensor(net.h, b"w8dq", i)]
+    mx_dgrad = [i for i, L in enumerate(net.layers)
+                if mode == 1 and kfp16.nnet.nnet_debug_tensor(net.h, b"w8dq", i)]
     early = {L[0] for i, L in enumerate(net.layers[:first + 1]) if not any(j > i for j in mx_dgrad)}
     net.close()
     tp = {k: synth.trunc_fp16(v) for k, v in params.items()}
     refs = []
-    for mx8 in (True, False):
+    for mx8 in (mode, 0):
         on = oracle.OracleNet(xcfg, tp, bns, round_mode=oracle.ROUND_FUSED, threads=16, mx8=mx8)
         on.forward(feats.astype(np.float32), force_masks=masks)
         on.backward(og.astype(np.float32))
@@ -253,7 +258,11 @@ def _check_fp8_grads(emx, e16, early_params, early_tol):
     """every gradient within FP8_GRAD_TOL of the MX emulation; those of layers no e4m3 flip
     reaches within early_tol; the rest no further from the emulation than from fp16"""
     msg = "; ".join(f"{k} {emx[k]:.3g}/{e16[k]:.3g}" for k in emx)
-    print("fp8 backward grad errors (vs MX emulation / vs fp16):", msg)
+    print("\nfp8 backward weight-gradient rel-Frobenius errors (bar: %.2f; early layers %.3g)" %
+          (FP8_GRAD_TOL, early_tol))
+    print("%-28s %12s %12s %s" % ("parameter", "vs MX emul", "vs fp16", "early"))
+    for k in emx:
+        print("%-28s %12.4g %12.4g %s" % (k, emx[k], e16[k], "yes" if k in early_params else ""))
     for k in emx:
         assert emx[k] <= FP8_GRAD_TOL, msg
         if k in early_params:
@@ -265,12 +274,23 @@ def _check_fp8_grads(emx, e16, early_params, early_tol):
 
 
 def test_tiny_fp8_backward(gpu):
-    """configs[4]'s train step runs the fp16 backward on the MXFP8 forward's
-    activations: its weight gradients follow the oracle's MX emulation (replayed ReLU
-    decisions), within the fp16 bar up to the first fp8 layer"""
+    """configs[4]'s train step (MXFP8 forward, MXFP8 strided TDNN-F affine input
+    gradients, the rest of the backward fp16): its weight gradients follow the oracle's
+    MX emulation (replayed ReLU decisions)"""
     from kfp16 import synth
     emx, e16, early = _fp8_backward_errors(gpu, synth.load_xconfig("tiny.xconfig"), 300)
     _check_fp8_grads(emx, e16, early, early_tol=2e-2)
+
+
+def test_tiny_fp8_backward_fp16_dgrad(gpu):
+    """the MXFP8 forward with an all-fp16 backward (nnet_set_fp8 mode 2): no e4m3 rounding
+    reaches the layers up to the first fp8 layer, which then hold the fp16 weight-gradient
+    bar, 5e-3 (the conv and first TDNN-F gradients, measured <= 1.5e-3; with the MXFP8 input
+    gradients on they sit below one and get only the deep layers' bars)"""
+    from kfp16 import synth
+    emx, e16, early = _fp8_backward_errors(gpu, synth.load_xconfig("tiny.xconfig"), 300, mode=2)
+    assert early, "no early layers"
+    _check_fp8_grads(emx, e16, early, early_tol=5e-3)
 
 
 @pytest.mark.slow
@@ -279,6 +299,16 @@ def test_config5_fp8_backward(gpu):
     from kfp16 import synth
     emx, e16, early = _fp8_backward_errors(gpu, synth.load_xconfig("cnn_tdnn_17f_3072.xconfig"), 150)
     _check_fp8_grads(emx, e16, early, early_tol=2e-2)
+
+
+@pytest.mark.slow
+def test_config5_fp8_backward_fp16_dgrad(gpu):
+    """mode 2 on the configs[4] model: the early layers (convs, tdnnf7) within 5e-3
+    (measured <= 3e-3)"""
+    from kfp16 import synth
+    emx, e16, early = _fp8_backward_errors(gpu, synth.load_xconfig("cnn_tdnn_17f_3072.xconfig"), 150, mode=2)
+    assert early, "no early layers"
+    _check_fp8_grads(emx, e16, early, early_tol=5e-3)
 
 
 def _mx_rows(kfp16, q, sc, rows, ld):
