@@ -84,6 +84,8 @@ def parse(argv=None):
                    help="upload the step's inputs once before timing (default: TrainStep's per-minibatch "
                         "feature and numerator upload inside every step, overlapped on a copy stream)")
     p.add_argument("--input-pool", type=int, default=2, help="distinct host minibatches cycled through (h2d)")
+    p.add_argument("--no-wgrad-stream", action="store_true",
+                   help="weight gradients on the main stream (default: their own stream, nnet_set_wgrad_stream)")
     p.add_argument("--fp8", action="store_true",
                    help="MXFP8 forward GEMMs (configs[4]; use with --xconfig cnn_tdnn_17f_3072.xconfig)")
     p.add_argument("--mode", choices=("train", "forward"), default="train",
@@ -427,6 +429,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
     params, bns = synth.init_network(net, seed=42)        # identical replicas on every rank
     if fp8:
         net.set_fp8(True)
+    if a.no_wgrad_stream:
+        net.set_wgrad_stream(False)
     bucket_bytes = int(a.bucket_mb * (1 << 20))
     if comm is not None and mode == "train":
         net.bind_dp(comm, bucket_bytes)                    # bucketed all-reduce inside backward

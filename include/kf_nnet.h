@@ -117,8 +117,16 @@ int nnet_dp_plan(const KfNet *net, long long bucket_bytes, int max_buckets, int 
  * gradient exists: the negative control of the overlap tests (kf_dp_debug). */
 int nnet_dp_debug_early(KfNet *net, int on);
 
+/* Weight gradients on a second stream (default on): nnet_backward launches every dW / db
+ * GEMM (and the data-parallel bucket gates) on a stream of its own, ordered by events after
+ * the producers on the caller's stream, so they overlap the input-gradient chain; the
+ * caller's stream waits for them before nnet_backward returns. 0 = everything on the
+ * caller's stream (the r4 order, A/B and tests). */
+int nnet_set_wgrad_stream(KfNet *net, int on);
+
 /* diagnostics (tests): back-propagate through the top n layers only; device
- * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott", "aux", "mask",
+ * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott" (the buffer of the last
+ * TDNN-F / prefinal step), "aux", "mask",
  * "bn_scale", "bn2_scale", "dproj" (attention: the gradient of its affine output), and with fp8 on "x8q" / "x8s": the e4m3 values
  * [T x pad128(in_dim)] and E8M0 scales [T x pad128(in_dim)/32] of the MXFP8 input copy
  * the layer's GEMM reads; "w8dq" / "w8ds": a strided TDNN-F layer's e4m3 affine weight rows

@@ -109,6 +109,16 @@ typedef struct {
  * (NULL = legacy default stream, the reference's behaviour) */
 void kf_set_stream(void *hip_stream);
 void *kf_get_stream(void);
+/* streams and events for host layers built without HIP headers (libkaldi_fp16_nnet's
+ * weight-gradient stream): a non-blocking stream (NULL on failure), a timing-disabled
+ * event; record / wait return 0 or -1 */
+void *kf_stream_new(void);
+void *kf_stream_new_high(void);  /* the device's highest stream priority */
+void kf_stream_free(void *hip_stream);
+void *kf_event_new(void);
+void kf_event_free(void *hip_event);
+int kf_event_record(void *hip_event, void *hip_stream);
+int kf_stream_wait(void *hip_stream, void *hip_event);
 
 /* C[M x N] = epilogue(A . B^T-style contraction over K) */
 int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,

@@ -15,6 +15,32 @@ KF_DECLARE_ERR(bridge)
 static __thread hipStream_t g_stream = nullptr;
 hipStream_t kf_stream() { return g_stream; }
 extern "C" void kf_set_stream(void *s) { g_stream = (hipStream_t)s; }
+extern "C" void *kf_stream_new(void) {
+    hipStream_t s = nullptr;
+    return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? (void *)s : nullptr;
+}
+extern "C" void *kf_stream_new_high(void) {
+    int least = 0, greatest = 0;
+    hipStream_t s = nullptr;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
+    return hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) == hipSuccess ? (void *)s : nullptr;
+}
+extern "C" void kf_stream_free(void *s) {
+    if (s) hipStreamDestroy((hipStream_t)s);
+}
+extern "C" void *kf_event_new(void) {
+    hipEvent_t e = nullptr;
+    return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess ? (void *)e : nullptr;
+}
+extern "C" void kf_event_free(void *e) {
+    if (e) hipEventDestroy((hipEvent_t)e);
+}
+extern "C" int kf_event_record(void *e, void *s) {
+    return hipEventRecord((hipEvent_t)e, (hipStream_t)s) == hipSuccess ? 0 : -1;
+}
+extern "C" int kf_stream_wait(void *s, void *e) {
+    return hipStreamWaitEvent((hipStream_t)s, (hipEvent_t)e, 0) == hipSuccess ? 0 : -1;
+}
 extern "C" void *kf_get_stream(void) { return (void *)g_stream; }
 
 namespace {

@@ -1441,7 +1441,7 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     // workgroups per launch: every split writes an M x N fp32 slab that the reduce
     // reads back, so the target trades CU fill against slab traffic
     // (targets of 256 / 384 / 768 / 1024 measured slower)
-    int splits = (512 + tiles - 1) / tiles;
+    int splits = ((kf_expt() & 2 ? 256 : 512) + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
     if (splits > maxsplit) splits = maxsplit;
     if (splits < 1) splits = 1;

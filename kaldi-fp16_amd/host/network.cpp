@@ -22,6 +22,8 @@
 
 #include "nnet_host.h"
 
+int kf_expt();  // libkaldi_fp16: A/B experiment bits (KF_EXPT), 0 = the defaults
+
 using kf::Layer;
 using kf::LayerType;
 
@@ -208,6 +210,15 @@ struct KfNet {
     void *w16 = nullptr;
     void *dz[2] = {nullptr, nullptr}, *g[2] = {nullptr, nullptr};
     void *dbott = nullptr, *edge = nullptr;
+    // Weight gradients run on their own stream (nnet_set_wgrad_stream, default on): a layer's
+    // dW GEMMs hang off the input-gradient chain (dz -> dbott -> dz below) and overlap it.
+    // dbott alternates between two buffers by backward step, so the next layer's affine
+    // input gradient never waits for this layer's linear weight gradient.
+    void *dbott2 = nullptr;
+    void *wg_stream = nullptr, *ev_go = nullptr, *ev_side = nullptr;
+    void *hp_stream = nullptr;  // high-priority stream for the input-gradient chain (KF_EXPT bit 0)
+    int wg_side = 1;
+    void *dbott_last = nullptr;  // the dbott buffer of the last TDNN-F / prefinal step (tests)
     size_t edge_half = 0;
     int fp8 = 0;
     int fp8_dgrad = 1;  // nnet_set_fp8(net, 2): MXFP8 forward, fp16 affine input gradients (tests)
@@ -229,6 +240,11 @@ struct KfNet {
         return p;
     }
     ~KfNet() {
+        if (wg_stream) bridge_gpu_sync();
+        kf_event_free(ev_go);
+        kf_event_free(ev_side);
+        kf_stream_free(wg_stream);
+        kf_stream_free(hp_stream);
         for (void *p : allocs) bridge_gpu_free(p);
     }
 };
@@ -730,10 +746,19 @@ static bool alloc_device(KfNet *net, int max_frames) {
         net->g[i] = net->dalloc((T + 2) * maxw * 2);
     }
     net->dbott = net->dalloc((T + 2) * maxw * 2);
+    net->dbott2 = net->dalloc((T + 2) * maxw * 2);
     net->edge_half = align_up(maxw * 2, 256);
     net->edge = net->dalloc(net->edge_half * 2);
-    if (!net->dz[0] || !net->dz[1] || !net->g[0] || !net->g[1] || !net->dbott || !net->edge) {
+    if (!net->dz[0] || !net->dz[1] || !net->g[0] || !net->g[1] || !net->dbott || !net->dbott2 || !net->edge) {
         set_err("alloc backward scratch");
+        return false;
+    }
+    net->wg_stream = kf_stream_new();
+    net->hp_stream = kf_stream_new_high();
+    net->ev_go = kf_event_new();
+    net->ev_side = kf_event_new();
+    if (!net->wg_stream || !net->ev_go || !net->ev_side) {
+        set_err("create the weight-gradient stream");
         return false;
     }
     return true;
@@ -1469,7 +1494,7 @@ extern "C" const void *nnet_debug_tensor(KfNet *net, const char *what, int layer
     if (w == "dz1") return net->dz[1];
     if (w == "g0") return net->g[0];
     if (w == "g1") return net->g[1];
-    if (w == "dbott") return net->dbott;
+    if (w == "dbott") return net->dbott_last ? net->dbott_last : net->dbott;
     // the MXFP8 copies of dz[layer] (layer = buffer 0 / 1) and the layer whose affine input
     // gradient reads it (as an int, through the pointer's low bits: -1 none), MXFP8 train step
     if ((w == "dz8q" || w == "dz8s" || w == "dz8layer") && (layer == 0 || layer == 1)) {
@@ -1500,15 +1525,62 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         return -1;
     }
     const int n = (int)net->layers.size();
+    // Two streams: the input-gradient chain on the caller's stream (main), every write into
+    // the gradient buffer on the weight-gradient stream (side), which waits for main at each
+    // wgrad(): the dW GEMMs of a layer overlap the input gradients below it. Hazards (WAR on
+    // shared scratch) are ordered by events: main waits for all of the previous step's side
+    // work before it overwrites the dz / g ping-pong buffer that work read (dx_wait), and
+    // dbott alternates between two buffers. All gradient writes (and so the data-parallel
+    // bucket gates, dp_issue) are on side; main joins side before returning.
+    void *const caller = kf_get_stream();
+    void *mainst = caller;
+    const bool two = net->wg_side != 0 && net->wg_stream != nullptr;
+    struct Restore {  // every return leaves the caller's stream current
+        void *s;
+        ~Restore() { kf_set_stream(s); }
+    } restore{caller};
+    // experiment (KF_EXPT bit 0): the input-gradient chain on a high-priority stream, so its
+    // workgroups are dispatched ahead of the weight gradients'
+    const bool hp = two && net->hp_stream && (kf_expt() & 1);
+    if (hp) {
+        if (kf_event_record(net->ev_go, caller) != 0 || kf_stream_wait(net->hp_stream, net->ev_go) != 0) {
+            set_err("backward: chain stream order");
+            return -1;
+        }
+        mainst = net->hp_stream;
+        kf_set_stream(mainst);
+    }
+    auto to_side = [&]() -> bool {  // side continues after everything main enqueued so far
+        if (!two) return true;
+        if (kf_event_record(net->ev_go, mainst) != 0 || kf_stream_wait(net->wg_stream, net->ev_go) != 0) {
+            set_err("backward: weight-gradient stream order");
+            return false;
+        }
+        kf_set_stream(net->wg_stream);
+        return true;
+    };
+    auto to_main = [&]() { kf_set_stream(mainst); };
+    bool side_pending = false;  // side work of the previous step that main has not waited for
+    auto dx_wait = [&]() -> bool {  // main waits for the previous step's side work
+        if (!two || !side_pending) return true;
+        if (kf_stream_wait(mainst, net->ev_side) != 0) {
+            set_err("backward: weight-gradient stream join");
+            return false;
+        }
+        side_pending = false;
+        return true;
+    };
     // the top layer must be the chain output
     const void *dz = out_grad;  // gradient w.r.t. pre-activation of the current layer
     const void *gcur = out_grad;  // stored gradient w.r.t. the current layer's output
     int flip = 0, done = 0;
     size_t dp_next = 0;
+    if (!to_side()) return -1;
     for (const auto &r : net->offpath) bridge_gpu_memset(net->grad + r.first, 0, (size_t)r.second * 4);
     (void)n;
     // negative control of the data-parallel tests: exchanging before any producer ran
     if (net->dp && net->dp_early && !dp_issue(net, dp_next, INT_MAX)) return -1;
+    to_main();
     for (int li = net->chain_out; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
         NetLayer &nl = net->layers[li];
         const Layer &L = nl.L;
@@ -1516,9 +1588,17 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         const void *x = act_of(net, nl.input);
         bool want_dx = nl.needs_dx && nl.input >= 0;
         void *dz_next = net->dz[flip], *g_next = net->g[flip];
+        void *const dbott_buf = (done & 1) && two ? net->dbott2 : net->dbott;
         net->dz8_layer[flip] = -1;
         KfEpilogue E;
         if (want_dx && !dx_epilogue(net, nl.input, dz_next, g_next, E)) return -1;
+        // a weight gradient: on side, after what main enqueued so far
+        auto wgrad = [&](const std::function<bool()> &f) -> bool {
+            if (!to_side()) return false;
+            const bool ok = f();
+            to_main();
+            return ok;
+        };
         if (nl.bypass) {
             E.resid = gcur;
             E.ldr = dout;
@@ -1529,13 +1609,15 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
             case LayerType::Linear: {
                 KfOperand A = op_base(x, din, T, din, 0);
                 KfOperand B = op_base(dz, dout, T, dout, 0);
-                if (!ck(kf_gemm_wgrad(din, dout, T, &A, &B, gptr(net, nl.pW), dout, gptr(net, nl.pb), 0),
-                        "wgrad"))
+                if (!wgrad([&] {
+                        return ck(kf_gemm_wgrad(din, dout, T, &A, &B, gptr(net, nl.pW), dout, gptr(net, nl.pb), 0),
+                                  "wgrad");
+                    }))
                     return -1;
                 if (want_dx) {
                     KfOperand A2 = op_base(dz, dout, T, dout, 1);
                     KfOperand B2 = op_base(wptr(net, nl.pW), dout, din, dout, 1);
-                    if (!ck(kf_gemm_fused(T, din, dout, &A2, &B2, &E), "dgrad")) return -1;
+                    if (!dx_wait() || !ck(kf_gemm_fused(T, din, dout, &A2, &B2, &E), "dgrad")) return -1;
                 }
                 break;
             }
@@ -1549,13 +1631,15 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     return -1;
                 KfOperand Aw = op_base(x, din, T, din, 0);
                 KfOperand Bw = op_base(nl.dproj, A, T, A, 0);
-                if (!ck(kf_gemm_wgrad(din, A, T, &Aw, &Bw, gptr(net, nl.pW), A, gptr(net, nl.pb), 0),
-                        "attention wgrad"))
+                if (!wgrad([&] {
+                        return ck(kf_gemm_wgrad(din, A, T, &Aw, &Bw, gptr(net, nl.pW), A, gptr(net, nl.pb), 0),
+                                  "attention wgrad");
+                    }))
                     return -1;
                 if (want_dx) {
                     KfOperand A2 = op_base(nl.dproj, A, T, A, 1);
                     KfOperand B2 = op_base(wptr(net, nl.pW), A, din, A, 1);
-                    if (!ck(kf_gemm_fused(T, din, A, &A2, &B2, &E), "attention dgrad")) return -1;
+                    if (!dx_wait() || !ck(kf_gemm_fused(T, din, A, &A2, &B2, &E), "attention dgrad")) return -1;
                 }
                 break;
             }
@@ -1564,10 +1648,13 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 // dz = gradient at the small (BN2) pre-activation
                 KfOperand A = op_base(nl.aux, big, T, big, 0);
                 KfOperand B = op_base(dz, small, T, small, 0);
-                if (!ck(kf_gemm_wgrad(big, small, T, &A, &B, gptr(net, nl.pW2), small, nullptr, 0),
-                        "prefinal small wgrad"))
+                if (!wgrad([&] {
+                        return ck(kf_gemm_wgrad(big, small, T, &A, &B, gptr(net, nl.pW2), small, nullptr, 0),
+                                  "prefinal small wgrad");
+                    }))
                     return -1;
-                void *dzbig = net->dbott;
+                void *dzbig = dbott_buf;
+                net->dbott_last = dzbig;
                 KfEpilogue E1 = epi0();
                 E1.out2 = dzbig;
                 E1.ldo2 = big;
@@ -1578,13 +1665,15 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 if (!ck(kf_gemm_fused(T, big, small, &A1, &B1, &E1), "prefinal small dgrad")) return -1;
                 KfOperand A3 = op_base(x, din, T, din, 0);
                 KfOperand B3 = op_base(dzbig, big, T, big, 0);
-                if (!ck(kf_gemm_wgrad(din, big, T, &A3, &B3, gptr(net, nl.pW), big, gptr(net, nl.pb), 0),
-                        "prefinal big wgrad"))
+                if (!wgrad([&] {
+                        return ck(kf_gemm_wgrad(din, big, T, &A3, &B3, gptr(net, nl.pW), big, gptr(net, nl.pb), 0),
+                                  "prefinal big wgrad");
+                    }))
                     return -1;
                 if (want_dx) {
                     KfOperand A4 = op_base(dzbig, big, T, big, 1);
                     KfOperand B4 = op_base(wptr(net, nl.pW), big, din, big, 1);
-                    if (!ck(kf_gemm_fused(T, din, big, &A4, &B4, &E), "prefinal big dgrad")) return -1;
+                    if (!dx_wait() || !ck(kf_gemm_fused(T, din, big, &A4, &B4, &E), "prefinal big dgrad")) return -1;
                 }
                 break;
             }
@@ -1595,11 +1684,14 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 KfOperand A = s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 0)
                                     : op_base(nl.aux, bn, T, bn, 0);
                 KfOperand B = op_base(dz, dout, T, dout, 0);
-                if (!ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
-                        "tdnnf affine wgrad"))
+                if (!wgrad([&] {
+                        return ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
+                                  "tdnnf affine wgrad");
+                    }))
                     return -1;
                 // bottleneck gradient: transpose of the [0, +s] clamped splice
-                void *dbott = net->dbott;
+                void *dbott = dbott_buf;
+                net->dbott_last = dbott;
                 KfEpilogue E1 = epi0();
                 E1.out = dbott;
                 E1.ldo = bn;
@@ -1648,10 +1740,13 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 KfOperand A2 = s > 0 ? op_splice(x, T, din, -s, 0, KF_CLAMP, 0)
                                      : op_base(x, din, T, din, 0);
                 KfOperand B2 = op_base(dbott, bn, T, bn, 0);
-                if (!ck(kf_gemm_wgrad(klin, bn, T, &A2, &B2, gptr(net, nl.pW), bn, nullptr, 0),
-                        "tdnnf linear wgrad"))
+                if (!wgrad([&] {
+                        return ck(kf_gemm_wgrad(klin, bn, T, &A2, &B2, gptr(net, nl.pW), bn, nullptr, 0),
+                                  "tdnnf linear wgrad");
+                    }))
                     return -1;
                 if (want_dx) {
+                    if (!dx_wait()) return -1;
                     // input gradient: transpose of the [-s, 0] clamped splice
                     if (s > 0) {
                         // spare row T of dbott holds sum_{t <= s} dbott[t]
@@ -1680,11 +1775,22 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     const int K = noff * L.fin;
                     KfOperand A = op_base(nl.im2col, nl.kp, T * L.hout, nl.kp, 0);
                     KfOperand B = op_base(dz, L.fout, T * L.hout, L.fout, 0);
-                    if (!ck(kf_gemm_wgrad(nl.kp, L.fout, T * L.hout, &A, &B, nl.gwpad, L.fout, gptr(net, nl.pb), 0),
-                            "conv small-fin wgrad") ||
-                        !ck(ops_copy(gptr(net, nl.pW), nl.gwpad, 2 * K * L.fout), "conv small-fin wgrad copy"))
+                    if (!wgrad([&] {
+                            return ck(kf_gemm_wgrad(nl.kp, L.fout, T * L.hout, &A, &B, nl.gwpad, L.fout,
+                                                    gptr(net, nl.pb), 0),
+                                      "conv small-fin wgrad") &&
+                                   ck(ops_copy(gptr(net, nl.pW), nl.gwpad, 2 * K * L.fout), "conv small-fin wgrad copy");
+                        }))
                         return -1;
                     if (want_dx) {
+                        // the input gradient overwrites nl.im2col, which the weight gradient
+                        // just read on side: main waits for side here
+                        if (two && (kf_event_record(net->ev_side, net->wg_stream) != 0 ||
+                                    kf_stream_wait(mainst, net->ev_side) != 0)) {
+                            set_err("backward: weight-gradient stream join");
+                            return -1;
+                        }
+                        side_pending = false;
                         if (E.out || E.mask_in || E.scale2 || !E.out2) {
                             set_err("conv " + L.name + ": small-fin input gradient only into combine-feature-maps");
                             return -1;
@@ -1704,19 +1810,24 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     break;
                 }
                 if (L.fin == 1) {
-                    if (!ck(kf_conv_c1_wgrad(T, L.hin, L.hout, L.hsub, L.fout, noff, nl.dt.data(),
-                                             nl.dh.data(), x, dz, gptr(net, nl.pW), gptr(net, nl.pb)),
-                            "conv c1 wgrad"))
+                    if (!wgrad([&] {
+                            return ck(kf_conv_c1_wgrad(T, L.hin, L.hout, L.hsub, L.fout, noff, nl.dt.data(),
+                                                       nl.dh.data(), x, dz, gptr(net, nl.pW), gptr(net, nl.pb)),
+                                      "conv c1 wgrad");
+                        }))
                         return -1;
                 } else {
                     KfOperand A = op_im2col(nl, x, T, 0);
                     KfOperand B = op_base(dz, L.fout, T * L.hout, L.fout, 0);
-                    if (!ck(kf_gemm_wgrad(noff * L.fin, L.fout, T * L.hout, &A, &B, gptr(net, nl.pW),
-                                          L.fout, gptr(net, nl.pb), 0),
-                            "conv wgrad"))
+                    if (!wgrad([&] {
+                            return ck(kf_gemm_wgrad(noff * L.fin, L.fout, T * L.hout, &A, &B, gptr(net, nl.pW),
+                                                    L.fout, gptr(net, nl.pb), 0),
+                                      "conv wgrad");
+                        }))
                         return -1;
                 }
                 if (want_dx) {
+                    if (!dx_wait()) return -1;
                     if (L.fin == 1) {
                         set_err("conv " + L.name + ": input gradient of a 1-filter conv not supported");
                         return -1;
@@ -1785,9 +1896,11 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                             if (!ck(kf_scale_cols(nl.gdb, qd, q.bn_scale, nl.gdb, qd, rowsB, qd), "ivector bn backward"))
                                 return -1;
                         } else if (q.L.type == LayerType::Linear) {
-                            if (!ck(kf_rows_wgrad(act_of(net, q.input), q.L.in_dim, nl.gdb, qd, gptr(net, q.pW), qd,
-                                                  rowsB, q.L.in_dim, qd),
-                                    "ivector linear wgrad"))
+                            if (!wgrad([&] {
+                                    return ck(kf_rows_wgrad(act_of(net, q.input), q.L.in_dim, nl.gdb, qd,
+                                                            gptr(net, q.pW), qd, rowsB, q.L.in_dim, qd),
+                                              "ivector linear wgrad");
+                                }))
                                 return -1;
                             if (q.input >= 0) {
                                 set_err("ivector branch: a linear-component below another one is not supported");
@@ -1809,7 +1922,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 break;
             case LayerType::Batchnorm:
                 if (want_dx) {  // dz already is the gradient at the BN input (dx_epilogue)
-                    if (net->dp && !dp_issue(net, dp_next, done)) return -1;
+                    if (net->dp && !wgrad([&] { return dp_issue(net, dp_next, done); })) return -1;
                     continue;   // same dz / gcur buffers for the layer below: no flip
                 }
                 break;
@@ -1824,20 +1937,51 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 set_err("backward: unsupported layer " + L.name);
                 return -1;
         }
-        // gradient buckets complete at this step go to the communication stream
+        // gradient buckets complete at this step go to the communication stream (their
+        // gates on side, behind the step's weight gradients)
+        if (two) kf_set_stream(net->wg_stream);
         if (net->dp && !dp_issue(net, dp_next, done)) return -1;
+        if (two) {
+            if (kf_event_record(net->ev_side, net->wg_stream) != 0) {
+                set_err("backward: weight-gradient stream event");
+                return -1;
+            }
+            side_pending = true;
+        }
+        to_main();
         if (!want_dx) break;  // nothing trainable below
         dz = dz_next;
         gcur = g_next;
         flip ^= 1;
     }
-    if (net->dp) {  // the rest, then the compute stream waits for every bucket (SGD reads them)
-        if (!dp_issue(net, dp_next, INT_MAX)) return -1;
-        if (kf_dp_join(net->dp) != 0) {
-            set_err(std::string("dp join: ") + (kf_dp_last_error() ? kf_dp_last_error() : ""));
+    // the rest of the buckets, then main waits for side (SGD reads every gradient) and for
+    // every bucket
+    if (two) kf_set_stream(net->wg_stream);
+    if (net->dp && !dp_issue(net, dp_next, INT_MAX)) return -1;
+    to_main();
+    if (two && (kf_event_record(net->ev_side, net->wg_stream) != 0 || kf_stream_wait(mainst, net->ev_side) != 0)) {
+        set_err("backward: weight-gradient stream join");
+        return -1;
+    }
+    if (hp) {  // the caller's stream continues after the chain (which joined side)
+        if (kf_event_record(net->ev_go, mainst) != 0 || kf_stream_wait(caller, net->ev_go) != 0) {
+            set_err("backward: chain stream join");
             return -1;
         }
+        mainst = caller;
+        kf_set_stream(caller);
     }
+    if (net->dp && kf_dp_join(net->dp) != 0) {
+        set_err(std::string("dp join: ") + (kf_dp_last_error() ? kf_dp_last_error() : ""));
+        return -1;
+    }
+    return 0;
+}
+
+extern "C" int nnet_set_wgrad_stream(KfNet *net, int on) {
+    if (!net) return -1;
+    if (!on && net->wg_stream) bridge_gpu_sync();
+    net->wg_side = on != 0 && net->wg_stream != nullptr;
     return 0;
 }
 

@@ -98,6 +98,7 @@ _sig(nnet, "nnet_create_layout", _vp, C.c_char_p, _i)
 _sig(nnet, "nnet_bind_dp", _i, _vp, _vp, _ll)
 _sig(nnet, "nnet_dp_plan", _i, _vp, _ll, _i, C.POINTER(_i), C.POINTER(_ll), C.POINTER(_ll))
 _sig(nnet, "nnet_dp_debug_early", _i, _vp, _i)
+_sig(nnet, "nnet_set_wgrad_stream", _i, _vp, _i)
 _sig(nnet, "nnet_weights_changed", _i, _vp)
 # kf_dp.h (RCCL data parallel)
 _sig(core, "kf_dp_last_error", C.c_char_p)
@@ -356,6 +357,11 @@ class Network:
     def weights_changed(self):
         """The fp16 weights were written through nnet_weight_buffer (kf_nnet.h)."""
         check(nnet.nnet_weights_changed(self.h), "nnet_weights_changed")
+
+    def set_wgrad_stream(self, on: bool):
+        """Weight gradients on their own stream, overlapping the input gradients (default
+        on; kf_nnet.h nnet_set_wgrad_stream)."""
+        check(nnet.nnet_set_wgrad_stream(self.h, int(on)), "nnet_set_wgrad_stream")
 
     def dp_debug_early(self, on: bool):
         """Test hook: issue every gradient bucket before the backward runs (the

@@ -150,3 +150,34 @@ def test_full_model_one_eg(gpu):
     ref = on.grads()
     errs = {k: rel_fro(got[k], ref[k]) for k in ref}
     assert all(v <= 5e-3 for v in errs.values()), errs
+
+
+@pytest.mark.parametrize("xname,T", [("tiny.xconfig", 300), ("cnn_tdnn_17f.xconfig", 3000)])
+def test_wgrad_stream_bit_identical(gpu, xname, T):
+    """nnet_backward with the weight gradients on their own stream (the default) against
+    the one-stream order: every gradient, and the next step's activations after SGD,
+    bit-identical (the same kernels on the same inputs; only the launch streams and the
+    alternating dbott buffer differ). Twice in a row with the stream on, so a race on the
+    ping-pong buffers between consecutive backward calls would show as well."""
+    kfp16 = gpu
+    from kfp16 import synth
+    xcfg = synth.load_xconfig(xname)
+    P = None
+    res = []
+    for on in (False, True, True):
+        net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
+        net.set_wgrad_stream(on)
+        P = net.layers[-1][3]
+        og = (np.random.default_rng(11).standard_normal((T, P)) * 0.05).astype(np.float16)
+        gb = kfp16.upload_fp16(og)
+        net.backward(gb.ptr)
+        net.sgd(1e-3, 0.9)
+        net.forward(fbuf.ptr, T)
+        net.backward(gb.ptr)
+        res.append((net.read_grads(), net.read_activation("output").astype(np.float32)))
+        net.close()
+    g0, a0 = res[0]
+    for g1, a1 in res[1:]:
+        for k in g0:
+            assert np.array_equal(g0[k], g1[k]), k
+        assert np.array_equal(a0, a1)
