@@ -151,6 +151,28 @@ def ivector_input(xcfg):
     return int(m.group(1)) if m else 0
 
 
+def box_hbm_probe():
+    """HBM streaming rate of this box (torch copy of a [96,000 x 1536] fp16 tensor, the
+    TDNN-F epilogue shape; median of 10, HIP events): the pool's MI355X boxes differ
+    (memory-bound kernels run up to ~1.8x slower on some), so the line says which it ran on."""
+    a = torch.empty((96000, 1536), dtype=torch.float16, device="cuda").fill_(1.0)
+    c = torch.empty_like(a)
+    c.copy_(a)
+    ts = []
+    for _ in range(10):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        c.copy_(a)
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = float(np.median(ts))
+    del a, c
+    torch.cuda.empty_cache()
+    return {"copy_GBps": round(2 * 96000 * 1536 * 2 / (ms * 1e-3) / 1e9, 1),
+            "probe": "torch copy of a [96000 x 1536] fp16 tensor (read + write), median of 10"}
+
+
 def host_cores():
     try:
         return len(os.sched_getaffinity(0))
@@ -650,6 +672,7 @@ def main():
 
     prof_on = not a.no_prof
     peak = PEAK_FP8_TFLOPS if a.fp8 else PEAK_FP16_TFLOPS
+    box = box_hbm_probe()
     head, ctx = run_workload(a, a.xconfig, a.mode, a.fp8, rank, world, comm, a.steps, a.warmup, prof_on,
                              keep=True)
     extra = {}
@@ -720,6 +743,8 @@ def main():
                   "objective_finite_seqs"):
             if k in d:
                 out[k] = d[k]
+        out["box"] = box
+        out["wgrad_stream"] = not a.no_wgrad_stream
         if not fwd_only:
             out["den_exchange_timeouts"] = 0   # kf_chain_result raised otherwise
         if world > 1:

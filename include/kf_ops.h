@@ -132,6 +132,9 @@ int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
  */
 int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW,
                   long long ldw, float *bias_grad, int accumulate);
+/* split-K workgroup target of kf_gemm_wgrad on the calling thread (default 512); returns
+ * the previous value (wgs <= 0: query only) */
+int kf_gemm_wgrad_target(int wgs);
 
 /*
  * MXFP8 quantisation (OCP MX): per block of 32 consecutive values of a row,

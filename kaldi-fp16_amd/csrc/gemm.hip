@@ -1406,6 +1406,16 @@ int kf_expt() {
     return v;
 }
 
+// workgroups per weight-gradient launch (split-K target): 512 alone on the device; nnet's
+// backward sets 256 while its weight gradients run on their own stream beside the
+// input-gradient chain (half the CUs each, half the fp32 slab bytes)
+static thread_local int g_wgrad_target = 512;
+extern "C" int kf_gemm_wgrad_target(int wgs) {
+    const int old = g_wgrad_target;
+    if (wgs > 0) g_wgrad_target = wgs;
+    return old;
+}
+
 extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              float *dW, long long ldw, float *bias_grad, int accumulate) {
     if (M <= 0 || N <= 0) return 0;
@@ -1441,7 +1451,7 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     // workgroups per launch: every split writes an M x N fp32 slab that the reduce
     // reads back, so the target trades CU fill against slab traffic
     // (targets of 256 / 384 / 768 / 1024 measured slower)
-    int splits = ((kf_expt() & 2 ? 256 : 512) + tiles - 1) / tiles;
+    int splits = (g_wgrad_target + tiles - 1) / tiles;
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
     if (splits > maxsplit) splits = maxsplit;
     if (splits < 1) splits = 1;

@@ -22,8 +22,6 @@
 
 #include "nnet_host.h"
 
-int kf_expt();  // libkaldi_fp16: A/B experiment bits (KF_EXPT), 0 = the defaults
-
 using kf::Layer;
 using kf::LayerType;
 
@@ -216,7 +214,7 @@ struct KfNet {
     // input gradient never waits for this layer's linear weight gradient.
     void *dbott2 = nullptr;
     void *wg_stream = nullptr, *ev_go = nullptr, *ev_side = nullptr;
-    void *hp_stream = nullptr;  // high-priority stream for the input-gradient chain (KF_EXPT bit 0)
+    void *hp_stream = nullptr;  // high-priority stream for the input-gradient chain
     int wg_side = 1;
     void *dbott_last = nullptr;  // the dbott buffer of the last TDNN-F / prefinal step (tests)
     size_t edge_half = 0;
@@ -1539,9 +1537,17 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         void *s;
         ~Restore() { kf_set_stream(s); }
     } restore{caller};
-    // experiment (KF_EXPT bit 0): the input-gradient chain on a high-priority stream, so its
-    // workgroups are dispatched ahead of the weight gradients'
-    const bool hp = two && net->hp_stream && (kf_expt() & 1);
+    // With the weight-gradient stream the input-gradient chain runs on a high-priority
+    // stream (its workgroups are dispatched ahead of the weight gradients') and each weight
+    // gradient launches 256 workgroups instead of 512. A/B on one box (bench default, r5):
+    // one stream 49.1-49.5 ms, two streams 41.0-41.4, + priority 40.7, + 256 40.8, both
+    // 39.1-39.4 ms (a box whose memory-bound kernels run ~1.3x slower than the fastest
+    // ones'; on a fast box the two-stream order measured 37.3 against 37.1 ms).
+    const bool hp = two && net->hp_stream;
+    struct Target {
+        int old;
+        ~Target() { kf_gemm_wgrad_target(old); }
+    } target{kf_gemm_wgrad_target(two ? 256 : 0)};
     if (hp) {
         if (kf_event_record(net->ev_go, caller) != 0 || kf_stream_wait(net->hp_stream, net->ev_go) != 0) {
             set_err("backward: chain stream order");

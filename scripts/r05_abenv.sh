@@ -9,5 +9,5 @@ for v in "$@"; do
   i=$((i+1))
   t=e${v}_$i
   KF_EXPT=$v timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r05/ab_$tag/$t -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-prof --no-extra $BENCH_ARGS > gpurun_out/r05/ab_$tag/$t.log 2>&1 || exit $?
-  echo "$t $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/r05/ab_$tag/$t.log) $(grep -o '"ms_per_step_mean": [0-9.]*' gpurun_out/r05/ab_$tag/$t.log)"
+  echo "$t $(python3 scripts/bline.py gpurun_out/r05/ab_$tag/$t.log)"
 done
