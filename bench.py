@@ -84,6 +84,11 @@ def parse(argv=None):
                    help="upload the step's inputs once before timing (default: TrainStep's per-minibatch "
                         "feature and numerator upload inside every step, overlapped on a copy stream)")
     p.add_argument("--input-pool", type=int, default=2, help="distinct host minibatches cycled through (h2d)")
+    p.add_argument("--own-stream", action="store_true",
+                   help="run the step on a non-blocking stream of its own instead of torch's default stream")
+    p.add_argument("--h2d-mode", choices=("inline", "overlap"), default="inline",
+                   help="inline: the step's uploads are the first work of the step on its stream; overlap: "
+                        "on a copy stream during the previous step")
     p.add_argument("--no-wgrad-stream", action="store_true",
                    help="weight gradients on the main stream (default: their own stream, nnet_set_wgrad_stream)")
     p.add_argument("--fp8", action="store_true",
@@ -483,13 +488,14 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         seq_off = np.arange(a.egs + 1, dtype=np.int32) * FRAMES_PER_EG
 
     comp = torch.cuda.current_stream()
+    inline = h2d and a.h2d_mode == "inline"
     if h2d:
         # TrainStep's input stage (train_step.go:155 TransferBatch -> bridge.cu:206-267, and the
         # per-sequence FST uploads of chain_loss.go:44-97) inside every timed step: step i+1's
         # fp32 features (pinned host) and numerator FSTs (kf_num_batch_refill) go up on a copy
         # stream while step i computes; the step then rounds its features to fp16 (RNE,
         # fp16.go:12-70) on the GPU. Two device slots; events order reuse.
-        copy = torch.cuda.Stream()
+        copy = comp if inline else torch.cuda.Stream()
         host = [torch.from_numpy(f).pin_memory() for f in feats_pool]
         f32 = [torch.empty((T, 40), dtype=torch.float32, device="cuda") for _ in range(2)]
         fbufs = [torch.empty((T, 40), dtype=torch.float16, device="cuda") for _ in range(2)]
@@ -504,20 +510,22 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         state = {"i": 0}
 
         def stage(i):
-            """step i's inputs into slot i % 2, on the copy stream"""
+            """step i's inputs into slot i % 2, on the copy stream (inline: the step's stream)"""
             sl = i % 2
-            copy.wait_event(ev_conv[sl])    # the slot's fp32 features were converted (step i - 2)
-            copy.wait_event(ev_obj[sl])     # the slot's numerator was used (step i - 2)
-            # and not before step i - 1's forward has finished: the copies then run under its
-            # den recursion (latency-bound, ~5 ms). Issued whenever the host got there, they
-            # sometimes landed under the den posteriors, which then took ~0.9 ms longer.
-            copy.wait_event(ev_fwd)
+            if not inline:
+                copy.wait_event(ev_conv[sl])    # the slot's fp32 features were converted (step i - 2)
+                copy.wait_event(ev_obj[sl])     # the slot's numerator was used (step i - 2)
+                # and not before step i - 1's forward has finished: the copies then run under
+                # its den recursion (latency-bound, ~5 ms). Issued whenever the host got there,
+                # they sometimes landed under the den posteriors, which then took ~0.9 ms longer.
+                copy.wait_event(ev_fwd)
             with torch.cuda.stream(copy):
                 f32[sl].copy_(host[i % npool], non_blocking=True)
                 ev_copied[sl].record(copy)
             nums[sl].refill(packs[i % npool], copy.cuda_stream)
 
-        stage(0)
+        if not inline:
+            stage(0)
     else:
         feats = feats_pool[0]
         fbuf = torch.from_numpy(feats.view(np.int16)).to("cuda")
@@ -527,6 +535,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         if h2d:
             i = state["i"]
             sl = i % 2
+            if inline:
+                stage(i)
             comp.wait_event(ev_copied[sl])
             kfp16.check(kfp16.core.bridge_fp32_to_fp16_gpu(fbufs[sl].data_ptr(), f32[sl].data_ptr(), T * 40),
                         "bridge_fp32_to_fp16_gpu")
@@ -545,7 +555,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         objective.compute(num, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
         if h2d:
             ev_obj[sl].record(comp)
-            stage(i + 1)                    # the next step's inputs, overlapped with this backward
+            if not inline:
+                stage(i + 1)                # the next step's inputs, overlapped with this backward
             state["i"] = i + 1
         net.backward(gbuf.data_ptr())       # + the overlapped gradient all-reduce (N > 1)
         net.sgd(a.lr, a.momentum)
@@ -620,7 +631,8 @@ def describe(r, a, world, mode, fp8, xconfig, peak):
     mean_ms = r["elapsed"] / r["steps"] * 1e3
     value = r["T"] * world * r["steps"] / r["elapsed"]
     d = {"value": round(value, 1), "ms_per_step": round(r["median_ms"], 3), "ms_per_step_mean": round(mean_ms, 3),
-         "ms_per_step_min_max": [round(min(r["step_ms"]), 3), round(max(r["step_ms"]), 3)]}
+         "ms_per_step_min_max": [round(min(r["step_ms"]), 3), round(max(r["step_ms"]), 3)],
+         "step_ms": [round(x, 2) for x in r["step_ms"]]}
     mf = MODEL_MFLOP_PER_FRAME.get(r["xconfig"])
     if mf is not None:
         # whole step against the dense FP16 MFMA roofline: frames/s x algorithmic FLOPs per
@@ -664,7 +676,8 @@ def main():
     import kfp16
     from kfp16 import dp
     kfp16.check(kfp16.core.bridge_gpu_init(local), "bridge_gpu_init")
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream() if a.own_stream else torch.cuda.current_stream()
+    torch.cuda.set_stream(stream)
     kfp16.set_stream(stream.cuda_stream)
     kfp16.assert_single_hip_runtime()
     comm = dp.Communicator.from_process_group(local) if world > 1 else None
@@ -730,15 +743,17 @@ def main():
                        "xconfig": a.xconfig, "egs_per_gpu": a.egs, "frames_per_eg": FRAMES_PER_EG,
                        "global_batch_egs": a.egs * world, "parallelism": f"dp{world}",
                        "h2d_in_step": bool(head["h2d"]),
-                       "inputs": ("per step: fp32 features from pinned host memory and the minibatch's "
-                                  "numerator FSTs (kf_num_batch_refill) uploaded on a copy stream during the "
-                                  "previous step, RNE to fp16 on the GPU inside the step; "
+                       "inputs": (("per step, first on the step's stream: " if a.h2d_mode == "inline" else
+                                   "per step, on a copy stream during the previous step: ") +
+                                  "fp32 features from pinned host memory and the minibatch's numerator FSTs "
+                                  "(kf_num_batch_refill) uploaded, then RNE to fp16 on the GPU; "
                                   f"{head['input_pool']} distinct host minibatches cycled")
                                  if head["h2d"] else "resident in HBM before timing",
                        "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)"},
         }
         out["ms_per_step_mean"] = d["ms_per_step_mean"]
         out["ms_per_step_min_max"] = d["ms_per_step_min_max"]
+        out["step_ms"] = d["step_ms"]
         for k in ("step_mfma_frac", "step_mfma_peak", "step_mflop_per_frame", "objf_per_frame",
                   "objective_finite_seqs"):
             if k in d:
