@@ -571,6 +571,7 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         dist.barrier()
     if prof_on:
         kfp16.core.kf_prof_reset()
+        kfp16.core.kf_prof_reserve(256 * steps)   # ~190 profiled launches per step
         kfp16.core.kf_prof_enable(1)
     dp0 = comm.stats() if comm is not None else (0, 0)
     # per-step HIP events on the launch stream (the library runs on torch's current stream):

@@ -257,6 +257,8 @@ int kf_scale_cols(const void *x, long long ldx, const float *scale, void *y, lon
  * L2/HBM bytes), 4 = kf_gemm_fused on the 3x3 conv halo kernel, 5 = the conv halo weight
  * gradient, 6 = the split-K slab reduce (bytes only) */
 void kf_prof_enable(int on);
+/* pre-create the timing events of n profiled launches (no event creation in timed code) */
+int kf_prof_reserve(int n);
 int kf_prof_collect(int cls, long long *count, double *ms, double *flops);
 /* the same plus the algorithmic HBM bytes of those launches (GEMM classes: each
  * operand's source tensor read once, epilogue tensors read / written once) */

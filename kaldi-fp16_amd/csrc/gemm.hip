@@ -904,6 +904,16 @@ void kf_prof_stop(int idx) {
 }
 
 extern "C" void kf_prof_enable(int on) { g_prof = on != 0; }
+// pre-create events for n timed launches' worth of records (two per launch), so that no
+// hipEventCreate falls inside a timed region
+extern "C" int kf_prof_reserve(int n) {
+    while ((int)g_prof_pool.size() < 2 * n) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return -1;
+        g_prof_pool.push_back(e);
+    }
+    return 0;
+}
 // sums per class since the last collect: count, milliseconds, flops, algorithmic bytes
 extern "C" int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes) {
     long long c = 0;

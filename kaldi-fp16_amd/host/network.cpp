@@ -14,6 +14,7 @@
 //     and the data-parallel gradient exchange is one contiguous buffer.
 // Memory comes from the bridge_* ABI, as the Go layer does (internal/gpu/tensor.go).
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 #include <functional>
 #include <cstdio>
@@ -1543,11 +1544,15 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     // one stream 49.1-49.5 ms, two streams 41.0-41.4, + priority 40.7, + 256 40.8, both
     // 39.1-39.4 ms (a box whose memory-bound kernels run ~1.3x slower than the fastest
     // ones'; on a fast box the two-stream order measured 37.3 against 37.1 ms).
-    const bool hp = two && net->hp_stream;
+    // (A/B knobs: KF_BWD_HP=0 keeps the chain on the caller's stream, KF_BWD_WGT=<n> sets
+    // the weight gradients' workgroup target)
+    static const int env_hp = getenv("KF_BWD_HP") ? atoi(getenv("KF_BWD_HP")) : 1;
+    static const int env_wgt = getenv("KF_BWD_WGT") ? atoi(getenv("KF_BWD_WGT")) : 256;
+    const bool hp = two && net->hp_stream && env_hp;
     struct Target {
         int old;
         ~Target() { kf_gemm_wgrad_target(old); }
-    } target{kf_gemm_wgrad_target(two ? 256 : 0)};
+    } target{kf_gemm_wgrad_target(two ? env_wgt : 0)};
     if (hp) {
         if (kf_event_record(net->ev_go, caller) != 0 || kf_stream_wait(net->hp_stream, net->ev_go) != 0) {
             set_err("backward: chain stream order");

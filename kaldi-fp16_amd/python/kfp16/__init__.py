@@ -116,6 +116,7 @@ _sig(core, "kf_dp_debug", _i, _vp, _i, _vp, _vp, C.c_size_t)
 _sig(core, "kf_dp_plan", _i, _i, C.POINTER(_ll), C.POINTER(_ll), _ll, _ll, _i, C.POINTER(_i),
      C.POINTER(_ll), C.POINTER(_ll))
 _sig(core, "kf_prof_enable", None, _i)
+_sig(core, "kf_prof_reserve", _i, _i)
 _sig(core, "kf_prof_collect", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double))
 _sig(core, "kf_prof_reset", None)
 _sig(core, "kf_prof_collect2", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double),
