@@ -89,6 +89,9 @@ def parse(argv=None):
     p.add_argument("--h2d-mode", choices=("inline", "overlap"), default="inline",
                    help="inline: the step's uploads are the first work of the step on its stream; overlap: "
                         "on a copy stream during the previous step")
+    p.add_argument("--implicit-dz", action="store_true",
+                   help="TDNN-F consumers read g through the ReLU mask instead of a stored dz "
+                        "(nnet_set_implicit_dz; default: dz stored)")
     p.add_argument("--no-wgrad-stream", action="store_true",
                    help="weight gradients on the main stream (default: their own stream, nnet_set_wgrad_stream)")
     p.add_argument("--fp8", action="store_true",
@@ -458,6 +461,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         net.set_fp8(True)
     if a.no_wgrad_stream:
         net.set_wgrad_stream(False)
+    if a.implicit_dz:
+        net.set_implicit_dz(True)
     bucket_bytes = int(a.bucket_mb * (1 << 20))
     if comm is not None and mode == "train":
         net.bind_dp(comm, bucket_bytes)                    # bucketed all-reduce inside backward
@@ -580,9 +585,12 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    t_issue = []
     for i in range(steps):
         evs[i].record(st)
+        t_issue.append(time.perf_counter())
         step()
+    t_issue.append(time.perf_counter())
     evs[steps].record(st)
     torch.cuda.synchronize()
     if world > 1:
@@ -613,7 +621,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         res = objective.result()
         stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
                                   "cuda")
-    out = {"T": T, "elapsed": elapsed, "median_ms": median_ms, "step_ms": step_ms, "steps": steps, "prof": prof, "chain_prof": chain_prof, "classes": classes,
+    cpu_issue_ms = [(t_issue[i + 1] - t_issue[i]) * 1e3 for i in range(steps)]
+    out = {"T": T, "elapsed": elapsed, "median_ms": median_ms, "step_ms": step_ms, "cpu_issue_ms": cpu_issue_ms, "steps": steps, "prof": prof, "chain_prof": chain_prof, "classes": classes,
            "xconfig": xconfig, "mode": mode, "h2d": h2d, "input_pool": npool,
            "stats": stats, "ivd": ivd, "dp": (dp1[0] - dp0[0], dp1[1] - dp0[1]),
            "buckets": len(net.dp_plan(bucket_bytes)) if comm is not None else 0}
@@ -633,7 +642,8 @@ def describe(r, a, world, mode, fp8, xconfig, peak):
     value = r["T"] * world * r["steps"] / r["elapsed"]
     d = {"value": round(value, 1), "ms_per_step": round(r["median_ms"], 3), "ms_per_step_mean": round(mean_ms, 3),
          "ms_per_step_min_max": [round(min(r["step_ms"]), 3), round(max(r["step_ms"]), 3)],
-         "step_ms": [round(x, 2) for x in r["step_ms"]]}
+         "step_ms": [round(x, 2) for x in r["step_ms"]],
+         "cpu_issue_ms": [round(x, 2) for x in r["cpu_issue_ms"]]}
     mf = MODEL_MFLOP_PER_FRAME.get(r["xconfig"])
     if mf is not None:
         # whole step against the dense FP16 MFMA roofline: frames/s x algorithmic FLOPs per
@@ -755,12 +765,14 @@ def main():
         out["ms_per_step_mean"] = d["ms_per_step_mean"]
         out["ms_per_step_min_max"] = d["ms_per_step_min_max"]
         out["step_ms"] = d["step_ms"]
+        out["cpu_issue_ms"] = d["cpu_issue_ms"]
         for k in ("step_mfma_frac", "step_mfma_peak", "step_mflop_per_frame", "objf_per_frame",
                   "objective_finite_seqs"):
             if k in d:
                 out[k] = d[k]
         out["box"] = box
         out["wgrad_stream"] = not a.no_wgrad_stream
+        out["implicit_dz"] = bool(a.implicit_dz)
         if not fwd_only:
             out["den_exchange_timeouts"] = 0   # kf_chain_result raised otherwise
         if world > 1:

@@ -124,6 +124,16 @@ int nnet_dp_debug_early(KfNet *net, int on);
  * caller's stream (the r4 order, A/B and tests). */
 int nnet_set_wgrad_stream(KfNet *net, int on);
 
+/* Implicit dz (default off; fp16 steps): the input-gradient GEMM that produces a TDNN-F
+ * layer's output gradient g (layers with a bypass, which store g anyway) does not also
+ * store dz = rne(g * bnscale * relu_mask). The layer's affine weight gradient and input
+ * gradient read g through the forward's ReLU mask (masked operands, kf_ops.h); the BN scale
+ * multiplies the weight gradient's columns in its split-K reduction and is folded into a
+ * scaled fp16 copy of W2 for the input gradient. Rounding points change accordingly (the
+ * oracle's OrcNet.implicit_dz follows them). Measured step-neutral, hence
+ * off: 0 = store dz (the default). */
+int nnet_set_implicit_dz(KfNet *net, int on);
+
 /* diagnostics (tests): back-propagate through the top n layers only; device
  * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott" (the buffer of the last
  * TDNN-F / prefinal step), "aux", "mask",

@@ -36,6 +36,15 @@
  * hout = 1 are accepted, ncols and part_width multiples of 128, ld multiple of
  * 16; both operands of a GEMM must then be MXFP8 (kf_gemm_fused runs the CDNA4
  * v_mfma_scale_f32_16x16x128_f8f6f4, twice the fp16 MFMA rate).
+ *
+ * Masked operands (mask != NULL, fp16 only): with i = st*ld + sh*part_width + kk the
+ * linear source index of the rule above, the element reads as zero unless bit i of mask
+ * (bit i % 8 of byte i / 8) is set; rows st >= mask_rows (e.g. an edge row) are not
+ * masked. This is how the TDNN-F backward reads dz = g * bnscale * relu_mask without
+ * storing it: g with the forward's ReLU mask, the BN scale folded into the other operand
+ * (kf_scale_cols on W2) or into the weight gradient (kf_gemm_wgrad_scaled). Accepted on the A
+ * operand of kf_gemm_fused (k-contiguous plain or two-part time splice, N = 160 / 320,
+ * k-contiguous B) and the B operand of kf_gemm_wgrad(_scaled) (plain, reduction-major).
  */
 #ifndef KALDI_FP16_AMD_KF_OPS_H
 #define KALDI_FP16_AMD_KF_OPS_H
@@ -65,6 +74,8 @@ typedef struct {
     int fmt;                   /* KF_FMT_FP16 (0) or KF_FMT_MXFP8 (1) */
     const uint8_t *scales;     /* MXFP8: E8M0 block scales */
     long long lds;             /* MXFP8: bytes between the scale rows of consecutive source rows */
+    const uint8_t *mask;       /* masked operand (above), or NULL */
+    int mask_rows;             /* source rows the mask covers */
 } KfOperand;
 
 #define KF_FMT_FP16 0
@@ -132,6 +143,11 @@ int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
  */
 int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW,
                   long long ldw, float *bias_grad, int accumulate);
+/* kf_gemm_wgrad, then dW[:, n] and bias_grad[n] scaled by col_scale[n] (fp32 [N]) in the
+ * split-K reduction: the TDNN-F affine weight gradient on the implicit dz (a masked B
+ * operand g with the BN scale applied here) */
+int kf_gemm_wgrad_scaled(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW,
+                         long long ldw, float *bias_grad, int accumulate, const float *col_scale);
 /* split-K workgroup target of kf_gemm_wgrad on the calling thread (default 512); returns
  * the previous value (wgs <= 0: query only) */
 int kf_gemm_wgrad_target(int wgs);
@@ -171,6 +187,9 @@ int kf_dot2_rows(void *out, const void *x0, const void *x1, const void *W, int r
 /* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols
  * (edge may be a spare row of src's own allocation) */
 int kf_rows_sum(void *edge, const void *src, long long ld, int r0, int r1, int cols);
+/* the same over the masked source: element r*ld + c counts only when its bit in mask is set */
+int kf_rows_sum_mask(void *edge, const void *src, long long ld, int r0, int r1, int cols,
+                     const uint8_t *mask);
 
 /* ---- non-MFMA layer pieces (csrc/layers.hip) ---- */
 /* y[T x N] = x[T x K] . M[K x N], K <= 64, N % 8 == 0 (IDCT, forward.go:317-330) */
@@ -248,7 +267,7 @@ int kf_rows_gemm(const void *x, long long ldx, const void *W, long long ldw, voi
                  int N);
 int kf_rows_wgrad(const void *x, long long ldx, const void *g, long long ldg, float *dW, long long ldd, int R, int M,
                   int N);
-/* y[r][c] = x[r][c] * scale[c] (fp16 in / out, fp32 scale) */
+/* y[r][c] = rne_fp16(fp32(x[r][c] * scale[c])) (fp16 in / out, fp32 scale; x may be y) */
 int kf_scale_cols(const void *x, long long ldx, const float *scale, void *y, long long ldy, int rows, int cols);
 
 /* optional HIP-event timing of the step's kernel classes on the stream each runs on;

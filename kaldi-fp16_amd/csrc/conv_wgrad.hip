@@ -253,7 +253,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wgrad_halo_kernel(OpD B,
 
 // defined in gemm.hip
 void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int M, int N, float *dW,
-                     long long ldw, float *bias_grad, int accumulate);
+                     long long ldw, float *bias_grad, int accumulate, const float *cs = nullptr);
 int kf_prof_start2(int cls, double flops, double bytes);
 void kf_prof_stop(int idx);
 

@@ -350,9 +350,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
                                                                KfEpilogue E, WgradArgs G,
                                                                int n_mtiles, int n_ntiles) {
     constexpr int NW = WM * WN, NTH = 64 * NW;
-    using SCS = ScaleStager<F8 ? BM : 64, F8 ? BN : 64, NW, AM>;  // used by MXFP8 only
+    // operand modes; bit 3 (OP_MASKED) = the operand carries a bit mask (KfOperand.mask)
+    constexpr int AMD = AM & 7, BMD = BMODE & 7;
+    constexpr bool AMK = (AM & OP_MASKED) != 0, BMK = (BMODE & OP_MASKED) != 0, MK = AMK || BMK;
+    static_assert(!MK || (ST == 2 && !F8), "masked operands: two-stage ring, fp16");
+    using SCS = ScaleStager<F8 ? BM : 64, F8 ? BN : 64, NW, AMD>;  // used by MXFP8 only
     constexpr int SCB = F8 ? SCS::BYTES : 0;
-    static_assert(!F8 || (AKC && BKC && !WGRAD && BMODE == OP_SIMPLE && AM != OP_GEN),
+    static_assert(!F8 || (AKC && BKC && !WGRAD && BMD == OP_SIMPLE && AMD != OP_GEN),
                   "MXFP8: k-contiguous plain / spliced A, plain B");
     static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -360,15 +364,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     static_assert(TM * 16 == WTM && TN * 16 == WTN, "wave tile multiple of 16");
     constexpr int A_STAGE = BM * BK * 2, B_STAGE = BN * BK * 2;
     constexpr int STAGE = A_STAGE + B_STAGE + SCB;
-    using SA = Stager<AKC, BM, AM, NW>;
-    using SB = Stager<BKC, BN, BMODE, NW>;
+    using SA = Stager<AKC, BM, AMD, NW, AMK>;
+    using SB = Stager<BKC, BN, BMD, NW, BMK>;
     constexpr int LPT = SA::NC + SB::NC + (F8 ? SCS::SPW : 0);  // LDS-DMA per thread per stage
     static_assert((SA::EVEN && SB::EVEN) || ST == 2, "uneven stagers need the vmcnt(0) ring");
     static_assert(ST >= 2 && ST <= 4, "stages");
     static_assert(WGRAD || 4 * BN * 4 + (32 * EpiMap<WTN>::LDT * 4) * NW <= SmemSize<BM, BN, ST, SCB>::bytes,
                   "epilogue staging");
 
-    __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, ST, SCB>::bytes];
+    __shared__ __attribute__((aligned(16))) char smem[SmemSize<BM, BN, ST, SCB>::bytes + (MK ? 4096 : 0)];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -454,10 +458,15 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     // alternate between the parts, so each 64-column chunk of the source rows is fetched
     // for both parts while it is still in L2 (in part order the second pass misses)
     int kil = 0;
-    if constexpr (!WGRAD && !F8 && AKC && AM == OP_P2)
+    if constexpr (!WGRAD && !F8 && AKC && AMD == OP_P2)
         // (wide parts only: a narrow part's second pass is a few K-steps away and still hits)
         kil = (A.nparts == 2 && A.pw % BK == 0 && A.pw >= 8 * BK && K == 2 * A.pw && G.kil) ? A.pw : 0;
     auto kofs = [&](int kt) { return kbeg + (kil ? (kt & 1) * kil + (kt >> 1) * BK : kt * BK); };
+    uint4 *const mlut = reinterpret_cast<uint4 *>(smem + ST * STAGE);
+    if constexpr (MK) {
+        mask_lut_fill(mlut, tid, NTH);
+        __syncthreads();
+    }
     if (nk > 0) issue(0, kofs(0));
     if (ST >= 3 && nk > 1) issue(1, kofs(1));
     if (ST >= 4 && nk > 2) issue(2, kofs(2));
@@ -465,6 +474,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     for (int kt = 0; kt < nk; ++kt) {
         if (kt + ST - 2 < nk) wait_vmcnt<LPT * (ST - 2)>();
         else wait_vmcnt<0>();
+        if constexpr (MK) {
+            // ST == 2: the wait above retired this stage's chunks and mask bytes
+            char *stg = smem + (kt % ST) * STAGE;
+            if constexpr (AMK) sa.apply_mask(stg, mlut, wave, lane);
+            if constexpr (BMK) sb.apply_mask(stg + A_STAGE, mlut, wave, lane);
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the masked chunks are in LDS
+        }
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if (kt < 40) GEMM_TP(2 + kt);
@@ -773,7 +789,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
 // and keeps 8 slab loads in flight; the scalar form (one dependent load chain per
 // element) ran at ~1.2 TB/s.
 __device__ __forceinline__ void slab_reduce_body(const float *slab, int splits, int M, int N, float *dst,
-                                                 long long ldw, int accumulate, int bid, int nblk) {
+                                                 long long ldw, int accumulate, int bid, int nblk,
+                                                 const float *cs) {
     const long long total = (long long)M * N;
     const long long step = (long long)nblk * blockDim.x;
     if ((N & 3) == 0) {
@@ -792,6 +809,10 @@ __device__ __forceinline__ void slab_reduce_body(const float *slab, int splits, 
             for (; k < splits; ++k) acc += __builtin_nontemporal_load(s4 + k * t4 + i);
             const long long e = 4 * i, m = e / N, n = e - m * N;
             float *d = dst + m * ldw + n;
+            if (cs) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) acc[u] *= cs[n + u];
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) d[u] = accumulate ? d[u] + acc[u] : acc[u];
         }
@@ -801,6 +822,7 @@ __device__ __forceinline__ void slab_reduce_body(const float *slab, int splits, 
         float s = 0.f;
         for (int k = 0; k < splits; ++k) s += slab[k * total + i];
         const long long m = i / N, n = i - m * N;
+        if (cs) s *= cs[n];
         float *d = dst + m * ldw + n;
         *d = accumulate ? *d + s : s;
     }
@@ -809,7 +831,7 @@ __device__ __forceinline__ void slab_reduce_body(const float *slab, int splits, 
 // bias column sums over the splits: 4 waves split the slabs of 64 columns, fixed-order
 // combine (the one-thread-per-column form was latency bound: 27 us for 86 splits)
 __device__ __forceinline__ void slab_reduce_cols_body(const float *slab, int splits, int N, float *dst,
-                                                      int accumulate, int bid) {
+                                                      int accumulate, int bid, const float *cs) {
     __shared__ float part[4][64];
     const int c = bid * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
     float s = 0.f;
@@ -819,31 +841,38 @@ __device__ __forceinline__ void slab_reduce_cols_body(const float *slab, int spl
     __syncthreads();
     if (g == 0 && c < N) {
         const int l = threadIdx.x & 63;
-        const float t = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+        float t = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+        if (cs) t *= cs[c];
         dst[c] = accumulate ? dst[c] + t : t;
     }
 }
 
 __global__ __launch_bounds__(256) void k_slab_reduce(const float *slab, int splits, int M, int N,
-                                                     float *dst, long long ldw, int accumulate) {
-    slab_reduce_body(slab, splits, M, N, dst, ldw, accumulate, blockIdx.x, gridDim.x);
+                                                     float *dst, long long ldw, int accumulate,
+                                                     const float *cs) {
+    slab_reduce_body(slab, splits, M, N, dst, ldw, accumulate, blockIdx.x, gridDim.x, cs);
 }
 // both reduces in one launch: the first ncb blocks sum the bias columns, the rest the
 // dW slabs (the column job alone is a few latency-bound blocks: 9.5 us per launch)
 __global__ __launch_bounds__(256) void k_slab_reduce_both(const float *slab, int splits, int M, int N,
                                                           float *dst, long long ldw, int accumulate,
-                                                          const float *bias_slab, float *bias_dst, int ncb) {
+                                                          const float *bias_slab, float *bias_dst, int ncb,
+                                                          const float *cs) {
     if ((int)blockIdx.x < ncb)
-        slab_reduce_cols_body(bias_slab, splits, N, bias_dst, accumulate, blockIdx.x);
+        slab_reduce_cols_body(bias_slab, splits, N, bias_dst, accumulate, blockIdx.x, cs);
     else
-        slab_reduce_body(slab, splits, M, N, dst, ldw, accumulate, blockIdx.x - ncb, gridDim.x - ncb);
+        slab_reduce_body(slab, splits, M, N, dst, ldw, accumulate, blockIdx.x - ncb, gridDim.x - ncb, cs);
 }
 
-__global__ void k_rows_sum(h16 *edge, const h16 *src, long long ld, int r0, int r1, int cols) {
+__global__ void k_rows_sum(h16 *edge, const h16 *src, long long ld, int r0, int r1, int cols,
+                           const uint8_t *mask) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= cols) return;
     float s = 0.f;
-    for (int r = r0; r < r1; ++r) s += h2f(src[(long long)r * ld + c]);
+    for (int r = r0; r < r1; ++r) {
+        const long long i = (long long)r * ld + c;
+        if (!mask || ((mask[i >> 3] >> (i & 7)) & 1u)) s += h2f(src[i]);
+    }
     edge[c] = f2h(s);
 }
 
@@ -946,6 +975,7 @@ static double op_src_bytes(const OpD &o, int f8) {
     // geometry is in 2-byte units, also for MXFP8 (there: payload bytes)
     double b = o.simple ? (double)o.nrows * o.ncols * 2.0 : (double)o.T * (o.hsrc > 0 ? o.hsrc : 1) * o.pw * 2.0;
     if (f8) b += b / 32.0;  // one E8M0 scale per 32 e4m3 values
+    if (o.mk) b += b / 16.0;  // one mask bit per fp16 element
     return b;
 }
 static double epi_bytes(const KfEpilogue &E, long long M, long long N) {
@@ -1034,6 +1064,15 @@ static bool to_dev(const KfOperand &d, OpD &o, const char *name) {
     }
     o.simple = d.nparts == 1 && d.hout == 1 && d.dt[0] == 0 && !edges;
     o.edges = edges;
+    if (d.mask) {
+        if (f8 || d.hout != 1 || d.mask_rows < 0) {
+            kf_set_error("operand %s: a mask needs an fp16 operand with hout 1", name);
+            return false;
+        }
+        o.mk = d.mask;
+        const long long lim = (long long)d.mask_rows * d.ld * 2;
+        o.mlim = lim > 0xFFFFFFF0LL ? 0xFFFFFFF0u : (unsigned)lim;
+    }
     o.ldb = (unsigned)(d.ld * 2 / u);
     o.pwb = (unsigned)(d.part_width * 2 / u);
     // 32-bit byte offsets (buffer addressing): the largest source row must fit
@@ -1334,6 +1373,25 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
             return launch<128, 128, 2, 2, true, true, false, 2, OP_SIMPLE, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
         return launch<128, 128, 2, 2, true, true, false, 2, OP_P2, OP_SIMPLE, 1>(M, N, K2, a, b, E, G, 1);
     }
+    if (a.mk || b.mk) {
+        // masked A (the TDNN-F affine input gradient on the implicit dz, N = bottleneck):
+        // 384x160 tiles for N = 160 / 320, 256x64 for N <= 64, else 128x128
+        if (!b.mk && B->kcontig && !E.out8 && ((am == OP_P2 && bm == OP_P2) || (am == OP_SIMPLE && bm == OP_SIMPLE))) {
+            const int mt = N % 160 == 0 && N <= 320 ? 5 : N <= 64 ? 2 : 0;
+#define KF_MASKED(AM_, BM_)                                                                                    \
+    do {                                                                                                       \
+        if (mt == 5) return launch<384, 160, 4, 2, true, true, false, 2, AM_ | OP_MASKED, BM_>(M, N, K, a, b, E, G, 1); \
+        if (mt == 2) return launch<256, 64, 4, 1, true, true, false, 2, AM_ | OP_MASKED, BM_>(M, N, K, a, b, E, G, 1);  \
+        return launch<128, 128, 2, 2, true, true, false, 2, AM_ | OP_MASKED, BM_>(M, N, K, a, b, E, G, 1);               \
+    } while (0)
+            if (am == OP_P2) KF_MASKED(OP_P2, OP_P2);
+            KF_MASKED(OP_SIMPLE, OP_SIMPLE);
+#undef KF_MASKED
+        }
+        kf_set_error("kf_gemm_fused: a masked operand must be A (plain or two-part time splice, with a "
+                     "k-contiguous B of the same kind, no MXFP8 copy) (M=%d N=%d K=%d)", M, N, K);
+        return -1;
+    }
     {  // the halo kernel shares fused_epilogue, MXFP8 copy included (BN >= 64)
         const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);
         if (hr != 0) return hr < 0 ? -1 : 0;
@@ -1377,7 +1435,7 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
 
 // split-K reduce of kf_gemm_wgrad's slabs (also used by conv_wgrad.hip)
 void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int M, int N, float *dW,
-                     long long ldw, float *bias_grad, int accumulate) {
+                     long long ldw, float *bias_grad, int accumulate, const float *cs) {
     const int nb = kf_blocks((long long)M * N / 4 + 1, 256, 4096);
     const int ncb = bias_grad ? (N + 63) / 64 : 0;
     ProfRec rec{};
@@ -1392,15 +1450,15 @@ void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int 
     }
     if (bias_grad && g_prof)
         hipExtLaunchKernelGGL(k_slab_reduce_both, dim3(ncb + nb), dim3(256), 0, kf_stream(), ea, eb, 0, slab, splits,
-                              M, N, dW, ldw, accumulate, bias_slab, bias_grad, ncb);
+                              M, N, dW, ldw, accumulate, bias_slab, bias_grad, ncb, cs);
     else if (bias_grad)
         k_slab_reduce_both<<<ncb + nb, 256, 0, kf_stream()>>>(slab, splits, M, N, dW, ldw, accumulate, bias_slab,
-                                                             bias_grad, ncb);
+                                                             bias_grad, ncb, cs);
     else if (g_prof)
         hipExtLaunchKernelGGL(k_slab_reduce, dim3(nb), dim3(256), 0, kf_stream(), ea, eb, 0, slab, splits, M, N, dW,
-                              ldw, accumulate);
+                              ldw, accumulate, cs);
     else
-        k_slab_reduce<<<nb, 256, 0, kf_stream()>>>(slab, splits, M, N, dW, ldw, accumulate);
+        k_slab_reduce<<<nb, 256, 0, kf_stream()>>>(slab, splits, M, N, dW, ldw, accumulate, cs);
 }
 
 int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
@@ -1426,8 +1484,8 @@ extern "C" int kf_gemm_wgrad_target(int wgs) {
     return old;
 }
 
-extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B,
-                             float *dW, long long ldw, float *bias_grad, int accumulate) {
+static int wgrad_impl(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW, long long ldw,
+                      float *bias_grad, int accumulate, const float *cs) {
     if (M <= 0 || N <= 0) return 0;
     OpD a, b;
     if (!to_dev(*A, a, "A") || !to_dev(*B, b, "B")) return -1;
@@ -1436,8 +1494,12 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         return -1;
     }
     if (!mn_gen_ok(a, "A") || !mn_gen_ok(b, "B")) return -1;
+    if (a.mk || (b.mk && (op_mode(b) != OP_SIMPLE || op_mode(a) == OP_GEN))) {
+        kf_set_error("kf_gemm_wgrad: a masked operand must be a plain B (A plain or a two-part time splice)");
+        return -1;
+    }
     // 3x3 convolutions: the source halo in LDS instead of nine im2col slabs
-    {
+    if (!b.mk) {
         const int hr = kf_conv_wgrad_halo_try(M, N, K, a, b, dW, ldw, bias_grad, accumulate);
         if (hr != 0) return hr < 0 ? -1 : 0;
     }
@@ -1504,13 +1566,31 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
         else                                                                                     \
             rc = launch<256, 64, 4, 1, false, false, true, 2, AM_, BM_>(M, N, K, a, b, E, G, splits); \
     } while (0)
-    if (bm == OP_SIMPLE && am == OP_SIMPLE) KF_WG(OP_SIMPLE, OP_SIMPLE);
+    if (b.mk) {
+        // masked B (the TDNN-F affine weight gradient on the implicit dz, N = layer width)
+        if (BNc != 256) {
+            kf_set_error("kf_gemm_wgrad: masked B needs N > 128 (M=%d N=%d)", M, N);
+            return -1;
+        }
+#define KF_WGM(AM_)                                                                                      \
+    do {                                                                                                 \
+        if (BMc == 320)                                                                                  \
+            rc = launch<320, 256, 2, 4, false, false, true, 2, AM_, OP_SIMPLE | OP_MASKED>(M, N, K, a, b, E, G, splits); \
+        else if (BMc == 192)                                                                             \
+            rc = launch<192, 256, 2, 4, false, false, true, 2, AM_, OP_SIMPLE | OP_MASKED>(M, N, K, a, b, E, G, splits); \
+        else                                                                                             \
+            rc = launch<256, 256, 2, 4, false, false, true, 2, AM_, OP_SIMPLE | OP_MASKED>(M, N, K, a, b, E, G, splits); \
+    } while (0)
+        if (am == OP_SIMPLE) KF_WGM(OP_SIMPLE);
+        else KF_WGM(OP_P2);
+#undef KF_WGM
+    } else if (bm == OP_SIMPLE && am == OP_SIMPLE) KF_WG(OP_SIMPLE, OP_SIMPLE);
     else if (bm == OP_SIMPLE && am == OP_P2) KF_WG(OP_P2, OP_SIMPLE);
     else if (bm == OP_SIMPLE) KF_WG(OP_GEN, OP_SIMPLE);
     else KF_WG(OP_GEN, OP_GEN);
 #undef KF_WG
     if (rc) return rc;
-    kf_wgrad_reduce(G.slab, G.bias_slab, splits, M, N, dW, ldw, bias_grad, accumulate);
+    kf_wgrad_reduce(G.slab, G.bias_slab, splits, M, N, dW, ldw, bias_grad, accumulate, cs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         kf_set_error("wgrad reduce: %s", hipGetErrorString(e));
@@ -1519,16 +1599,33 @@ extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOp
     return 0;
 }
 
-extern "C" int kf_rows_sum(void *edge, const void *src, long long ld, int r0, int r1, int cols) {
+extern "C" int kf_gemm_wgrad(int M, int N, int K, const KfOperand *A, const KfOperand *B,
+                             float *dW, long long ldw, float *bias_grad, int accumulate) {
+    return wgrad_impl(M, N, K, A, B, dW, ldw, bias_grad, accumulate, nullptr);
+}
+extern "C" int kf_gemm_wgrad_scaled(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW,
+                                    long long ldw, float *bias_grad, int accumulate, const float *col_scale) {
+    if (!col_scale) {
+        kf_set_error("kf_gemm_wgrad_scaled: null col_scale");
+        return -1;
+    }
+    return wgrad_impl(M, N, K, A, B, dW, ldw, bias_grad, accumulate, col_scale);
+}
+
+extern "C" int kf_rows_sum_mask(void *edge, const void *src, long long ld, int r0, int r1, int cols,
+                                const uint8_t *mask) {
     if (cols <= 0) return 0;
     k_rows_sum<<<(cols + 255) / 256, 256, 0, kf_stream()>>>((h16 *)edge, (const h16 *)src, ld,
-                                                            r0, r1, cols);
+                                                            r0, r1, cols, mask);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
         kf_set_error("rows_sum: %s", hipGetErrorString(e));
         return -1;
     }
     return 0;
+}
+extern "C" int kf_rows_sum(void *edge, const void *src, long long ld, int r0, int r1, int cols) {
+    return kf_rows_sum_mask(edge, src, ld, r0, r1, cols, nullptr);
 }
 
 // out[j] = rne_fp16(x0 . W[j] + x1 . W[rows + j]) for j < rows (W [2*rows x cols], fp32

@@ -27,6 +27,11 @@ struct OpD {
     const uint8_t *sc;
     unsigned lds;
     int pw8;            // part width in fp8 elements
+    // masked operand (KfOperand.mask): element i of the source (linear index, ld-strided)
+    // reads as zero unless bit i of mk is set; source bytes >= mlim (rows past the mask,
+    // e.g. an edge row) are unmasked
+    const uint8_t *mk;
+    unsigned mlim;
 };
 
 // compile-time loop: body(I) with I a std::integral_constant (forces full unrolling,
@@ -130,6 +135,8 @@ __device__ __forceinline__ half8 load_frag(const char *tile, int idx0, int s, in
 // ---------------------------------------------------------------------------
 // operand kinds, chosen on the host: the stager keeps only the state its kind needs
 enum { OP_SIMPLE = 0, OP_P2 = 1, OP_GEN = 2 };
+// or-ed into a gemm_kernel operand mode: the operand is masked (Stager MK)
+constexpr int OP_MASKED = 8;
 constexpr unsigned BAD = 0xFFFFFFFFu;  // byte offset that reads as zero (buffer range check)
 
 // buffer resource (SGPR quad): base, stride 0, 2^32 - 1 records (an offset of BAD reads
@@ -176,7 +183,7 @@ __device__ __forceinline__ unsigned op_boff(const OpD &d, int t, int h, int kk, 
     return off < 0 ? BAD : (unsigned)(off * 2);
 }
 
-template <bool KC, int TR, int MODE, int NW>
+template <bool KC, int TR, int MODE, int NW, bool MK = false>
 struct Stager {
     // 1 KiB pieces (= chunks) per thread; when TR / 8 pieces do not split evenly over
     // the waves (160-row tiles on 8 waves) the last wave issues fewer (wave-uniform skip)
@@ -188,6 +195,7 @@ struct Stager {
     unsigned o1[MODE == OP_P2 && KC ? NC : 1];  // KC/P2: part-1 row byte offset
     int th[MODE == OP_GEN ? NC : 1];    // GEN: KC packed (t<<8)|h ; MN packed part info
     int dt1[!KC && MODE != OP_SIMPLE ? NC : 1];  // MN: dt of the chunk's part
+    unsigned mbv[MK ? NC : 1];          // MK: the mask byte of each chunk of the last issue
     int curp;
 
     __device__ __forceinline__ static int kc_row(int q, int lane) { return q * 8 + (lane >> 3); }
@@ -315,10 +323,47 @@ struct Stager {
                     }
                 }
             }
+            if constexpr (MK) {
+                // a 16-byte chunk is 8 consecutive source elements at an 8-aligned linear
+                // index: one mask byte, loaded ahead of the chunk itself
+                mbv[j] = 0xFFu;
+                if ((EVEN || q < NP) && voff < d.mlim) mbv[j] = d.mk[voff >> 4];
+            }
             if (EVEN || q < NP) lds_dma<16>(rs, dst + q * 1024, voff);
         });
     }
+
+    // MK: zero the masked elements of this thread's chunks of the stage at `dst` once they
+    // have landed (after the stage's vmcnt wait, before the barrier that publishes it).
+    // lut: 256 x 16-byte AND masks in LDS (byte b -> fp16 lane e kept iff bit e of b)
+    __device__ __forceinline__ void apply_mask(char *dst, const uint4 *lut, int wave, int lane) const {
+        static_for<NC>([&](auto J) {
+            constexpr int j = decltype(J)::value;
+            const int q = wave * NC + j;
+            if (EVEN || q < NP) {
+                uint4 *p = reinterpret_cast<uint4 *>(dst + q * 1024 + 16 * lane);
+                const uint4 m = lut[mbv[j] & 0xFFu];
+                uint4 v = *p;
+                v.x &= m.x;
+                v.y &= m.y;
+                v.z &= m.z;
+                v.w &= m.w;
+                *p = v;
+            }
+        });
+    }
 };
+
+// the 256-entry AND-mask table of Stager::apply_mask, filled by the whole workgroup
+__device__ __forceinline__ void mask_lut_fill(uint4 *lut, int tid, int nth) {
+    for (int b = tid; b < 256; b += nth) {
+        unsigned w[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+            w[d] = (((b >> (2 * d)) & 1u) ? 0x0000FFFFu : 0u) | (((b >> (2 * d + 1)) & 1u) ? 0xFFFF0000u : 0u);
+        lut[b] = uint4{w[0], w[1], w[2], w[3]};
+    }
+}
 
 // s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0], vmcnt[5:4] at 15:14)
 template <int N>

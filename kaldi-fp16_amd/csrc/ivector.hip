@@ -139,7 +139,12 @@ __global__ void k_scale_cols(const h16 *x, long long ldx, const float *scale, h1
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
          i += (long long)gridDim.x * blockDim.x) {
         const int r = (int)(i / cols), c = (int)(i - (long long)r * cols);
-        y[(long long)r * ldy + c] = (h16)((float)x[(long long)r * ldx + c] * scale[c]);
+        // the fp32 product, then one RNE to fp16 (the oracle's rounding points); without the
+        // barrier hipcc fuses both into v_fma_mixlo_f16, which rounds the exact product once
+        // and differs from rne(fp32 product) at near-ties
+        float p = (float)x[(long long)r * ldx + c] * scale[c];
+        asm volatile("" : "+v"(p));
+        y[(long long)r * ldy + c] = (h16)p;
     }
 }
 

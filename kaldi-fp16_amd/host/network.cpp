@@ -217,6 +217,16 @@ struct KfNet {
     void *wg_stream = nullptr, *ev_go = nullptr, *ev_side = nullptr;
     void *hp_stream = nullptr;  // high-priority stream for the input-gradient chain
     int wg_side = 1;
+    // Implicit dz (nnet_set_implicit_dz, default off, fp16 step): the input-gradient epilogue
+    // that produces a TDNN-F layer's g stores no dz = rne(g * bnscale * mask); the layer's
+    // affine weight and input gradients read g through the forward's ReLU mask (masked
+    // operands, kf_ops.h) with the BN scale folded into W2 (w2s scratch) or the weight
+    // gradient's reduction. One full-width fp16 tensor fewer written per TDNN-F layer, but
+    // step-neutral on the MI355X (the linear input gradient's saving is spent
+    // by the masked affine input gradient on the same chain), so off by default.
+    int implicit_dz = 0;
+    bool dz_imp[2] = {false, false};  // dz[i] was left implicit by the producing epilogue
+    void *w2s = nullptr;              // [kaff x dout] fp16: W2 with the BN scale folded in
     void *dbott_last = nullptr;  // the dbott buffer of the last TDNN-F / prefinal step (tests)
     size_t edge_half = 0;
     int fp8 = 0;
@@ -746,6 +756,17 @@ static bool alloc_device(KfNet *net, int max_frames) {
     }
     net->dbott = net->dalloc((T + 2) * maxw * 2);
     net->dbott2 = net->dalloc((T + 2) * maxw * 2);
+    {
+        size_t w2 = 0;
+        for (auto &nl : net->layers)
+            if (nl.L.type == LayerType::TDNNF)
+                w2 = std::max(w2, (size_t)(nl.L.time_stride > 0 ? 2 : 1) * nl.L.bottleneck * nl.L.out_dim * 2);
+        net->w2s = w2 ? net->dalloc(w2) : nullptr;
+        if (w2 && !net->w2s) {
+            set_err("alloc backward scratch");
+            return false;
+        }
+    }
     net->edge_half = align_up(maxw * 2, 256);
     net->edge = net->dalloc(net->edge_half * 2);
     if (!net->dz[0] || !net->dz[1] || !net->g[0] || !net->g[1] || !net->dbott || !net->dbott2 || !net->edge) {
@@ -1424,6 +1445,8 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
     const int w = L.out_dim;
     E.ldo2 = w;
     E.out2 = dz_out;
+    const int di = dz_out == net->dz[0] ? 0 : dz_out == net->dz[1] ? 1 : -1;
+    if (di >= 0) net->dz_imp[di] = false;
     switch (L.type) {
         case LayerType::TDNNF: {
             E.scale2 = pl.bn_scale;
@@ -1431,6 +1454,16 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
             if (pl.bypass) {
                 E.out = g_out;
                 E.ldo = w;
+                // implicit dz: g is stored anyway, its consumers apply mask and scale (the
+                // masked weight gradient needs 256-column tiles: w > 128, not 160 / 320)
+                const bool shape_ok = w > 128 && !(w % 160 == 0 && w <= 320);
+                if (net->implicit_dz && !net->fp8 && di >= 0 && pl.mask && pl.bn_scale && net->w2s && shape_ok) {
+                    E.out2 = nullptr;
+                    E.scale2 = nullptr;
+                    E.mask_in = nullptr;
+                    net->dz_imp[di] = true;
+                    return true;
+                }
             }
             // MXFP8 train step: also the e4m3 copy of dz_P for P's affine input gradient; only
             // when the copy's row is exactly w wide (w % 128 == 0), so the dgrad GEMM's K range
@@ -1691,15 +1724,36 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
             case LayerType::TDNNF: {
                 const int s = L.time_stride, bn = L.bottleneck;
                 const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
+                // implicit dz (dx_epilogue): the layer's g read through its ReLU mask, the BN
+                // scale applied to the weight gradient's columns and folded into W2 below
+                const int ib = dz == net->dz[0] ? 0 : dz == net->dz[1] ? 1 : -1;
+                const bool imp = ib >= 0 && net->dz_imp[ib];
+                const void *dzs = imp ? gcur : dz;
+                auto masked = [&](KfOperand o) {
+                    if (imp) {
+                        o.mask = nl.mask;
+                        o.mask_rows = T;
+                    }
+                    return o;
+                };
                 // affine weight / bias gradient: splice+(bott)^T . dz
                 KfOperand A = s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 0)
                                     : op_base(nl.aux, bn, T, bn, 0);
-                KfOperand B = op_base(dz, dout, T, dout, 0);
+                KfOperand B = masked(op_base(dzs, dout, T, dout, 0));
                 if (!wgrad([&] {
+                        if (imp)
+                            return ck(kf_gemm_wgrad_scaled(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout,
+                                                           gptr(net, nl.pb2), 0, nl.bn_scale),
+                                      "tdnnf affine wgrad");
                         return ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
                                   "tdnnf affine wgrad");
                     }))
                     return -1;
+                const void *w2 = wptr(net, nl.pW2);
+                if (imp) {
+                    if (!ck(kf_scale_cols(w2, dout, nl.bn_scale, net->w2s, dout, kaff, dout), "tdnnf scaled W2")) return -1;
+                    w2 = net->w2s;
+                }
                 // bottleneck gradient: transpose of the [0, +s] clamped splice
                 void *dbott = dbott_buf;
                 net->dbott_last = dbott;
@@ -1708,11 +1762,14 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 E1.ldo = bn;
                 const int i8 = dz == net->dz[0] ? 0 : dz == net->dz[1] ? 1 : -1;
                 if (s > 0) {
-                    // spare row T of dz holds sum_{t >= T-1-s} dz[t] (clamped-splice transpose)
-                    void *edge = (char *)dz + (size_t)T * dout * 2;
-                    if (!ck(kf_rows_sum(edge, dz, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout), "edge"))
+                    // spare row T of dz (of g when dz is implicit: the masked sum) holds
+                    // sum_{t >= T-1-s} dz[t] (clamped-splice transpose)
+                    void *edge = (char *)dzs + (size_t)T * dout * 2;
+                    if (!ck(kf_rows_sum_mask(edge, dzs, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout,
+                                             imp ? nl.mask : nullptr),
+                            "edge"))
                         return -1;
-                    KfOperand B1 = op_wrows(wptr(net, nl.pW2), 2, bn, dout);
+                    KfOperand B1 = op_wrows(w2, 2, bn, dout);
                     if (net->fp8 && i8 >= 0 && net->dz8_layer[i8] == li && T > 1) {
                         // MXFP8 (the one MFMA-bound backward product, K = 2 x dout): rows
                         // 0 .. T-2 from dz's e4m3 copy [dz(t) | dz(t-s)] against the e4m3
@@ -1736,15 +1793,15 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                                 "tdnnf affine dgrad edge row"))
                             return -1;
                     } else {
-                        KfOperand A1 = op_splice(dz, T, dout, 0, -s, KF_ZERO, 1);
+                        KfOperand A1 = masked(op_splice(dzs, T, dout, 0, -s, KF_ZERO, 1));
                         A1.edge_t[1] = T - 1;
                         A1.edge_row[1] = T;
                         if (!ck(kf_gemm_fused(T, bn, 2 * dout, &A1, &B1, &E1), "tdnnf affine dgrad"))
                             return -1;
                     }
                 } else {
-                    KfOperand A1 = op_base(dz, dout, T, dout, 1);
-                    KfOperand B1 = op_base(wptr(net, nl.pW2), dout, bn, dout, 1);
+                    KfOperand A1 = masked(op_base(dzs, dout, T, dout, 1));
+                    KfOperand B1 = op_base(w2, dout, bn, dout, 1);
                     if (!ck(kf_gemm_fused(T, bn, dout, &A1, &B1, &E1), "tdnnf affine dgrad")) return -1;
                 }
                 // linear weight gradient: splice-(x)^T . dbott
@@ -1986,6 +2043,12 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         set_err(std::string("dp join: ") + (kf_dp_last_error() ? kf_dp_last_error() : ""));
         return -1;
     }
+    return 0;
+}
+
+extern "C" int nnet_set_implicit_dz(KfNet *net, int on) {
+    if (!net) return -1;
+    net->implicit_dz = on != 0;
     return 0;
 }
 

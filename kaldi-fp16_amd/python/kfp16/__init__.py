@@ -99,6 +99,7 @@ _sig(nnet, "nnet_bind_dp", _i, _vp, _vp, _ll)
 _sig(nnet, "nnet_dp_plan", _i, _vp, _ll, _i, C.POINTER(_i), C.POINTER(_ll), C.POINTER(_ll))
 _sig(nnet, "nnet_dp_debug_early", _i, _vp, _i)
 _sig(nnet, "nnet_set_wgrad_stream", _i, _vp, _i)
+_sig(nnet, "nnet_set_implicit_dz", _i, _vp, _i)
 _sig(nnet, "nnet_weights_changed", _i, _vp)
 # kf_dp.h (RCCL data parallel)
 _sig(core, "kf_dp_last_error", C.c_char_p)
@@ -364,6 +365,11 @@ class Network:
         on; kf_nnet.h nnet_set_wgrad_stream)."""
         check(nnet.nnet_set_wgrad_stream(self.h, int(on)), "nnet_set_wgrad_stream")
 
+    def set_implicit_dz(self, on: bool):
+        """TDNN-F input gradients without the stored dz: consumers read g through the ReLU
+        mask (default off; kf_nnet.h nnet_set_implicit_dz)."""
+        check(nnet.nnet_set_implicit_dz(self.h, int(on)), "nnet_set_implicit_dz")
+
     def dp_debug_early(self, on: bool):
         """Test hook: issue every gradient bucket before the backward runs (the
         negative control of the overlap tests)."""
@@ -407,7 +413,7 @@ class KfOperand(C.Structure):
                 ("nparts", _i), ("part_width", _i), ("T", _i), ("hout", _i), ("hsrc", _i),
                 ("hmul", _i), ("hdiv", _i), ("tpolicy", _i), ("dt", _i * MAXP), ("dh", _i * MAXP),
                 ("edge_t", _i * MAXP), ("edge_row", _i * MAXP), ("fmt", _i), ("scales", _vp),
-                ("lds", _ll)]
+                ("lds", _ll), ("mask", _vp), ("mask_rows", _i)]
 
 
 FMT_FP16, FMT_MXFP8 = 0, 1
@@ -421,9 +427,13 @@ class KfEpilogue(C.Structure):
 
 
 def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, hout=1, hsrc=1,
-            hmul=0, hdiv=1, tpolicy=0, dt=(), dh=(), edges=(), scales=None, lds=0):
-    """scales != None makes an MXFP8 operand (base: e4m3 bytes, scales: E8M0, lds bytes/row)"""
+            hmul=0, hdiv=1, tpolicy=0, dt=(), dh=(), edges=(), scales=None, lds=0, mask=None, mask_rows=0):
+    """scales != None makes an MXFP8 operand (base: e4m3 bytes, scales: E8M0, lds bytes/row);
+    mask != None a masked fp16 operand (kf_ops.h: bit i of mask gates source element i of the
+    first mask_rows source rows)"""
     o = KfOperand()
+    if mask is not None:
+        o.mask, o.mask_rows = mask, mask_rows
     if scales is not None:
         o.fmt, o.scales, o.lds = FMT_MXFP8, scales, lds
     o.base, o.ld, o.nrows, o.ncols, o.kcontig = base, ld, rows, cols, kcontig
@@ -445,6 +455,10 @@ def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, ho
 _sig(core, "kf_gemm_fused", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), C.POINTER(KfEpilogue))
 _sig(core, "kf_gemm_wgrad", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i)
 _sig(core, "kf_rows_sum", _i, _vp, _vp, _ll, _i, _i, _i)
+_sig(core, "kf_rows_sum_mask", _i, _vp, _vp, _ll, _i, _i, _i, _vp)
+_sig(core, "kf_scale_cols", _i, _vp, _ll, _vp, _vp, _ll, _i, _i)
+_sig(core, "kf_gemm_wgrad_scaled", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i,
+     _vp)
 _sig(core, "kf_gemm_debug_kil", None, _i)
 _sig(core, "kf_gemm_trace", None, _vp, _i, _i)
 _sig(core, "kf_quant_mxfp8", _i, _vp, _ll, _i, _i, _i, _vp, _ll, _vp, _ll)

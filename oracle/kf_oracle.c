@@ -743,17 +743,21 @@ int orc_net_backward_top(OrcNet *net, const float *features, const float *out_gr
             }
             case ORC_TDNNF: {
                 const int s = L->stride, bn = L->bn_dim;
+                /* implicit dz (kf_oracle.h): the GPU's dx_epilogue stores no dz for this layer */
+                const int imp = net->implicit_dz && mode == ORC_ROUND_FUSED && !net->mx8 && li != top_li &&
+                                L->bypass > 0.f && din == dout && dout > 128 && !(dout % 160 == 0 && dout <= 320);
                 float *dz = (float *)xalloc(sizeof(float) * (size_t)T * dout);
                 for (long long i = 0; i < (long long)T * dout; ++i) {
                     int d = (int)(i % dout);
-                    dz[i] = net->mask[li][i] ? g[i] * bn_scale(&L->bn, d) : 0.f;
+                    if (imp) dz[i] = net->mask[li][i] ? gr[i] : 0.f;  /* rne(v) masked, unscaled */
+                    else dz[i] = net->mask[li][i] ? g[i] * bn_scale(&L->bn, d) : 0.f;
                 }
                 /* MXFP8 train step (network.cpp backward_impl): the affine input gradient of a
                    strided layer reads the e4m3 copy of the unrounded dz and of W2's rows, except
                    for row T-1 (the clamped-edge row), which stays fp16 */
                 float *dz8 = NULL;
                 if (net->mx8 && s > 0 && T > 1 && mx_dgrad_layer(net, li)) dz8 = mx_rows_new(dz, T, dout);
-                if (mode) orc_round_f16(dz, (long long)T * dout);
+                if (mode && !imp) orc_round_f16(dz, (long long)T * dout);
                 const float *bott = net->aux[li];
                 const int kaff = s > 0 ? 2 * bn : bn, klin = s > 0 ? 2 * din : din;
                 float *aff_in = s > 0 ? splice_plus(bott, T, bn, s) : (float *)bott;
@@ -761,8 +765,24 @@ int orc_net_backward_top(OrcNet *net, const float *features, const float *out_gr
                 matmul_tn(kaff, dout, T, aff_in, dz, net->gW2[li]);
                 if (s > 0) free(aff_in);
                 net->gb2[li] = colsum(dz, T, dout);
+                const float *w2 = L->W2;
+                float *w2s = NULL;
+                if (imp) {
+                    /* the BN scale after the reduction (kf_gemm_wgrad_scaled) and folded into
+                       rne(W2 * scale) for the input gradient (kf_scale_cols) */
+                    for (int r = 0; r < kaff; ++r)
+                        for (int d = 0; d < dout; ++d) net->gW2[li][(size_t)r * dout + d] *= bn_scale(&L->bn, d);
+                    for (int d = 0; d < dout; ++d) net->gb2[li][d] *= bn_scale(&L->bn, d);
+                    w2s = (float *)xalloc(sizeof(float) * (size_t)kaff * dout);
+                    for (int r = 0; r < kaff; ++r)
+                        for (int d = 0; d < dout; ++d)
+                            w2s[(size_t)r * dout + d] = L->W2[(size_t)r * dout + d] * bn_scale(&L->bn, d);
+                    orc_round_f16(w2s, (long long)kaff * dout);
+                    w2 = w2s;
+                }
                 float *daff = (float *)xalloc(sizeof(float) * (size_t)T * kaff);
-                matmul_nt(T, kaff, dout, dz, L->W2, daff);
+                matmul_nt(T, kaff, dout, dz, w2, daff);
+                free(w2s);
                 float *daff8 = daff;
                 if (dz8) {
                     float *w8 = mx_rows_new(L->W2, kaff, dout);

@@ -112,6 +112,12 @@ typedef struct {
     /* MXFP8 copy of the features (dequantised, [T x feat_dim]) for a layer reading the
      * input directly: lets a test run one layer on the GPU's own fp8 input (mx8 only) */
     const float *feat8;
+    /* F mode: emulate the GPU's implicit dz (kf_nnet.h nnet_set_implicit_dz, network.cpp
+     * dx_epilogue): for a TDNN-F layer with a bypass whose gradient comes from the layer
+     * above, dz is the stored g = rne(v) under the ReLU mask, the affine weight / bias
+     * gradients are scaled by the BN scale after the reduction and the affine input
+     * gradient uses rne(W2 * bnscale). Not with mx8 (the GPU's fp8 steps store dz). */
+    int implicit_dz;
 } OrcNet;
 
 /* OCP MXFP8 quantise-dequantise of rows of `cols` (cols % 32 == 0) values:

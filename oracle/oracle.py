@@ -114,7 +114,7 @@ class OrcNet(C.Structure):
                 ("gW2", C.POINTER(_fp)), ("gb2", C.POINTER(_fp)), ("gact", C.POINTER(_fp)),
                 ("force_mask", C.POINTER(C.POINTER(C.c_uint8))), ("mx8", C.c_int),
                 ("act8", C.POINTER(_fp)), ("ivec", _fp), ("B", C.c_int), ("ivec_dim", C.c_int),
-                ("seq_off", C.POINTER(C.c_int)), ("feat8", _fp)]
+                ("seq_off", C.POINTER(C.c_int)), ("feat8", _fp), ("implicit_dz", C.c_int)]
 
 
 def parse_xconfig(text: str):
@@ -217,7 +217,7 @@ class OracleNet:
     bns: (layer, which) -> (mean, var, gamma, beta)."""
 
     def __init__(self, xconfig: str, params: dict, bns: dict, round_mode=ROUND_FUSED, threads=None,
-                 mx8=False):
+                 mx8=False, implicit_dz=False):
         self.L = parse_xconfig(xconfig)
         self.keep = []
         index = {"ivector": -2}
@@ -283,6 +283,8 @@ class OracleNet:
         self.index = index
         self.round_mode = round_mode
         self.mx8 = int(mx8)    # emulate the GPU's MXFP8 step (kf_nnet.h nnet_set_fp8: 1, or 2 = fp16 backward)
+        # F mode: the GPU's implicit TDNN-F dz (kf_nnet.h nnet_set_implicit_dz, default off)
+        self.implicit_dz = int(implicit_dz)
         if threads:
             lib().orc_set_threads(int(threads))
         self.net = None
@@ -323,6 +325,7 @@ class OracleNet:
         self.net.feat_dim = x.shape[1]
         self.net.round_mode = self.round_mode
         self.net.mx8 = int(self.mx8)   # 1: MX forward + MX strided affine dgrad; 2: MX forward only
+        self.net.implicit_dz = int(self.implicit_dz)
         if ivectors is not None:
             iv = np.ascontiguousarray(ivectors, dtype=np.float32)
             so = np.ascontiguousarray(seq_off, dtype=np.int32)

@@ -9,4 +9,4 @@ for line in open(sys.argv[1]):
     if line.startswith("{") and '"metric"' in line:
         d = json.loads(line)
         print(f"med {d['ms_per_step']} mean {d.get('ms_per_step_mean')} value {d['value']:.0f} "
-              f"box {d.get('box', {}).get('copy_GBps')} GB/s wgrad_stream {d.get('wgrad_stream')} steps {d.get('step_ms')}")
+              f"box {d.get('box', {}).get('copy_GBps')} GB/s wgrad_stream {d.get('wgrad_stream')} steps {d.get('step_ms')} issue {d.get('cpu_issue_ms')}")

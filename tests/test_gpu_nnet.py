@@ -100,6 +100,43 @@ def test_tiny_network_forward_backward(gpu, T):
     assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
 
 
+@pytest.mark.parametrize("implicit", [False, True])
+def test_tiny_backward_dz_modes(gpu, implicit):
+    """nnet_set_implicit_dz off (dz stored by the producing epilogue) and on (g read
+    through the ReLU mask, the BN scale folded into W2 / the wgrad reduce), each against the
+    oracle at the matching rounding points (kf_oracle.h implicit_dz); the two GPU modes
+    agree with each other to a few fp16 roundings."""
+    kfp16 = gpu
+    from kfp16 import synth
+    xcfg = synth.load_xconfig("tiny.xconfig")
+    T = 517
+    net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
+    masks = net.relu_masks()
+    tp = {k: synth.trunc_fp16(v) for k, v in params.items()}
+    on = oracle.OracleNet(xcfg, tp, bns, round_mode=oracle.ROUND_FUSED, threads=16, implicit_dz=implicit)
+    on.forward(feats.astype(np.float32), force_masks=masks)
+    P = net.layers[-1][3]
+    og = (np.random.default_rng(11).standard_normal((T, P)) * 0.05).astype(np.float16)
+    gbuf = kfp16.upload_fp16(og)
+    grads = {}
+    for mode in (not implicit, implicit):  # the mode under test last
+        net.set_implicit_dz(mode)
+        net.backward(gbuf.ptr)
+        grads[mode] = net.read_grads()
+    net.set_implicit_dz(False)
+    on.backward(og.astype(np.float32))
+    ref = on.grads()
+    got = grads[implicit]
+    errs = {k: rel_fro(got[k], ref[k]) for k in ref}
+    bad = {k: v for k, v in errs.items() if v > 5e-3}
+    assert not bad, "grad errors: " + ", ".join(f"{k}={v:.2e}" for k, v in errs.items())
+    cross = {k: rel_fro(grads[True][k], grads[False][k]) for k in ref}
+    assert max(cross.values()) <= 2e-3, cross
+    # the implicit mode reaches the TDNN-F layers with a bypass (tdnnf6-8)
+    if implicit:
+        assert any(cross[k] > 0 for k in cross if k.startswith("tdnnf7")), cross
+
+
 def test_sgd_step_matches_oracle(gpu):
     kfp16 = gpu
     from kfp16 import synth
@@ -130,17 +167,22 @@ def test_sgd_step_matches_oracle(gpu):
 
 
 @pytest.mark.slow
-def test_full_model_one_eg(gpu):
-    """The benchmark model (cnn_tdnn_17f) on one 1500-frame eg."""
+@pytest.mark.parametrize("implicit", [False, True])
+def test_full_model_one_eg(gpu, implicit):
+    """The benchmark model (cnn_tdnn_17f) on one 1500-frame eg; the backward with the
+    stored dz (default) and with the implicit dz (the 384x160 masked affine input
+    gradients and 320x256 masked weight gradients of the 1536-wide layers)."""
     kfp16 = gpu
     from kfp16 import synth
     xcfg = synth.load_xconfig("cnn_tdnn_17f.xconfig")
     T = 1500
     net, params, bns, feats, fbuf = _run_product(kfp16, xcfg, T)
+    net.set_implicit_dz(implicit)
     on = _oracle(xcfg, params, bns, feats)
     masks = _forward_parity(net, on, None)
     on.close()
     on = _oracle(xcfg, params, bns, feats)
+    on.implicit_dz = int(implicit)
     on.forward(feats.astype(np.float32), force_masks=masks)
     og = (np.random.default_rng(7).standard_normal((T, 3080)) * 0.02).astype(np.float16)
     gbuf = kfp16.upload_fp16(og)
