@@ -1573,12 +1573,11 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     } restore{caller};
     // With the weight-gradient stream the input-gradient chain runs on a high-priority
     // stream (its workgroups are dispatched ahead of the weight gradients') and each weight
-    // gradient launches 256 workgroups instead of 512. A/B on one box (bench default, r5):
-    // one stream 49.1-49.5 ms, two streams 41.0-41.4, + priority 40.7, + 256 40.8, both
-    // 39.1-39.4 ms (a box whose memory-bound kernels run ~1.3x slower than the fastest
-    // ones'; on a fast box the two-stream order measured 37.3 against 37.1 ms).
-    // (A/B knobs: KF_BWD_HP=0 keeps the chain on the caller's stream, KF_BWD_WGT=<n> sets
-    // the weight gradients' workgroup target)
+    // gradient launches 256 workgroups instead of 512. Same-box A/B (bench default, 20
+    // steps, median): one stream 38.13 / 38.36 ms, two streams 37.57 / 37.52;
+    // the chain's priority is neutral (37.55 without it), 512-workgroup weight gradients
+    // cost 1.2 ms (38.78). (A/B knobs: KF_BWD_HP=0 keeps the chain on the caller's stream,
+    // KF_BWD_WGT=<n> sets the weight gradients' workgroup target)
     static const int env_hp = getenv("KF_BWD_HP") ? atoi(getenv("KF_BWD_HP")) : 1;
     static const int env_wgt = getenv("KF_BWD_WGT") ? atoi(getenv("KF_BWD_WGT")) : 256;
     const bool hp = two && net->hp_stream && env_hp;
