@@ -218,9 +218,11 @@ def step_classes(cls, steps, peak_tflops):
 def roofline(prof, steps, peak_tflops):
     """Dominant GEMM class: algorithmic FLOPs and algorithmic HBM bytes (kf_prof_collect2)
     over its HIP-event time on the launch stream. `bound` names the longer floor (FLOPs at
-    the dense MFMA peak, bytes at the HBM peak), or "latency" when both floors are under
-    half the measured time: then neither roof binds, and `achieved` / `frac` stay those of
-    the longer floor's unit, with both fractions beside them."""
+    the dense MFMA peak, bytes at the HBM peak); `regime` is "latency" when both floors are
+    under half the measured time (neither roof binds), else the bound. `achieved` / `frac`
+    are in the bound's unit, with both fractions beside them. With the weight-gradient
+    stream the class's launches share the device with weight gradients, so
+    their event times include that sharing."""
     dom = max(prof, key=lambda k: prof[k][1])
     n, ms, fl, by = prof[dom]
     t_mfma = fl / (peak_tflops * 1e12)
@@ -234,9 +236,7 @@ def roofline(prof, steps, peak_tflops):
     else:
         r = {"bound": "mfma", "achieved": round(tf, 2), "peak": peak_tflops, "unit": "TFLOP/s",
              "frac": round(tf / peak_tflops, 4)}
-    if sec > 0 and max(t_hbm, t_mfma) < 0.5 * sec:
-        r["bound"] = "latency"
-        r["longer_floor"] = "hbm" if t_hbm > t_mfma else "mfma"
+    r["regime"] = "latency" if sec > 0 and max(t_hbm, t_mfma) < 0.5 * sec else r["bound"]
     r.update({"kernel": dom, "launches": n, "kernel_ms_per_step": round(ms / steps, 3),
               "mfma_tflops": round(tf, 2), "mfma_frac": round(tf / peak_tflops, 4),
               "alg_GBps": round(gbps, 1), "hbm_frac": round(gbps / PEAK_HBM_GBPS, 4),
