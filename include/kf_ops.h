@@ -183,6 +183,12 @@ int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs);
  * fp16 row-major, fp32 accumulation; cols % 8 == 0, 16-byte aligned pointers (out is not
  * required to be: it is written per element). One row of a two-part product. */
 int kf_dot2_rows(void *out, const void *x0, const void *x1, const void *W, int rows, int cols);
+/* kf_gemm_fused of an MXFP8 product (rows 0 .. M-1), whose last row tile's workgroups also
+ * compute kf_dot2_rows(edge_out, x0, x1, W, N, cols): the TDNN-F affine input gradient's
+ * clamped-edge row T - 1 (M = T - 1) in the same launch. As a separate one-row kernel beside
+ * the weight-gradient stream it waited ~340 us per layer for CU slots (3072 model). */
+int kf_gemm_fused_edge(int M, int N, int K, const KfOperand *A, const KfOperand *B, const KfEpilogue *epi,
+                       void *edge_out, const void *x0, const void *x1, const void *W, int cols);
 
 /* edge[c] = rne_fp16(sum_{r in [r0, r1)} src[r*ld + c]) for c < cols
  * (edge may be a spare row of src's own allocation) */

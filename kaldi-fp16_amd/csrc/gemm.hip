@@ -56,6 +56,11 @@ struct WgradArgs {
     // (tid 0), then per block {start, end, hw id | xcc id << 32}
     unsigned long long *trace;
     int trace_blk;
+    // fused MXFP8 only (kf_gemm_fused_edge): the last M tile's workgroups also write the fp16
+    // row eo[j] = sum_c ex0[c] ew[j][c] + ex1[c] ew[N + j][c] for their columns j
+    h16 *eo;
+    const h16 *ex0, *ex1, *ew;
+    int ecols;
 };
 
 template <int BM, int BN, int ST, int SCB = 0>
@@ -557,6 +562,26 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void gemm_kernel(int M, int N, int
     } else {
         GEMM_TP(42);
         fused_epilogue<BM, BN, WM, WN>(acc, smem, E, M, N, m0, n0, tid, lane, wave, &epre);
+        if constexpr (F8) {
+            if (G.eo && mt == n_mtiles - 1) {
+                // the clamped-edge row of the TDNN-F affine input gradient in fp16 (its second
+                // part is a sum of rows, which the MXFP8 operand does not hold): one wave per
+                // output column, 8-element chunks per lane, fixed-order wave reduction
+                for (int j = n0 + wave; j < min(n0 + BN, N); j += NW) {
+                    const h16 *w0 = G.ew + (long long)j * G.ecols, *w1 = G.ew + (long long)(N + j) * G.ecols;
+                    float a = 0.f;
+                    for (int c = 8 * lane; c < G.ecols; c += 8 * 64) {
+                        const half8 x = load_h8(G.ex0 + c), y = load_h8(G.ex1 + c), u = load_h8(w0 + c),
+                                    v = load_h8(w1 + c);
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) a = fmaf((float)x[e], (float)u[e], fmaf((float)y[e], (float)v[e], a));
+                    }
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+                    if (lane == 0) G.eo[j] = f2h(a);
+                }
+            }
+        }
     }
     GEMM_TP(43);
     if (trb) G.trace[64 + 3 * bid + 1] = wall_clock64();
@@ -1317,8 +1342,31 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
 static int g_kil = 1;
 extern "C" void kf_gemm_debug_kil(int on) { g_kil = on != 0; }
 
+static int fused_impl(int M, int N, int K, const KfOperand *A, const KfOperand *B, const KfEpilogue *epi,
+                      const WgradArgs *edge);
 extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOperand *B,
                              const KfEpilogue *epi) {
+    return fused_impl(M, N, K, A, B, epi, nullptr);
+}
+extern "C" int kf_gemm_fused_edge(int M, int N, int K, const KfOperand *A, const KfOperand *B,
+                                  const KfEpilogue *epi, void *edge_out, const void *x0, const void *x1,
+                                  const void *W, int cols) {
+    if (!edge_out || !x0 || !x1 || !W || cols <= 0 || cols % 8 || ((uintptr_t)x0 | (uintptr_t)x1 | (uintptr_t)W) & 15 ||
+        A->fmt != KF_FMT_MXFP8 || M <= 0) {
+        kf_set_error("kf_gemm_fused_edge: an MXFP8 product with M > 0, an edge row and 16-byte aligned fp16 "
+                     "operands, cols %% 8 == 0 (cols=%d)", cols);
+        return -1;
+    }
+    WgradArgs g{};
+    g.eo = (h16 *)edge_out;
+    g.ex0 = (const h16 *)x0;
+    g.ex1 = (const h16 *)x1;
+    g.ew = (const h16 *)W;
+    g.ecols = cols;
+    return fused_impl(M, N, K, A, B, epi, &g);
+}
+static int fused_impl(int M, int N, int K, const KfOperand *A, const KfOperand *B, const KfEpilogue *epi,
+                      const WgradArgs *edge) {
     if (M <= 0 || N <= 0) return 0;
     OpD a, b;
     if (!to_dev(*A, a, "A") || !to_dev(*B, b, "B")) return -1;
@@ -1346,6 +1394,13 @@ extern "C" int kf_gemm_fused(int M, int N, int K, const KfOperand *A, const KfOp
         return -1;
     }
     WgradArgs G{nullptr, nullptr, 0, 0, g_kil};
+    if (edge) {
+        G.eo = edge->eo;
+        G.ex0 = edge->ex0;
+        G.ex1 = edge->ex1;
+        G.ew = edge->ew;
+        G.ecols = edge->ecols;
+    }
     const int am = op_mode(a), bm = op_mode(b);
     const bool f8 = A->fmt == KF_FMT_MXFP8;
     if (f8 != (B->fmt == KF_FMT_MXFP8)) {
@@ -1523,7 +1578,11 @@ static int wgrad_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     // workgroups per launch: every split writes an M x N fp32 slab that the reduce
     // reads back, so the target trades CU fill against slab traffic
     // (targets of 256 / 384 / 768 / 1024 measured slower)
-    int splits = (g_wgrad_target + tiles - 1) / tiles;
+    // at most the target (rounding the split count down): beside the input-gradient chain a
+    // launch with a few workgroups more than fit at once holds them pending until a whole
+    // workgroup's K range retires, and the chain's launches queue behind them (a 4-row
+    // edge sum took 128 us instead of 6.5; bench 36.90-37.02 -> 36.57-36.65 ms, r5)
+    int splits = std::max(1, g_wgrad_target / tiles);
     const int maxsplit = (K + 4 * BK - 1) / (4 * BK);  // at least 4 K-steps per split
     if (splits > maxsplit) splits = maxsplit;
     if (splits < 1) splits = 1;

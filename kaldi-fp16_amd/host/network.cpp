@@ -1785,11 +1785,12 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         A1.scales = d8.s;
                         A1.lds = d8.ld / 32;
                         KfOperand B8 = op_mxw(nl.w8d, bn);
-                        if (!ck(kf_gemm_fused(T, bn, 2 * pw, &A1, &B8, &E1), "tdnnf affine dgrad mxfp8")) return -1;
-                        if (!ck(kf_dot2_rows((char *)dbott + (size_t)(T - 1) * bn * 2,
-                                             (const char *)dz + (size_t)(T - 1) * dout * 2, edge,
-                                             wptr(net, nl.pW2), bn, dout),
-                                "tdnnf affine dgrad edge row"))
+                        // rows 0 .. T-2, and row T-1 by the last row tile's workgroups
+                        if (!ck(kf_gemm_fused_edge(T - 1, bn, 2 * pw, &A1, &B8, &E1,
+                                                   (char *)dbott + (size_t)(T - 1) * bn * 2,
+                                                   (const char *)dz + (size_t)(T - 1) * dout * 2, edge,
+                                                   wptr(net, nl.pW2), dout),
+                                "tdnnf affine dgrad mxfp8"))
                             return -1;
                     } else {
                         KfOperand A1 = masked(op_splice(dzs, T, dout, 0, -s, KF_ZERO, 1));

@@ -40,6 +40,8 @@ _vp, _i, _f, _ll, _sz = C.c_void_p, C.c_int, C.c_float, C.c_longlong, C.c_size_t
 
 
 def _sig(lib, name, res, *args):
+    if os.environ.get("KFP16_LIBDIR") and not hasattr(lib, name):
+        return None  # A/B against an older build that lacks this entry point
     fn = getattr(lib, name)
     fn.restype = res
     fn.argtypes = list(args)
@@ -456,6 +458,9 @@ _sig(core, "kf_gemm_fused", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOp
 _sig(core, "kf_gemm_wgrad", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i)
 _sig(core, "kf_rows_sum", _i, _vp, _vp, _ll, _i, _i, _i)
 _sig(core, "kf_rows_sum_mask", _i, _vp, _vp, _ll, _i, _i, _i, _vp)
+_sig(core, "kf_dot2_rows", _i, _vp, _vp, _vp, _vp, _i, _i)
+_sig(core, "kf_gemm_fused_edge", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), C.POINTER(KfEpilogue),
+     _vp, _vp, _vp, _vp, _i)
 _sig(core, "kf_scale_cols", _i, _vp, _ll, _vp, _vp, _ll, _i, _i)
 _sig(core, "kf_gemm_wgrad_scaled", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i,
      _vp)

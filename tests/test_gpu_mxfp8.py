@@ -199,3 +199,36 @@ def test_quantiser_batch_matches_single_calls(gpu):
         scales = np.frombuffer(kf.read_fp16(sc.ptr, (rows * cpad // 64,)).tobytes(), np.uint8).reshape(rows, cpad // 32)
         np.testing.assert_array_equal(codes, rc)
         np.testing.assert_array_equal(scales, rs)
+
+
+@pytest.mark.parametrize("M,N,K,cols", [(767, 320, 512, 1536), (384, 160, 256, 3072)])
+def test_mxfp8_gemm_with_edge_row(gpu, M, N, K, cols):
+    """kf_gemm_fused_edge: the MXFP8 product's rows 0 .. M-1 equal kf_gemm_fused's bit for bit,
+    and row M (written by the last row tile's workgroups) is the fp16 two-part dot product of
+    kf_dot2_rows (the TDNN-F affine input gradient's clamped-edge row, network.cpp)."""
+    kf = gpu
+    rng = np.random.default_rng(M + cols)
+    x = rng.standard_normal((M, K)) * 2
+    w = rng.standard_normal((N, K)) * 0.05
+    qa, sa, lda, a = mx_operand(kf, x)
+    qb, sb, ldb, b = mx_operand(kf, w)
+    A = kf.operand(qa.ptr, lda, M, K, 1, scales=sa.ptr, lds=lda // 32)
+    B = kf.operand(qb.ptr, ldb, N, K, 1, scales=sb.ptr, lds=ldb // 32)
+    x0, x1 = h(rng.standard_normal(cols)), h(rng.standard_normal(cols))
+    W = h(rng.standard_normal((2 * N, cols)) / np.sqrt(cols))
+    dx0, dx1, dW = kf.upload_fp16(x0), kf.upload_fp16(x1), kf.upload_fp16(W)
+    y1, y2 = kf.DeviceBuffer((M + 1) * N * 2), kf.DeviceBuffer((M + 1) * N * 2)
+    E1, E2 = kf.KfEpilogue(out=y1.ptr, ldo=N, alpha=1.0), kf.KfEpilogue(out=y2.ptr, ldo=N, alpha=1.0)
+    kf.check(kf.core.kf_gemm_fused(M, N, K, C.byref(A), C.byref(B), C.byref(E1)), "mxfp8 gemm")
+    kf.check(kf.core.kf_dot2_rows(y1.ptr + M * N * 2, dx0.ptr, dx1.ptr, dW.ptr, N, cols), "dot2")
+    kf.check(kf.core.kf_gemm_fused_edge(M, N, K, C.byref(A), C.byref(B), C.byref(E2), y2.ptr + M * N * 2,
+                                        dx0.ptr, dx1.ptr, dW.ptr, cols), "mxfp8 gemm + edge row")
+    kf.sync()
+    g1, g2 = kf.read_fp16(y1.ptr, (M + 1, N)), kf.read_fp16(y2.ptr, (M + 1, N))
+    assert np.array_equal(g1[:M].view(np.uint16), g2[:M].view(np.uint16))
+    W64 = W.astype(np.float64)
+    ref = W64[:N] @ x0.astype(np.float64) + W64[N:] @ x1.astype(np.float64)
+    mag = np.abs(W64[:N]) @ np.abs(x0.astype(np.float64)) + np.abs(W64[N:]) @ np.abs(x1.astype(np.float64))
+    tol = 2 * cols * 2.0 ** -23 * mag + np.abs(ref) * 2.0 ** -10 + 2.0 ** -24
+    for g in (g1[M], g2[M]):
+        assert np.all(np.abs(g.astype(np.float64) - ref) <= tol)
