@@ -730,6 +730,16 @@ def main():
             workload="cnn_tdnn_17f_3072 forward only, MXFP8 GEMMs",
             **describe(r, a, world, "forward", True, "", PEAK_FP8_TFLOPS))
         extra["dropin_per_op_abi_forward"] = dropin_forward(a)
+        # the same train step with the weight gradients on the chain's stream: its
+        # roofline prices the fused class without the weight gradients running beside it
+        import copy
+        a1 = copy.copy(a)
+        a1.no_wgrad_stream = True
+        r, _ = run_workload(a1, "cnn_tdnn_17f.xconfig", "train", False, rank, world, None, ks, kw, prof_on)
+        extra["train_1536_one_stream"] = dict(
+            workload="the headline train step with the weight gradients on the input-gradient chain's stream "
+                     "(nnet_set_wgrad_stream 0): per-launch times of the fused class without co-running work",
+            **describe(r, a1, world, "train", False, "cnn_tdnn_17f.xconfig", PEAK_FP16_TFLOPS))
 
     if rank == 0:
         # the box's CPU share (OMP_NUM_THREADS is set to it there; nproc shows the whole host)
