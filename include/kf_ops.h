@@ -91,6 +91,10 @@ typedef struct {
  *   if out2: out2[m][n] = rne_fp16(v * scale2[n] * bit(mask_in, m*ldo2+n))
  *   if out8: MXFP8 copy (kf_quant_mxfp8's rule, 32-column blocks) of the unrounded v, or
  *            with out8_src = 1 of the unrounded out2 value
+ *   if edge_out: edge_out[n] = rne_fp16(sum over rows m in [edge_r0, edge_r1) of the stored
+ *            out[m][n] (edge_src = 0) or out2[m][n] (edge_src = 1)), in row order: kf_rows_sum
+ *            of the result, written by the workgroups of the row tile holding those rows (a
+ *            separate sum kernel after the GEMM when the rows span two tiles)
  * Masks are bit-packed in the linear element order of the tensor they describe
  * (bit i of byte i/8), so producer and consumer may tile differently.
  */
@@ -114,6 +118,8 @@ typedef struct {
     long long ldo8;
     uint8_t *scale8;       /* E8M0 [M x ldo8/32] (required with out8) */
     int out8_src;          /* 0: out8 quantises v (out's value); 1: out2's value (needs out2) */
+    void *edge_out;        /* fp16 [N], or NULL: column sums of rows [edge_r0, edge_r1) (above) */
+    int edge_r0, edge_r1, edge_src;
 } KfEpilogue;
 
 /* current stream for every launch made by this library on the calling thread

@@ -347,6 +347,24 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     });
+    // edge row (KfEpilogue.edge_out): the row tile that holds rows [edge_r0, edge_r1) sums the
+    // values it just stored, per column in row order (kf_rows_sum's order and rounding), once
+    // every wave's stores are visible to the workgroup. The host falls back to kf_rows_sum when
+    // the rows span two tiles (launch<>).
+    if (E.edge_out && E.edge_r0 >= m0 && E.edge_r1 <= m0 + BM && E.edge_r1 <= M && E.edge_r0 < E.edge_r1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const h16 *src = (const h16 *)(E.edge_src ? E.out2 : E.out);
+        const long long ld = E.edge_src ? E.ldo2 : E.ldo;
+        for (int c = tid; c < BN; c += NTH) {
+            const int n = n0 + c;
+            if (n >= N) continue;
+            float s = 0.f;
+            for (int r = E.edge_r0; r < E.edge_r1; ++r) s += h2f(src[(long long)r * ld + n]);
+            ((h16 *)E.edge_out)[n] = f2h(s);
+        }
+    }
 }
 
 template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST, int AM, int BMODE,
@@ -1175,6 +1193,10 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
         kf_set_error("gemm launch (M=%d N=%d K=%d): %s", M, N, K, hipGetErrorString(e));
         return -1;
     }
+    if (!WGRAD && E.edge_out && E.edge_r0 < E.edge_r1 &&
+        (E.edge_r0 / BM != (E.edge_r1 - 1) / BM || E.edge_r1 > M || E.edge_r0 < 0))
+        return kf_rows_sum_mask(E.edge_out, E.edge_src ? E.out2 : E.out, E.edge_src ? E.ldo2 : E.ldo, E.edge_r0,
+                                E.edge_r1, N, nullptr);
     return 0;
 }
 
@@ -1226,6 +1248,7 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
         a.hmul < 1 || a.hmul > 2 || a.hout < 2 || a.ncols != K || a.nparts * a.pw != K)
         return 0;
     if (bkc ? bm != OP_GEN : bm != OP_SIMPLE) return 0;
+    if (E.edge_out) return 0;  // the edge-row sum is the tiled kernel's (launch<> has its fallback)
     // shifted weight rows (op_wrows): every tap's block lies inside the matrix
     bool brow = bkc && b.hout == 1 && b.hmul == 0 && !b.hshift && !b.edges && !b.tclamp &&
                 b.nparts == a.nparts && b.pw == a.pw;

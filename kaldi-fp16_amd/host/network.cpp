@@ -226,6 +226,7 @@ struct KfNet {
     // by the masked affine input gradient on the same chain), so off by default.
     int implicit_dz = 0;
     bool dz_imp[2] = {false, false};  // dz[i] was left implicit by the producing epilogue
+    bool dz_edge[2] = {false, false}; // row T of dz[i] already holds the strided TDNN-F edge sum
     void *w2s = nullptr;              // [kaff x dout] fp16: W2 with the BN scale folded in
     void *dbott_last = nullptr;  // the dbott buffer of the last TDNN-F / prefinal step (tests)
     size_t edge_half = 0;
@@ -1446,7 +1447,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
     E.ldo2 = w;
     E.out2 = dz_out;
     const int di = dz_out == net->dz[0] ? 0 : dz_out == net->dz[1] ? 1 : -1;
-    if (di >= 0) net->dz_imp[di] = false;
+    if (di >= 0) net->dz_imp[di] = net->dz_edge[di] = false;
     switch (L.type) {
         case LayerType::TDNNF: {
             E.scale2 = pl.bn_scale;
@@ -1464,6 +1465,16 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
                     net->dz_imp[di] = true;
                     return true;
                 }
+            }
+            // a strided P's clamped-splice edge row (row T of dz: sum of its rows T-1-s .. T-1),
+            // summed by the epilogue's last row tile instead of a separate kf_rows_sum launch
+            if (L.time_stride > 0 && di >= 0 && net->T > 0) {
+                const int T = net->T;
+                E.edge_out = (char *)dz_out + (size_t)T * w * 2;
+                E.edge_r0 = T - 1 - L.time_stride < 0 ? 0 : T - 1 - L.time_stride;
+                E.edge_r1 = T;
+                E.edge_src = 1;
+                net->dz_edge[di] = true;
             }
             // MXFP8 train step: also the e4m3 copy of dz_P for P's affine input gradient; only
             // when the copy's row is exactly w wide (w % 128 == 0), so the dgrad GEMM's K range
@@ -1739,15 +1750,19 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 KfOperand A = s > 0 ? op_splice(nl.aux, T, bn, 0, s, KF_CLAMP, 0)
                                     : op_base(nl.aux, bn, T, bn, 0);
                 KfOperand B = masked(op_base(dzs, dout, T, dout, 0));
-                if (!wgrad([&] {
-                        if (imp)
-                            return ck(kf_gemm_wgrad_scaled(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout,
-                                                           gptr(net, nl.pb2), 0, nl.bn_scale),
-                                      "tdnnf affine wgrad");
-                        return ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
+                auto aff_wgrad = [&] {
+                    if (imp)
+                        return ck(kf_gemm_wgrad_scaled(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout,
+                                                       gptr(net, nl.pb2), 0, nl.bn_scale),
                                   "tdnnf affine wgrad");
-                    }))
-                    return -1;
+                    return ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
+                              "tdnnf affine wgrad");
+                };
+                // A/B knob KF_BWD_MAIN_AFF: 1 = odd layers', 2 = every layer's affine weight
+                // gradient on the chain (after its input gradient) instead of the side stream
+                static const int main_aff = getenv("KF_BWD_MAIN_AFF") ? atoi(getenv("KF_BWD_MAIN_AFF")) : 0;
+                const bool aff_on_main = two && (main_aff == 2 || (main_aff == 1 && (done & 1)));
+                if (!aff_on_main && !wgrad(aff_wgrad)) return -1;
                 const void *w2 = wptr(net, nl.pW2);
                 if (imp) {
                     if (!ck(kf_scale_cols(w2, dout, nl.bn_scale, net->w2s, dout, kaff, dout), "tdnnf scaled W2")) return -1;
@@ -1759,14 +1774,23 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 KfEpilogue E1 = epi0();
                 E1.out = dbott;
                 E1.ldo = bn;
+                if (s > 0 && want_dx) {
+                    // the linear input gradient's edge row (row T of dbott: sum of rows 0 .. s),
+                    // summed by this GEMM's first row tile
+                    E1.edge_out = (char *)dbott + (size_t)T * bn * 2;
+                    E1.edge_r0 = 0;
+                    E1.edge_r1 = s + 1 < T ? s + 1 : T;
+                    E1.edge_src = 0;
+                }
                 const int i8 = dz == net->dz[0] ? 0 : dz == net->dz[1] ? 1 : -1;
                 if (s > 0) {
                     // spare row T of dz (of g when dz is implicit: the masked sum) holds
                     // sum_{t >= T-1-s} dz[t] (clamped-splice transpose)
                     void *edge = (char *)dzs + (size_t)T * dout * 2;
-                    if (!ck(kf_rows_sum_mask(edge, dzs, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout,
-                                             imp ? nl.mask : nullptr),
-                            "edge"))
+                    const bool have_edge = !imp && ib >= 0 && net->dz_edge[ib];  // dx_epilogue's
+                    if (!have_edge && !ck(kf_rows_sum_mask(edge, dzs, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout,
+                                                           imp ? nl.mask : nullptr),
+                                          "edge"))
                         return -1;
                     KfOperand B1 = op_wrows(w2, 2, bn, dout);
                     if (net->fp8 && i8 >= 0 && net->dz8_layer[i8] == li && T > 1) {
@@ -1804,6 +1828,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     KfOperand B1 = op_base(w2, dout, bn, dout, 1);
                     if (!ck(kf_gemm_fused(T, bn, dout, &A1, &B1, &E1), "tdnnf affine dgrad")) return -1;
                 }
+                if (aff_on_main && !aff_wgrad()) return -1;
                 // linear weight gradient: splice-(x)^T . dbott
                 KfOperand A2 = s > 0 ? op_splice(x, T, din, -s, 0, KF_CLAMP, 0)
                                      : op_base(x, din, T, din, 0);
@@ -1818,9 +1843,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     // input gradient: transpose of the [-s, 0] clamped splice
                     if (s > 0) {
                         // spare row T of dbott holds sum_{t <= s} dbott[t]
-                        void *edge = (char *)dbott + (size_t)T * bn * 2;
-                        if (!ck(kf_rows_sum(edge, dbott, bn, 0, s + 1 < T ? s + 1 : T, bn), "edge"))
-                            return -1;
+                        // (row T of dbott: the affine input gradient's epilogue summed it, E1)
                         KfOperand A3 = op_splice(dbott, T, bn, s, 0, KF_ZERO, 1);
                         A3.edge_t[0] = 0;
                         A3.edge_row[0] = T;

@@ -425,7 +425,8 @@ class KfEpilogue(C.Structure):
     _fields_ = [("out", _vp), ("ldo", _ll), ("alpha", _f), ("beta", _f), ("bias", _vp), ("relu", _i),
                 ("mask_out", _vp), ("scale", _vp), ("shift", _vp), ("resid", _vp), ("ldr", _ll),
                 ("resid_alpha", _f), ("out2", _vp), ("ldo2", _ll), ("scale2", _vp), ("mask_in", _vp),
-                ("out8", _vp), ("ldo8", _ll), ("scale8", _vp), ("out8_src", _i)]
+                ("out8", _vp), ("ldo8", _ll), ("scale8", _vp), ("out8_src", _i), ("edge_out", _vp),
+                ("edge_r0", _i), ("edge_r1", _i), ("edge_src", _i)]
 
 
 def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, hout=1, hsrc=1,
