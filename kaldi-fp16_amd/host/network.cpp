@@ -1758,9 +1758,13 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     return ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
                               "tdnnf affine wgrad");
                 };
-                // A/B knob KF_BWD_MAIN_AFF: 1 = odd layers', 2 = every layer's affine weight
-                // gradient on the chain (after its input gradient) instead of the side stream
-                static const int main_aff = getenv("KF_BWD_MAIN_AFF") ? atoi(getenv("KF_BWD_MAIN_AFF")) : 0;
+                // Every other TDNN-F layer's affine weight gradient runs on the chain, after its
+                // input gradient: with the edge sums in the epilogues the chain waits for the
+                // weight-gradient stream before each linear input gradient (dx_wait), and this
+                // balances the two (one box: 36.66 / 36.89 -> 36.55 / 36.65 ms; all of them on
+                // the chain 36.95 / 37.01). KF_BWD_MAIN_AFF: 0 = all on the weight-gradient
+                // stream, 2 = all on the chain (A/B).
+                static const int main_aff = getenv("KF_BWD_MAIN_AFF") ? atoi(getenv("KF_BWD_MAIN_AFF")) : 1;
                 const bool aff_on_main = two && (main_aff == 2 || (main_aff == 1 && (done & 1)));
                 if (!aff_on_main && !wgrad(aff_wgrad)) return -1;
                 const void *w2 = wptr(net, nl.pW2);
