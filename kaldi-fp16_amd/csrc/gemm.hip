@@ -1542,16 +1542,6 @@ void kf_wgrad_reduce(const float *slab, const float *bias_slab, int splits, int 
 int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
                            float *bias_grad, int accumulate);
 
-// A/B experiment bits (KF_EXPT in the environment, read once; 0 = the measured default)
-int kf_expt() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = getenv("KF_EXPT");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
 // workgroups per weight-gradient launch (split-K target): 512 alone on the device; nnet's
 // backward sets 256 while its weight gradients run on their own stream beside the
 // input-gradient chain (half the CUs each, half the fp32 slab bytes)

@@ -50,8 +50,6 @@ void kf_prof_stop(int idx);
 
 // persistent per-device scratch (never freed; grows monotonically)
 void *kf_workspace(size_t bytes, int slot);
-// A/B experiment bits: KF_EXPT in the environment, read once (gemm.hip); 0 = the defaults
-int kf_expt();
 
 static inline int kf_blocks(long long n, int threads, int cap = 1 << 20) {
     long long b = (n + threads - 1) / threads;

@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of KF_EXPT experiment bits under rocprofv3 (one build): scripts/r05_abenv.sh <tag> v1 v2 ...
+# A/B of KF_EXPT experiment bits under rocprofv3 (one build; the r5 experiment builds read KF_EXPT,
+# the committed code has no bits left): scripts/r05_abenv.sh <tag> v1 v2 ...
 # (a value listed twice shows the spread; BENCH_ARGS adds bench flags)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp
 tag=$1; shift
