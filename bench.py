@@ -98,6 +98,9 @@ def parse(argv=None):
                    help="MXFP8 forward GEMMs (configs[4]; use with --xconfig cnn_tdnn_17f_3072.xconfig)")
     p.add_argument("--mode", choices=("train", "forward"), default="train",
                    help="train: the metric's fwd+bwd+SGD step; forward: configs[1], forward only")
+    p.add_argument("--strict", action="store_true",
+                   help="exit 3 when a sub-result or the CPU baseline failed (default: the failure is recorded "
+                        "in sub_result_errors and the line, with the headline, is printed with exit status 0)")
     p.add_argument("--selftest", action="store_true",
                    help="CPU (gloo) check of the launcher and the bucketed gradient exchange")
     return p.parse_args(argv)
@@ -667,6 +670,81 @@ def describe(r, a, world, mode, fp8, xconfig, peak):
     return d
 
 
+def sub_results(a, rank, world, prof_on):
+    """The N = 1 sub-results measured after the headline (configs[1], configs[4], the drop-in
+    per-op path, the one-stream step), in this order. Each runs on its own: one that raises
+    is recorded as {"error": ...} (with the library's pending-error log) and the rest still
+    run, so a failing sub-result never discards the headline line. Returns (results, errors)."""
+    import copy
+    import traceback
+    import kfp16
+    ks, kw = a.extra_steps, 2
+    extra, errors = {}, {}
+
+    def guarded(name, fn):
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 -- recorded, reported, and the run continues
+            torch.cuda.synchronize()
+            errors[name] = {"error": f"{type(e).__name__}: {e}", "pending_log": kfp16.pending_log(),
+                            "where": traceback.format_exc(limit=4)}
+            extra[name] = {"error": errors[name]["error"]}
+            print(f"bench.py: sub-result {name} failed: {e}", file=sys.stderr, flush=True)
+
+    def fwd_1536():
+        r, _ = run_workload(a, "cnn_tdnn_17f.xconfig", "forward", False, rank, world, None, ks, kw, prof_on)
+        extra["configs[1]_forward_1536"] = dict(
+            workload="cnn_tdnn_17f forward only, fp16", **describe(r, a, world, "forward", False, "", PEAK_FP16_TFLOPS))
+    guarded("configs[1]_forward_1536", fwd_1536)
+
+    # the 3072 train step in fp16 and in MXFP8, A/B/A/B in this process: each sub-result
+    # is its second run; the speedup compares the means of both runs of each mode
+    def train_3072():
+        ms_ab = {False: [], True: []}
+        for rep in range(2):
+            for f8 in (False, True):
+                r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "train", f8, rank, world, None, ks, kw, prof_on)
+                d = describe(r, a, world, "train", f8, "", PEAK_FP8_TFLOPS if f8 else PEAK_FP16_TFLOPS)
+                ms_ab[f8].append(d["ms_per_step"])
+                if rep == 1 and not f8:
+                    extra["configs[4]_train_3072_fp16"] = dict(
+                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), fp16 (the MXFP8 step's reference point)",
+                        **d)
+                elif rep == 1:
+                    extra["configs[4]_train_3072_mxfp8"] = dict(
+                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD): MXFP8 forward GEMMs and strided "
+                                 "TDNN-F affine input gradients, the rest fp16", **d)
+        m8 = extra["configs[4]_train_3072_mxfp8"]
+        m8["ms_per_step_ab"] = {"fp16": ms_ab[False], "mxfp8": ms_ab[True]}
+        m16, m8ms = sum(ms_ab[False]) / 2, sum(ms_ab[True]) / 2
+        m8["speedup_vs_fp16_step"] = round(m16 / m8ms, 4) if m8ms else None
+    guarded("configs[4]_train_3072", train_3072)
+
+    def fwd_3072_fp8():
+        r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "forward", True, rank, world, None, ks, kw, prof_on)
+        extra["configs[4]_forward_3072_mxfp8"] = dict(
+            workload="cnn_tdnn_17f_3072 forward only, MXFP8 GEMMs",
+            **describe(r, a, world, "forward", True, "", PEAK_FP8_TFLOPS))
+    guarded("configs[4]_forward_3072_mxfp8", fwd_3072_fp8)
+
+    def dropin():
+        extra["dropin_per_op_abi_forward"] = dropin_forward(a)
+    guarded("dropin_per_op_abi_forward", dropin)
+
+    # the same train step with the weight gradients on the chain's stream (DESIGN §8a): its
+    # roofline prices the fused class without the weight gradients running beside it
+    def one_stream():
+        a1 = copy.copy(a)
+        a1.no_wgrad_stream = True
+        r, _ = run_workload(a1, "cnn_tdnn_17f.xconfig", "train", False, rank, world, None, ks, kw, prof_on)
+        extra["train_1536_one_stream"] = dict(
+            workload="the headline train step with the weight gradients on the input-gradient chain's stream "
+                     "(nnet_set_wgrad_stream 0): per-launch times of the fused class without co-running work",
+            **describe(r, a1, world, "train", False, "cnn_tdnn_17f.xconfig", PEAK_FP16_TFLOPS))
+    guarded("train_1536_one_stream", one_stream)
+    return extra, errors
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -699,54 +777,20 @@ def main():
     box = box_hbm_probe()
     head, ctx = run_workload(a, a.xconfig, a.mode, a.fp8, rank, world, comm, a.steps, a.warmup, prof_on,
                              keep=True)
-    extra = {}
+    extra, errors = {}, {}
     if world == 1 and not a.no_extra and a.xconfig == "cnn_tdnn_17f.xconfig" and a.mode == "train" and not a.fp8:
-        ks, kw = a.extra_steps, 2
-        r, _ = run_workload(a, "cnn_tdnn_17f.xconfig", "forward", False, rank, world, None, ks, kw, prof_on)
-        extra["configs[1]_forward_1536"] = dict(
-            workload="cnn_tdnn_17f forward only, fp16", **describe(r, a, world, "forward", False, "", PEAK_FP16_TFLOPS))
-        # the 3072 train step in fp16 and in MXFP8, A/B/A/B in this process: each sub-result
-        # is its second run; the speedup compares the means of both runs of each mode
-        ms_ab = {False: [], True: []}
-        for rep in range(2):
-            for f8 in (False, True):
-                r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "train", f8, rank, world, None, ks, kw, prof_on)
-                d = describe(r, a, world, "train", f8, "", PEAK_FP8_TFLOPS if f8 else PEAK_FP16_TFLOPS)
-                ms_ab[f8].append(d["ms_per_step"])
-                if rep == 1 and not f8:
-                    extra["configs[4]_train_3072_fp16"] = dict(
-                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), fp16 (the MXFP8 step's reference point)",
-                        **d)
-                elif rep == 1:
-                    extra["configs[4]_train_3072_mxfp8"] = dict(
-                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD): MXFP8 forward GEMMs and strided "
-                                 "TDNN-F affine input gradients, the rest fp16", **d)
-        m8 = extra["configs[4]_train_3072_mxfp8"]
-        m8["ms_per_step_ab"] = {"fp16": ms_ab[False], "mxfp8": ms_ab[True]}
-        m16, m8ms = sum(ms_ab[False]) / 2, sum(ms_ab[True]) / 2
-        m8["speedup_vs_fp16_step"] = round(m16 / m8ms, 4) if m8ms else None
-        r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "forward", True, rank, world, None, ks, kw, prof_on)
-        extra["configs[4]_forward_3072_mxfp8"] = dict(
-            workload="cnn_tdnn_17f_3072 forward only, MXFP8 GEMMs",
-            **describe(r, a, world, "forward", True, "", PEAK_FP8_TFLOPS))
-        extra["dropin_per_op_abi_forward"] = dropin_forward(a)
-        # the same train step with the weight gradients on the chain's stream: its
-        # roofline prices the fused class without the weight gradients running beside it
-        import copy
-        a1 = copy.copy(a)
-        a1.no_wgrad_stream = True
-        r, _ = run_workload(a1, "cnn_tdnn_17f.xconfig", "train", False, rank, world, None, ks, kw, prof_on)
-        extra["train_1536_one_stream"] = dict(
-            workload="the headline train step with the weight gradients on the input-gradient chain's stream "
-                     "(nnet_set_wgrad_stream 0): per-launch times of the fused class without co-running work",
-            **describe(r, a1, world, "train", False, "cnn_tdnn_17f.xconfig", PEAK_FP16_TFLOPS))
+        extra, errors = sub_results(a, rank, world, prof_on)
 
     if rank == 0:
         # the box's CPU share (OMP_NUM_THREADS is set to it there; nproc shows the whole host)
         threads = a.cpu_threads or min(host_cores(), int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or
                                        host_cores())
         if world == 1 and not a.no_extra and not a.no_cpu_baseline:
-            extra["configs[0]_affine_40x512"] = config1_affine(threads)
+            try:
+                extra["configs[0]_affine_40x512"] = config1_affine(threads)
+            except Exception as e:  # noqa: BLE001 -- recorded; the headline still prints
+                errors["configs[0]_affine_40x512"] = {"error": f"{type(e).__name__}: {e}"}
+                extra["configs[0]_affine_40x512"] = errors["configs[0]_affine_40x512"]
         fwd_only = a.mode == "forward"
         workload = ("cnn_tdnn_17f forward only (configs[1])" if fwd_only else
                     "cnn_tdnn_17f train step (fwd+bwd+SGD)") + f", {a.egs} egs x 1500 frames per GPU"
@@ -812,16 +856,32 @@ def main():
             from kfp16 import synth
             xcfg, params, bns, den_g, P = ctx
             den = (den_g, oracle.den_initial_probs(den_g))
-            out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, threads,
-                                               den, synth.make_num_fst(0, num_pdfs=P), a.gt_frames)
+            try:
+                out["cpu_baseline"] = cpu_baseline(xcfg, params, bns, a.cpu_frames, threads,
+                                                   den, synth.make_num_fst(0, num_pdfs=P), a.gt_frames)
+            except Exception as e:  # noqa: BLE001 -- recorded; the headline still prints
+                errors["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
+        one = extra.get("train_1536_one_stream", {}).get("roofline")
+        if one is not None:
+            # the dominant class priced without the weight gradients co-running
+            out["roofline_one_stream"] = {k: one[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel",
+                                                              "launches", "kernel_ms_per_step", "mfma_frac",
+                                                              "hbm_frac", "flops_per_launch",
+                                                              "alg_bytes_per_launch")}
         if extra:
             out["sub_results"] = extra
+        out["sub_result_errors"] = errors or None
+        pend = kfp16.pending_log()
+        if pend:   # HIP errors other calls left pending, consumed by the library's entry checks
+            out["hip_pending_log"] = pend
         print(json.dumps(out), flush=True)
     if comm is not None:
         torch.cuda.synchronize()
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+    if errors and a.strict:
+        return 3
     return 0
 
 

@@ -134,6 +134,14 @@ int nnet_set_wgrad_stream(KfNet *net, int on);
  * off: 0 = store dz (the default). */
 int nnet_set_implicit_dz(KfNet *net, int on);
 
+/* diagnostics (tests) of the two-stream backward: main_aff chooses where the TDNN-F
+ * affine weight gradients run (-1 = KF_BWD_MAIN_AFF / the default 1: every other one on
+ * the input-gradient chain; 0 = all on the weight-gradient stream; 2 = all on the chain);
+ * stall_cycles > 0 queues a spin kernel of that many GPU clock cycles (kf_debug_spin) on
+ * the weight-gradient stream before each of its batches of work, so that stream runs far
+ * behind the chain and any missing order shows as a wrong gradient. */
+int nnet_debug_backward(KfNet *net, int main_aff, long long stall_cycles);
+
 /* diagnostics (tests): back-propagate through the top n layers only; device
  * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott" (the buffer of the last
  * TDNN-F / prefinal step), "aux", "mask",

@@ -317,6 +317,23 @@ void kf_gemm_trace(unsigned long long *buf, int at, int blk);
 const char *kf_last_error(void);
 void kf_clear_error(void);
 
+/* Error hygiene across the C-ABI. HIP keeps one pending error per host
+ * thread, read and reset by hipGetLastError(). Every entry point of this library that
+ * checks its own launches with hipGetLastError() first calls kf_take_pending(its name):
+ * an error some earlier HIP call left pending (another library, the caller's own HIP
+ * calls, or a runtime call whose status nobody read) is consumed there and logged as
+ * "pending before <where>: <error>" instead of being reported as that entry's failure.
+ * kf_take_pending returns the consumed hipError_t (0 = none). kf_pending_log returns
+ * the log since the last kf_pending_clear (NULL if empty; at most the last 16 notes,
+ * plus the total count); kf_peek_error returns the pending error without consuming
+ * it. With KF_ERR_VERBOSE=1 in the environment every note is also printed to stderr. */
+int kf_take_pending(const char *where);
+const char *kf_pending_log(void);
+void kf_pending_clear(void);
+int kf_peek_error(void);
+/* diagnostics (tests): one workgroup spinning for `cycles` GPU clock cycles on `stream` */
+int kf_debug_spin(void *stream, long long cycles);
+
 #ifdef __cplusplus
 }
 #endif

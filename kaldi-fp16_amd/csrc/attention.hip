@@ -257,6 +257,7 @@ AttD att_dev(const KfAttention &a) {
 
 extern "C" int kf_attention_forward(const KfAttention *a, void *out, long long ldo, uint8_t *mask,
                                     const float *scale, const float *shift) {
+    kf_take_pending(__func__);
     if (!a || !att_check(*a, "kf_attention_forward")) return -1;
     const int width = a->num_heads * (a->value_dim + a->context);
     if (!out || !scale || !shift || ldo < width || (mask && (width % 8))) {
@@ -271,6 +272,7 @@ extern "C" int kf_attention_forward(const KfAttention *a, void *out, long long l
 
 extern "C" int kf_attention_backward(const KfAttention *a, const void *dz, long long ldz, void *dproj,
                                      float *scratch) {
+    kf_take_pending(__func__);
     if (!a || !att_check(*a, "kf_attention_backward")) return -1;
     const int width = a->num_heads * (a->value_dim + a->context);
     if (!dz || !dproj || !scratch || ldz < width) {

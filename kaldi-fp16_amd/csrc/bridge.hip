@@ -4,6 +4,8 @@
 // hands data back to the host synchronises, as the reference's blocking
 // cudaMemcpy calls do.
 #include "kf_common.h"
+#include <stdlib.h>
+#include <string>
 #include "../../include/bridge.h"
 #include "../../include/kf_ops.h"
 
@@ -43,6 +45,73 @@ extern "C" int kf_stream_wait(void *s, void *e) {
 }
 extern "C" void *kf_get_stream(void) { return (void *)g_stream; }
 
+// ---------------------------------------------------------------------------
+// error hygiene (include/kf_ops.h: kf_take_pending). HIP's pending error is per host
+// thread, and so is this log.
+// ---------------------------------------------------------------------------
+namespace {
+struct PendingLog {
+    enum { kKeep = 16 };
+    char note[kKeep][192];
+    int total = 0;
+    std::string text;
+};
+__thread PendingLog *g_pending = nullptr;
+PendingLog &pending_log() {
+    if (!g_pending) g_pending = new PendingLog();  // per thread, lives as long as the thread
+    return *g_pending;
+}
+bool pending_verbose() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("KF_ERR_VERBOSE");
+        v = e && *e && *e != '0';
+    }
+    return v;
+}
+}  // namespace
+
+extern "C" int kf_take_pending(const char *where) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    PendingLog &L = pending_log();
+    char *n = L.note[L.total % PendingLog::kKeep];
+    snprintf(n, sizeof(L.note[0]), "pending before %s: %s (%s)", where ? where : "?", hipGetErrorName(e),
+             hipGetErrorString(e));
+    ++L.total;
+    if (pending_verbose()) fprintf(stderr, "kfp16: HIP error %s\n", n);
+    return (int)e;
+}
+extern "C" const char *kf_pending_log(void) {
+    PendingLog &L = pending_log();
+    if (!L.total) return nullptr;
+    L.text = std::to_string(L.total) + " pending error(s)";
+    const int first = L.total > PendingLog::kKeep ? L.total - PendingLog::kKeep : 0;
+    for (int i = first; i < L.total; ++i) {
+        L.text += "; ";
+        L.text += L.note[i % PendingLog::kKeep];
+    }
+    return L.text.c_str();
+}
+extern "C" void kf_pending_clear(void) { pending_log().total = 0; }
+extern "C" int kf_peek_error(void) { return (int)hipPeekAtLastError(); }
+
+__global__ void k_spin(long long cycles, int *sink) {
+    const long long t0 = clock64();
+    long long n = 0;
+    while (clock64() - t0 < cycles) {
+        __builtin_amdgcn_s_sleep(8);
+        ++n;
+    }
+    if (n < 0) *sink = 1;  // never: keeps the loop
+}
+extern "C" int kf_debug_spin(void *stream, long long cycles) {
+    kf_take_pending(__func__);
+    if (cycles <= 0) return 0;
+    k_spin<<<1, 64, 0, (hipStream_t)stream>>>(cycles, nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 namespace {
 struct Slot {
     void *ptr = nullptr;
@@ -72,6 +141,62 @@ void *kf_workspace(size_t bytes, int slot) {
     }
     s.bytes = want;
     return s.ptr;
+}
+
+// Per-stream scratch for the weight gradients' split-K fp32 slabs (kf_common.h). One
+// backward runs weight gradients on two streams at once (the input-gradient chain's and
+// the weight-gradient stream), and a slab lives from its GEMM to its reduce,
+// so each stream gets a buffer of its own: two streams never share one. Up to kStreams
+// streams per device keep a buffer; another stream takes the least recently used one
+// after a device-wide sync (only when streams are new, e.g. a new network's).
+namespace {
+constexpr int kStreams = 4;
+struct StreamSlot {
+    hipStream_t s = nullptr;
+    bool used = false;
+    unsigned long long last = 0;
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+StreamSlot g_sws[kMaxDev][kStreams];
+unsigned long long g_sws_tick = 0;
+}  // namespace
+
+void *kf_workspace_stream(size_t bytes) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (dev < 0 || dev >= kMaxDev) return nullptr;
+    const hipStream_t st = g_stream;
+    StreamSlot *row = g_sws[dev], *s = nullptr;
+    for (int i = 0; i < kStreams && !s; ++i)
+        if (row[i].used && row[i].s == st) s = &row[i];
+    if (!s) {
+        for (int i = 0; i < kStreams && !s; ++i)
+            if (!row[i].used) s = &row[i];
+        if (!s) {  // evict the least recently used stream's buffer: its work may be queued
+            s = &row[0];
+            for (int i = 1; i < kStreams; ++i)
+                if (row[i].last < s->last) s = &row[i];
+            hipDeviceSynchronize();
+        }
+        s->s = st;
+        s->used = true;
+    }
+    s->last = ++g_sws_tick;
+    if (s->bytes >= bytes && s->ptr) return s->ptr;
+    if (s->ptr) {  // growing: this stream's queued work may still read the old buffer
+        hipStreamSynchronize(st);
+        hipFree(s->ptr);
+        s->ptr = nullptr;
+        s->bytes = 0;
+    }
+    const size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+    if (hipMalloc(&s->ptr, want) != hipSuccess) {
+        s->ptr = nullptr;
+        return nullptr;
+    }
+    s->bytes = want;
+    return s->ptr;
 }
 
 __global__ void k_f16_to_f32(float *dst, const h16 *src, size_t n) {
@@ -227,6 +352,7 @@ void bridge_gpu_memset(void *ptr, int value, size_t bytes) {
 }
 
 int bridge_fp16_to_fp32_gpu(float *dst_device, const void *src_device, size_t count) {
+    kf_take_pending(__func__);
     if (count == 0) return 0;
     k_f16_to_f32<<<kf_blocks(count, 256, 8192), 256, 0, g_stream>>>(dst_device,
                                                                     (const h16 *)src_device, count);
@@ -239,6 +365,7 @@ int bridge_fp16_to_fp32_gpu(float *dst_device, const void *src_device, size_t co
 }
 
 int bridge_fp32_to_fp16_gpu(void *dst_device, const float *src_device, size_t count) {
+    kf_take_pending(__func__);
     if (count == 0) return 0;
     k_f32_to_f16<<<kf_blocks(count, 256, 8192), 256, 0, g_stream>>>((h16 *)dst_device,
                                                                     src_device, count);

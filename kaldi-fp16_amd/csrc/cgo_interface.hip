@@ -144,6 +144,7 @@ KfOperand plain(const void *p, long long ld, int rows, int cols, int kcontig) {
 }
 
 void launch_act(TensorHandle h, int op, float a, const char *what) {
+    kf_take_pending(__func__);
     Tensor *t = as_tensor(h);
     if (!t || !t->size) return;
     k_act<<<blocks(t->size), 256, 0, kf_stream()>>>(t->data, (long long)t->size, op, a);
@@ -187,6 +188,7 @@ TensorHandle kaldi_tensor_zeros(int rows, int cols) {
 }
 
 TensorHandle kaldi_tensor_ones(int rows, int cols) {
+    kf_take_pending(__func__);
     Tensor *t = as_tensor(kaldi_tensor_create(rows, cols));
     if (t && t->size) {
         k_fill<<<blocks(t->size), 256, 0, kf_stream()>>>(t->data, (long long)t->size, 1.f);
@@ -211,6 +213,7 @@ size_t kaldi_tensor_size(TensorHandle h) { return h ? as_tensor(h)->size : 0; }
 void *kaldi_tensor_data(TensorHandle h) { return h ? (void *)as_tensor(h)->data : nullptr; }
 
 void kaldi_tensor_copy_from_host_fp32(TensorHandle h, const float *data, size_t count) {
+    kf_take_pending(__func__);
     Tensor *t = as_tensor(h);
     if (!t || !data) return;
     if (count > t->size) count = t->size;
@@ -226,6 +229,7 @@ void kaldi_tensor_copy_from_host_fp32(TensorHandle h, const float *data, size_t 
 }
 
 void kaldi_tensor_copy_to_host_fp32(TensorHandle h, float *data, size_t count) {
+    kf_take_pending(__func__);
     Tensor *t = as_tensor(h);
     if (!t || !data) return;
     if (count > t->size) count = t->size;
@@ -240,6 +244,7 @@ void kaldi_tensor_copy_to_host_fp32(TensorHandle h, float *data, size_t count) {
 
 void kaldi_gemm(CuBLASHandlePtr handle, TensorHandle hA, TensorHandle hB, TensorHandle hC,
                 float alpha, float beta, int transA, int transB) {
+    kf_take_pending(__func__);
     Tensor *A = as_tensor(hA), *B = as_tensor(hB), *Cm = as_tensor(hC);
     if (!handle || !A || !B || !Cm) {
         kaldi_set_error("null pointer in GEMM");
@@ -293,6 +298,7 @@ void kaldi_tanh(TensorHandle t) { launch_act(t, A_TANH, 0.f, "tanh"); }
 void kaldi_scale(TensorHandle t, float alpha) { launch_act(t, A_SCALE, alpha, "scale"); }
 
 void kaldi_softmax(TensorHandle h) {
+    kf_take_pending(__func__);
     Tensor *t = as_tensor(h);
     if (!t || !t->rows || !t->cols) return;
     k_softmax_rows<<<t->rows, 256, 0, kf_stream()>>>(t->data, t->cols);
@@ -300,6 +306,7 @@ void kaldi_softmax(TensorHandle h) {
 }
 
 void kaldi_add(TensorHandle ha, TensorHandle hb) {
+    kf_take_pending(__func__);
     Tensor *a = as_tensor(ha), *b = as_tensor(hb);
     if (!a || !b) return;
     if (b->size < a->size) {  // the reference reads past b here (cgo_interface.cu:357-365)

@@ -2075,6 +2075,7 @@ struct DevBuf {
 // Runs k_logfb over `fsts` (already filled) and returns the totals.
 bool run_logfb(std::vector<LogFstDev> &fsts, const void *nnet16, long long ld, int P,
                std::vector<float> &totals, const char **why) {
+    kf_take_pending(__func__);
     DevBuf d, tot;
     size_t n = fsts.size();
     if (!tot.alloc(n * sizeof(float)) || !d.alloc(n * sizeof(LogFstDev))) {
@@ -2347,6 +2348,7 @@ __global__ void k_l2(const float *x, float *g, float s, long long n, double *acc
 
 extern "C" int chain_combine_gradient(const float *num_post, const float *den_post, float weight,
                                       int T, int num_pdfs, void *grad_output) {
+    kf_take_pending(__func__);
     long long n = (long long)T * num_pdfs;
     if (n <= 0) return 0;
     hipLaunchKernelGGL(k_combine16, dim3(kf_blocks(n, 256)), dim3(256), 0, kf_stream(), num_post,
@@ -2359,6 +2361,7 @@ extern "C" int chain_combine_gradient(const float *num_post, const float *den_po
 }
 extern "C" int chain_add_posterior_gradient(const float *num_post, const float *den_post,
                                             float *grad, float weight, int total_elements) {
+    kf_take_pending(__func__);
     if (total_elements <= 0) return 0;
     hipLaunchKernelGGL(k_add_post, dim3(kf_blocks(total_elements, 256)), dim3(256), 0, kf_stream(),
                        num_post, den_post, grad, weight, (long long)total_elements);
@@ -2465,6 +2468,7 @@ extern "C" void den_fst_free(DenFstGPU *fst) {
 
 static float den_abi(const DenFstGPU *fst, const float *h_nnet, const float *h_init, int T,
                      float leaky, float *h_post) {
+    kf_take_pending(__func__);
     DenTables *t = nullptr;
     {
         std::lock_guard<std::mutex> lk(g_den_mu);
@@ -2689,7 +2693,11 @@ extern "C" int kf_den_graph_initial_probs(const KfDenGraph *g, float *out) {
     memcpy(out, g->init.data(), g->init.size() * 4);
     return 0;
 }
-extern "C" void kf_den_graph_free(KfDenGraph *g) { delete g; }
+extern "C" void kf_den_graph_free(KfDenGraph *g) {
+    kf_take_pending(__func__);
+    delete g;
+    kf_take_pending("the return of kf_den_graph_free");
+}
 
 // host CSR arrays (kf_chain.h layout) -> prepared numerator FSTs
 static bool num_hosts(const char *fn, int nseq, const int32_t *state_off, const int32_t *arc_off,
@@ -2815,7 +2823,11 @@ extern "C" int kf_num_batch_refill(KfNumBatch *b, int nseq, const int32_t *state
     ++b->gen;
     return 0;
 }
-extern "C" void kf_num_batch_free(KfNumBatch *b) { delete b; }
+extern "C" void kf_num_batch_free(KfNumBatch *b) {
+    kf_take_pending(__func__);
+    delete b;
+    kf_take_pending("the return of kf_num_batch_free");
+}
 
 extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max_frames) {
     if (!den || max_seqs <= 0 || max_frames <= 0) {
@@ -2858,12 +2870,17 @@ extern "C" KfChain *kf_chain_create(const KfDenGraph *den, int max_seqs, int max
     hipMemset(c->stats, 0, (size_t)max_seqs * 32);
     return c;
 }
-extern "C" void kf_chain_free(KfChain *c) { delete c; }
+extern "C" void kf_chain_free(KfChain *c) {
+    kf_take_pending(__func__);
+    delete c;
+    kf_take_pending("the return of kf_chain_free");
+}
 
 extern "C" int kf_chain_compute(KfChain *c, const KfNumBatch *num, const KfChainOpts *opts,
                                 const void *nnet_output, long long ld, long long num_rows, int nseq,
                                 const int32_t *seq_row0, const int32_t *seq_frames, int stride,
                                 void *out_grad, long long ldg) {
+    kf_take_pending(__func__);
     if (!c || !num || !opts || !nnet_output || !out_grad || !seq_row0 || !seq_frames) {
         kfc_set_error("kf_chain_compute: NULL argument");
         return -1;

@@ -269,6 +269,7 @@ extern "C" {
 void launch_conv1d_forward_fp16(const void *input, const void *weight, const void *bias,
                                 void *output, int B, int Ti, int Ci, int Co, int K, int stride,
                                 int pad, int dil, void *stream) {
+    kf_take_pending(__func__);
     if (!positive("conv1d_forward", {B, Ti, Ci, Co, K, stride, dil})) return;
     const int To = conv1d_output_size(Ti, K, stride, pad, dil);
     if (To <= 0) return;
@@ -283,6 +284,7 @@ void launch_conv1d_backward_fp16(const void *input, const void *grad_output, con
                                  void *grad_input, void *grad_weight, void *grad_bias, int B,
                                  int Ti, int Ci, int Co, int K, int stride, int pad, int dil,
                                  void *stream) {
+    kf_take_pending(__func__);
     if (!positive("conv1d_backward", {B, Ti, Ci, Co, K, stride, dil})) return;
     const int To = conv1d_output_size(Ti, K, stride, pad, dil);
     if (To <= 0) return;
@@ -305,6 +307,7 @@ void launch_conv1d_backward_fp16(const void *input, const void *grad_output, con
 
 void launch_maxpool1d_forward_fp16(const void *input, void *output, void *indices, int B, int Ti,
                                    int C, int K, int stride, void *stream) {
+    kf_take_pending(__func__);
     if (!positive("maxpool1d_forward", {B, Ti, C, K, stride})) return;
     const int To = pool1d_output_size(Ti, K, stride);
     if (To <= 0) return;
@@ -316,6 +319,7 @@ void launch_maxpool1d_forward_fp16(const void *input, void *output, void *indice
 
 void launch_maxpool1d_backward_fp16(const void *grad_output, const void *indices, void *grad_input,
                                     int B, int Ti, int To, int C, void *stream) {
+    kf_take_pending(__func__);
     if (!positive("maxpool1d_backward", {B, Ti, To, C})) return;
     k_maxpool_bwd<<<kf_blocks((long long)B * C, 256, 65536), 256, 0, pick(stream)>>>(
         (const h16 *)grad_output, (const int32_t *)indices, (h16 *)grad_input, B, Ti, To, C);
@@ -324,6 +328,7 @@ void launch_maxpool1d_backward_fp16(const void *grad_output, const void *indices
 
 void launch_stats_pooling_fp16(const void *input, void *output, int B, int T, int C,
                                void *stream) {
+    kf_take_pending(__func__);
     if (!positive("stats_pooling", {B, T, C})) return;
     k_stats_pool<<<kf_blocks((long long)B * C, 256, 65536), 256, 0, pick(stream)>>>(
         (const h16 *)input, (h16 *)output, B, T, C);
@@ -334,6 +339,7 @@ void launch_batchnorm1d_forward_fp16(const void *input, const void *gamma, const
                                      void *running_mean, void *running_var, void *output,
                                      void *save_mean, void *save_invstd, int B, int T, int C,
                                      float momentum, float eps, bool training, void *stream) {
+    kf_take_pending(__func__);
     if (!positive("batchnorm1d_forward", {B, T, C})) return;
     k_bn1d<<<C, 256, 0, pick(stream)>>>((const h16 *)input, (const h16 *)gamma, (const h16 *)beta,
                                         (h16 *)running_mean, (h16 *)running_var, (h16 *)output,
@@ -344,6 +350,7 @@ void launch_batchnorm1d_forward_fp16(const void *input, const void *gamma, const
 
 void launch_layernorm_forward_fp16(const void *input, const void *gamma, const void *beta,
                                    void *output, int B, int T, int C, float eps, void *stream) {
+    kf_take_pending(__func__);
     if (!positive("layernorm_forward", {B, T, C})) return;
     k_layernorm<<<B * T, 256, 0, pick(stream)>>>((const h16 *)input, (const h16 *)gamma,
                                                  (const h16 *)beta, (h16 *)output, C, eps);
@@ -353,6 +360,7 @@ void launch_layernorm_forward_fp16(const void *input, const void *gamma, const v
 void launch_depthwise_conv1d_fp16(const void *input, const void *weight, const void *bias,
                                   void *output, int B, int Ti, int C, int K, int stride, int pad,
                                   void *stream) {
+    kf_take_pending(__func__);
     if (!positive("depthwise_conv1d", {B, Ti, C, K, stride})) return;
     const int To = (Ti + 2 * pad - K) / stride + 1;
     if (To <= 0) return;
@@ -365,6 +373,7 @@ void launch_depthwise_conv1d_fp16(const void *input, const void *weight, const v
 
 void launch_pointwise_conv1d_fp16(const void *input, const void *weight, const void *bias,
                                   void *output, int B, int T, int Ci, int Co, void *stream) {
+    kf_take_pending(__func__);
     if (!positive("pointwise_conv1d", {B, T, Ci, Co})) return;
     const long long rows = (long long)B * T;
     k_pointwise<<<kf_blocks(rows * Co, 256, 65536), 256, 0, pick(stream)>>>(

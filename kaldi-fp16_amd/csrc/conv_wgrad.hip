@@ -261,6 +261,7 @@ void kf_prof_stop(int idx);
 // kernel covers (the caller runs the im2col GEMM), -1 on error.
 int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, float *dW, long long ldw,
                            float *bias_grad, int accumulate) {
+    kf_take_pending(__func__);
     if (a.nparts != WTAPS || a.pw % 64 || a.simple || a.edges || a.tclamp || a.hshift ||
         a.hmul < 1 || a.hmul > 2 || a.hout < 2 || a.ncols != WTAPS * a.pw || M != a.ncols ||
         a.nrows != K || !b.simple || b.nrows != K || b.ncols != N || N % 64)
@@ -330,7 +331,7 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     H.N = N;
     const size_t slab_bytes = (size_t)H.splits * M * N * 4;
     const size_t bias_bytes = bias_grad ? (size_t)H.splits * N * 4 : 0;
-    char *ws = (char *)kf_workspace(slab_bytes + bias_bytes + 256, 0);
+    char *ws = (char *)kf_workspace_stream(slab_bytes + bias_bytes + 256);
     if (!ws) {
         kf_report_error("conv wgrad: workspace allocation of %zu bytes failed", slab_bytes + bias_bytes);
         return -1;

@@ -23,6 +23,8 @@
 
 #include "../../include/kf_dp.h"
 
+extern "C" int kf_take_pending(const char *where);  // bridge.hip (kf_ops.h)
+
 hipStream_t kf_stream();
 // ops.hip: buf[i] = (buf[i] + peer[i]) * 0.5f on `s` (the KF_DP_DEBUG_PEER_MEAN exchange)
 int kf_dp_debug_mean_launch(float *buf, const float *peer, size_t n, hipStream_t s);
@@ -157,6 +159,7 @@ extern "C" int kf_dp_rank(const KfDp *dp) { return dp ? dp->rank : -1; }
 extern "C" int kf_dp_world(const KfDp *dp) { return dp ? dp->world : -1; }
 
 extern "C" int kf_dp_allreduce_mean_async(KfDp *dp, float *buf, size_t count) {
+    kf_take_pending(__func__);
     if (!dp || (!buf && count)) {
         set_err("kf_dp_allreduce_mean_async: null");
         return -1;

@@ -114,6 +114,7 @@ __global__ void __launch_bounds__(256) k_cm_expand(const KfCmDesc *__restrict__ 
 
 extern "C" int kf_cm_expand(const KfCmDesc *dev_desc, int nmat, int max_rows, int max_cols,
                             const void *dev_blob, void *dev_out, int ldo) {
+    kf_take_pending(__func__);
     if (nmat <= 0) return 0;
     if (!dev_desc || !dev_blob || !dev_out || max_rows <= 0 || max_cols <= 0 ||
         max_cols > kMaxCols || ldo < max_cols) {

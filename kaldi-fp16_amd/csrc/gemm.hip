@@ -1163,6 +1163,7 @@ template <int BM, int BN, int WM, int WN, bool AKC, bool BKC, bool WGRAD, int ST
           int F8 = 0>
 static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilogue &E,
                   const WgradArgs &G0, int splits) {
+    kf_take_pending(__func__);
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     dim3 grid(mt * nt, WGRAD ? splits : 1);
     WgradArgs G = G0;
@@ -1216,6 +1217,7 @@ extern "C" void kf_halo_trace(unsigned long long *buf, int at) {
 }
 template <int BM, int BN, int WM, int WN, bool BKC, int BMODE, bool BROW, int ST>
 static int launch_halo(int M, int N, const OpD &B, const KfEpilogue &E, const HaloArgs &H0, size_t lds) {
+    kf_take_pending(__func__);
     const int mt = (M + BM - 1) / BM, nt = (N + BN - 1) / BN;
     HaloArgs H = H0;
     H.trace = g_halo_trace && g_halo_launches++ == g_halo_trace_at ? g_halo_trace : nullptr;
@@ -1554,6 +1556,7 @@ extern "C" int kf_gemm_wgrad_target(int wgs) {
 
 static int wgrad_impl(int M, int N, int K, const KfOperand *A, const KfOperand *B, float *dW, long long ldw,
                       float *bias_grad, int accumulate, const float *cs) {
+    kf_take_pending(__func__);
     if (M <= 0 || N <= 0) return 0;
     OpD a, b;
     if (!to_dev(*A, a, "A") || !to_dev(*B, b, "B")) return -1;
@@ -1604,7 +1607,7 @@ static int wgrad_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     splits = (K + kps - 1) / kps;
     size_t slab_bytes = (size_t)splits * M * N * 4;
     size_t bias_bytes = bias_grad ? (size_t)splits * N * 4 : 0;
-    char *ws = (char *)kf_workspace(slab_bytes + bias_bytes + 256, 0);
+    char *ws = (char *)kf_workspace_stream(slab_bytes + bias_bytes + 256);
     if (!ws) {
         kf_set_error("kf_gemm_wgrad: workspace allocation of %zu bytes failed",
                      slab_bytes + bias_bytes);
@@ -1686,6 +1689,7 @@ extern "C" int kf_gemm_wgrad_scaled(int M, int N, int K, const KfOperand *A, con
 
 extern "C" int kf_rows_sum_mask(void *edge, const void *src, long long ld, int r0, int r1, int cols,
                                 const uint8_t *mask) {
+    kf_take_pending(__func__);
     if (cols <= 0) return 0;
     k_rows_sum<<<(cols + 255) / 256, 256, 0, kf_stream()>>>((h16 *)edge, (const h16 *)src, ld,
                                                             r0, r1, cols, mask);
@@ -1723,6 +1727,7 @@ __global__ __launch_bounds__(256) void k_dot2_rows(h16 *out, const h16 *x0, cons
 }
 
 extern "C" int kf_dot2_rows(void *out, const void *x0, const void *x1, const void *W, int rows, int cols) {
+    kf_take_pending(__func__);
     if (rows <= 0) return 0;
     if (cols % 8 || ((uintptr_t)x0 | (uintptr_t)x1 | (uintptr_t)W) & 15) {
         kf_set_error("kf_dot2_rows: cols %% 8 and 16-byte aligned operands required (cols=%d)", cols);
@@ -2069,6 +2074,7 @@ static bool quant_args_ok(const void *src, int rows, int cols, const void *q, lo
 }
 
 extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
+    kf_take_pending(__func__);
     if (n < 0 || n > KF_QUANT_MAX || (n && !jobs)) {
         kf_set_error("kf_quant_mxfp8_batch: %d jobs (at most %d)", n, KF_QUANT_MAX);
         return -1;
@@ -2121,6 +2127,7 @@ extern "C" int kf_quant_mxfp8_batch(int n, const KfQuantJob *jobs) {
 
 extern "C" int kf_quant_mxfp8(const void *src, long long ld_src, int rows, int cols, int transpose,
                               void *q, long long ldq, uint8_t *scales, long long lds) {
+    kf_take_pending(__func__);
     if (rows <= 0 || cols <= 0) return 0;
     const int cols_pad = (cols + 127) / 128 * 128;
     if (!src || !q || !scales || ldq < cols_pad || ldq % 16 || lds < cols_pad / 32 ||
@@ -2146,6 +2153,7 @@ extern "C" int kf_quant_mxfp8(const void *src, long long ld_src, int rows, int c
 
 int kf_ops_gemm_impl(int M, int N, int K, float alpha, const void *A, int lda, const void *B,
                      int ldb, float beta, void *C, int ldc, char *err, size_t errlen) {
+    kf_take_pending(__func__);
     if (M < 0 || N < 0 || K < 0) {
         snprintf(err, errlen, "ops_gemm: negative dims (M=%d N=%d K=%d)", M, N, K);
         return -1;

@@ -38,6 +38,10 @@ struct KfErr {
 // current stream (kf_ops.h: kf_set_stream)
 hipStream_t kf_stream();
 
+// consume and log an error an earlier HIP call left pending (kf_ops.h): called at the
+// top of every entry that checks its own launches with hipGetLastError()
+extern "C" int kf_take_pending(const char *where);
+
 // sets the kf_last_error() text from another module (gemm.hip owns the slot)
 void kf_report_error(const char *fmt, ...);
 
@@ -50,6 +54,9 @@ void kf_prof_stop(int idx);
 
 // persistent per-device scratch (never freed; grows monotonically)
 void *kf_workspace(size_t bytes, int slot);
+// scratch of the current stream (kf_stream()), never shared with another stream: the
+// weight gradients' split-K slabs, which two streams fill at once (bridge.hip)
+void *kf_workspace_stream(size_t bytes);
 
 static inline int kf_blocks(long long n, int threads, int cap = 1 << 20) {
     long long b = (n + threads - 1) / threads;

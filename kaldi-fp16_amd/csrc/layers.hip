@@ -267,6 +267,7 @@ __global__ void k_bn_apply(const h16 *x, h16 *y, long long rows, int D, const fl
 extern "C" {
 
 int kf_small_gemm(const void *x, int ldx, const void *Mw, void *y, int ldy, int T, int K, int N) {
+    kf_take_pending(__func__);
     if (K > 64 || N > 64 || N % 8) {
         lay_set_error("small_gemm: K=%d N=%d unsupported", K, N);
         return -1;
@@ -279,6 +280,7 @@ int kf_small_gemm(const void *x, int ldx, const void *Mw, void *y, int ldy, int 
 
 int kf_bn_apply(const void *x, void *y, long long rows, int D, const float *scale,
                 const float *shift) {
+    kf_take_pending(__func__);
     if (rows <= 0) return 0;
     k_bn_apply<<<kf_blocks(rows * D, 256, 8192), 256, 0, kf_stream()>>>(
         (const h16 *)x, (h16 *)y, rows, D, scale, shift);
@@ -288,6 +290,7 @@ int kf_bn_apply(const void *x, void *y, long long rows, int D, const float *scal
 int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
                        const int *dh, const void *x, const void *W, const void *bias,
                        const float *scale, const float *shift, void *y, uint8_t *mask) {
+    kf_take_pending(__func__);
     if (noff > 9 || fout % 8 || fout > 256 || 256 % (fout / 8) ||
         (long long)T * hout * fout >= (1LL << 31)) {
         lay_set_error("conv_c1_forward: noff=%d fout=%d T*hout=%lld unsupported", noff, fout,
@@ -321,6 +324,7 @@ int kf_conv_c1_forward(int T, int hin, int hout, int sub, int fout, int noff, co
 
 int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, const int *dt,
                      const int *dh, const void *x, const void *dz, float *dW, float *db) {
+    kf_take_pending(__func__);
     if (noff > 9 || fout % 8 || fout > 256 || 256 % (fout / 8) ||
         (long long)T * hout * fout >= (1LL << 31)) {
         lay_set_error("conv_c1_wgrad: noff=%d fout=%d T*hout=%lld unsupported", noff, fout,
@@ -366,6 +370,7 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
 
 int kf_sgd_flat(float *w32, void *w16, const float *g, float *v, float lr, float mom,
                 long long n) {
+    kf_take_pending(__func__);
     if (n <= 0) return 0;
     k_sgd_flat<<<kf_blocks(n / 4 + 1, 256, 8192), 256, 0, kf_stream()>>>(w32, (h16 *)w16, g, v, lr,
                                                                         mom, n);
@@ -373,6 +378,7 @@ int kf_sgd_flat(float *w32, void *w16, const float *g, float *v, float lr, float
 }
 
 int kf_f32_to_f16_flat(const float *src, void *dst, long long n) {
+    kf_take_pending(__func__);
     if (n <= 0) return 0;
     k_f32_to_f16_flat<<<kf_blocks(n, 256, 8192), 256, 0, kf_stream()>>>(src, (h16 *)dst, n);
     return lay_check("f32_to_f16_flat");

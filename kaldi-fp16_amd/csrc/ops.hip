@@ -60,6 +60,7 @@ __global__ void k_act(h16 *d, long long n, int kind, float ceil_, int vec) {
 }
 
 static int run_act(void *data, int count, int kind, float c, const char *name) {
+    kf_take_pending(__func__);
     if (count < 0) {
         ops_set_error("%s: negative count", name);
         return -1;
@@ -391,6 +392,7 @@ __global__ void k_dp_peer_mean(float *buf, const float *peer, long long n) {
     GRID_STRIDE(i, n) buf[i] = (buf[i] + peer[i]) * 0.5f;
 }
 int kf_dp_debug_mean_launch(float *buf, const float *peer, size_t n, hipStream_t s) {
+    kf_take_pending(__func__);
     if (!n) return 0;
     const long long blocks = ((long long)n + 255) / 256;
     hipLaunchKernelGGL(k_dp_peer_mean, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, buf, peer,
@@ -475,6 +477,7 @@ int ops_clipped_relu(void *data, int count, float ceiling) {
 }
 
 int ops_softmax(void *data, int rows, int cols) {
+    kf_take_pending(__func__);
     if (rows <= 0 || cols <= 0) return 0;
     k_softmax<<<rows, 256, 0, kf_stream()>>>((h16 *)data, cols, 0);
     return ops_check("softmax kernel");
@@ -524,6 +527,7 @@ __global__ __launch_bounds__(256) void k_log_softmax_rows(h16 *data, int rows, i
 }
 
 int ops_log_softmax(void *data, int rows, int cols) {
+    kf_take_pending(__func__);
     if (rows <= 0 || cols <= 0) return 0;
     if (cols % 8 == 0 && cols <= 64 * 8 * kLsmMaxChunks && aligned16(data)) {
         k_log_softmax_rows<<<(rows + 3) / 4, 256, 0, kf_stream()>>>((h16 *)data, rows, cols);
@@ -535,6 +539,7 @@ int ops_log_softmax(void *data, int rows, int cols) {
 
 static int run_bn(void *x, int T, int D, const float *mean, const float *var, const float *gamma,
                   const float *beta, float target_rms, float eps, int rms, const char *name) {
+    kf_take_pending(__func__);
     const long long total = (long long)T * D;
     if (D % 8 == 0 && aligned16(x)) {
         int blocks;
@@ -561,6 +566,7 @@ int ops_batchnorm_forward_rms(void *x, int T, int D, const float *mean, const fl
 }
 
 int ops_add_scaled(void *dst, const void *src, int count, float alpha, float beta) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     k_add_scaled<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
         (h16 *)dst, (const h16 *)src, count, alpha, beta, aligned16(dst) && aligned16(src));
@@ -570,6 +576,7 @@ int ops_add(void *dst, const void *src, int count) {
     return ops_add_scaled(dst, src, count, 1.f, 1.f);
 }
 int ops_copy(void *dst, const void *src, int count) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     if (count % 8 == 0 && aligned16(dst) && aligned16(src)) {
         const long long n8 = count / 8;
@@ -584,6 +591,7 @@ int ops_copy(void *dst, const void *src, int count) {
     return 0;
 }
 int ops_fill(void *dst, int count, float val) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     k_fill<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>((h16 *)dst, count, val, aligned16(dst));
     return ops_check("fill");
@@ -591,6 +599,7 @@ int ops_fill(void *dst, int count, float val) {
 
 int ops_concat_cols(void *dst, int T, int dst_cols, const void *src, int src_cols,
                     int dst_col_offset) {
+    kf_take_pending(__func__);
     if ((long long)T * src_cols <= 0) return 0;
     if (dst_col_offset < 0 || dst_col_offset + src_cols > dst_cols) {
         ops_set_error("concat_cols: offset %d + %d > %d", dst_col_offset, src_cols, dst_cols);
@@ -609,6 +618,7 @@ int ops_concat_cols(void *dst, int T, int dst_cols, const void *src, int src_col
 }
 int ops_slice_cols(const void *src, int T, int src_cols, void *dst, int dst_cols,
                    int src_col_offset) {
+    kf_take_pending(__func__);
     if ((long long)T * dst_cols <= 0) return 0;
     if (src_col_offset < 0 || src_col_offset + dst_cols > src_cols) {
         ops_set_error("slice_cols: offset %d + %d > %d", src_col_offset, dst_cols, src_cols);
@@ -627,6 +637,7 @@ int ops_slice_cols(const void *src, int T, int src_cols, void *dst, int dst_cols
 }
 
 int ops_combine_feature_maps(void *data, int T, int total_dim, int height, int nf1, int nf2) {
+    kf_take_pending(__func__);
     const long long total = (long long)T * total_dim;
     if (total <= 0) return 0;
     if ((long long)height * (nf1 + nf2) != total_dim) {
@@ -655,18 +666,21 @@ void ops_subsample_rows(void *dst, const void *src, int in_rows, int cols, int s
 }
 
 int ops_relu_backward(const void *x, void *grad, int count) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     k_act_bwd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
         (const h16 *)x, (h16 *)grad, count, ACT_RELU, aligned16(x) && aligned16(grad));
     return ops_check("relu_backward");
 }
 int ops_sigmoid_backward(const void *out, void *grad, int count) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     k_act_bwd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
         (const h16 *)out, (h16 *)grad, count, ACT_SIGMOID, aligned16(out) && aligned16(grad));
     return ops_check("sigmoid_backward");
 }
 int ops_tanh_backward(const void *out, void *grad, int count) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     k_act_bwd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(
         (const h16 *)out, (h16 *)grad, count, ACT_TANH, aligned16(out) && aligned16(grad));
@@ -700,6 +714,7 @@ __global__ void k_transpose_batch(TransposeJobs J) {
     }
 }
 extern "C" int kf_transpose_batch(int n, const void *const *src, void *const *dst, const int *M, const int *N) {
+    kf_take_pending(__func__);
     if (n < 0 || n > KF_TRANSPOSE_MAX) {
         kf_report_error("kf_transpose_batch: %d jobs (at most %d)", n, KF_TRANSPOSE_MAX);
         return -1;
@@ -727,6 +742,7 @@ extern "C" int kf_transpose_batch(int n, const void *const *src, void *const *ds
 }
 
 int ops_transpose(const void *src, void *dst, int M, int N) {
+    kf_take_pending(__func__);
     if (M <= 0 || N <= 0) return 0;
     dim3 grid((N + 63) / 64, (M + 63) / 64);
     k_transpose<<<grid, dim3(64, 4), 0, kf_stream()>>>((const h16 *)src, (h16 *)dst, M, N);
@@ -734,6 +750,7 @@ int ops_transpose(const void *src, void *dst, int M, int N) {
 }
 int ops_batchnorm_backward(const void *grad_out, void *grad_in, const float *gamma,
                            const float *variance, float eps, int rows, int cols) {
+    kf_take_pending(__func__);
     const long long total = (long long)rows * cols;
     if (total <= 0) return 0;
     if (cols % 8 == 0 && aligned16(grad_out) && aligned16(grad_in)) {
@@ -748,6 +765,7 @@ int ops_batchnorm_backward(const void *grad_out, void *grad_in, const float *gam
     return ops_check("batchnorm_backward");
 }
 int ops_fp16_to_fp32(const void *src, float *dst, int count) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     k_h2f<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>((const h16 *)src, dst, count,
                                                                        aligned16(src) && aligned16(dst));
@@ -755,6 +773,7 @@ int ops_fp16_to_fp32(const void *src, float *dst, int count) {
 }
 int ops_sgd_update(float *w_fp32, void *w_fp16, const void *grad_fp16, float *velocity,
                    float lr, float momentum, int count) {
+    kf_take_pending(__func__);
     if (count <= 0) return 0;
     const int vec = aligned16(w_fp32) && aligned16(w_fp16) && aligned16(grad_fp16) && aligned16(velocity);
     k_sgd<<<kf_blocks(count / 8 + 1, 256, 8192), 256, 0, kf_stream()>>>(

@@ -225,6 +225,8 @@ struct KfNet {
     // step-neutral on the MI355X (the linear input gradient's saving is spent
     // by the masked affine input gradient on the same chain), so off by default.
     int implicit_dz = 0;
+    int main_aff = -1;             // nnet_debug_backward (tests): -1 = KF_BWD_MAIN_AFF / 1
+    long long stall_side = 0;      // nnet_debug_backward (tests): spin before side work
     bool dz_imp[2] = {false, false};  // dz[i] was left implicit by the producing epilogue
     bool dz_edge[2] = {false, false}; // row T of dz[i] already holds the strided TDNN-F edge sum
     void *w2s = nullptr;              // [kaff x dout] fp16: W2 with the BN scale folded in
@@ -800,7 +802,11 @@ extern "C" KfNet *nnet_create_layout(const char *xconfig_text, int max_frames) {
     return net.release();
 }
 
-extern "C" void nnet_free(KfNet *net) { delete net; }
+extern "C" void nnet_free(KfNet *net) {
+    kf_take_pending(__func__);
+    delete net;
+    kf_take_pending("the return of nnet_free");  // a stream / event / free call that failed
+}
 
 extern "C" int nnet_num_layers(const KfNet *net) { return (int)net->layers.size(); }
 
@@ -1090,6 +1096,7 @@ static bool quantise_weights(KfNet *net, bool alloc) {
 }
 
 extern "C" int nnet_set_fp8(KfNet *net, int on) {
+    kf_take_pending(__func__);
     if (!on_device(net, "set_fp8")) return -1;
     if (!on) {
         net->fp8 = 0;
@@ -1133,6 +1140,7 @@ extern "C" int nnet_set_fp8(KfNet *net, int on) {
 // ---------------------------------------------------------------------------
 static int forward_impl(KfNet *net, const void *features, int T);
 extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
+    kf_take_pending(__func__);
     if (net->ivec_dim) {
         set_err("forward: the network has an ivector input; use nnet_forward_ivector");
         return -1;
@@ -1143,6 +1151,7 @@ extern "C" int nnet_forward(KfNet *net, const void *features, int T) {
 // seq_row0 host int[B+1] frame offsets (seq_row0[0] = 0, seq_row0[B] = T)
 extern "C" int nnet_forward_ivector(KfNet *net, const void *features, int T, const void *ivectors, int B,
                                     const int *seq_row0) {
+    kf_take_pending(__func__);
     if (!on_device(net, "forward_ivector")) return -1;
     // validate everything before touching the device or the network's state
     if (T <= 0 || T > net->max_T) {
@@ -1524,6 +1533,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
 static int backward_impl(KfNet *net, const void *out_grad, int max_layers);
 static bool dp_issue(KfNet *net, size_t &next, int step);
 extern "C" int nnet_backward(KfNet *net, const void *out_grad) {
+    kf_take_pending(__func__);
     return backward_impl(net, out_grad, 1 << 30);
 }
 // debugging / tests: back-propagate through the top `n` layers only
@@ -1611,6 +1621,10 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
             return false;
         }
         kf_set_stream(net->wg_stream);
+        if (net->stall_side > 0 && kf_debug_spin(net->wg_stream, net->stall_side) != 0) {
+            set_err("backward: debug stall");
+            return false;
+        }
         return true;
     };
     auto to_main = [&]() { kf_set_stream(mainst); };
@@ -1628,6 +1642,12 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     const void *dz = out_grad;  // gradient w.r.t. pre-activation of the current layer
     const void *gcur = out_grad;  // stored gradient w.r.t. the current layer's output
     int flip = 0, done = 0;
+    // dbott alternates by TDNN-F / prefinal step (the steps that write it), not by layer:
+    // step k's affine input gradient writes its buffer before this step's dx_wait, which is
+    // safe because the previous dbott step (k - 1, other buffer) waited for the side work of
+    // step k - 2 (this buffer's readers). A pass-through step in between (Batchnorm) must not
+    // advance the parity, or k would reuse k - 1's buffer while its weight gradient reads it.
+    int nbott = 0;
     size_t dp_next = 0;
     if (!to_side()) return -1;
     for (const auto &r : net->offpath) bridge_gpu_memset(net->grad + r.first, 0, (size_t)r.second * 4);
@@ -1642,7 +1662,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         const void *x = act_of(net, nl.input);
         bool want_dx = nl.needs_dx && nl.input >= 0;
         void *dz_next = net->dz[flip], *g_next = net->g[flip];
-        void *const dbott_buf = (done & 1) && two ? net->dbott2 : net->dbott;
+        void *const dbott_buf = (nbott & 1) && two ? net->dbott2 : net->dbott;
         net->dz8_layer[flip] = -1;
         KfEpilogue E;
         if (want_dx && !dx_epilogue(net, nl.input, dz_next, g_next, E)) return -1;
@@ -1709,6 +1729,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     return -1;
                 void *dzbig = dbott_buf;
                 net->dbott_last = dzbig;
+                ++nbott;
                 KfEpilogue E1 = epi0();
                 E1.out2 = dzbig;
                 E1.ldo2 = big;
@@ -1764,7 +1785,8 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 // balances the two (one box: 36.66 / 36.89 -> 36.55 / 36.65 ms; all of them on
                 // the chain 36.95 / 37.01). KF_BWD_MAIN_AFF: 0 = all on the weight-gradient
                 // stream, 2 = all on the chain (A/B).
-                static const int main_aff = getenv("KF_BWD_MAIN_AFF") ? atoi(getenv("KF_BWD_MAIN_AFF")) : 1;
+                static const int env_main_aff = getenv("KF_BWD_MAIN_AFF") ? atoi(getenv("KF_BWD_MAIN_AFF")) : 1;
+                const int main_aff = net->main_aff >= 0 ? net->main_aff : env_main_aff;
                 const bool aff_on_main = two && (main_aff == 2 || (main_aff == 1 && (done & 1)));
                 if (!aff_on_main && !wgrad(aff_wgrad)) return -1;
                 const void *w2 = wptr(net, nl.pW2);
@@ -1775,6 +1797,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 // bottleneck gradient: transpose of the [0, +s] clamped splice
                 void *dbott = dbott_buf;
                 net->dbott_last = dbott;
+                ++nbott;
                 KfEpilogue E1 = epi0();
                 E1.out = dbott;
                 E1.ldo = bn;
@@ -2079,6 +2102,13 @@ extern "C" int nnet_set_implicit_dz(KfNet *net, int on) {
     return 0;
 }
 
+extern "C" int nnet_debug_backward(KfNet *net, int main_aff, long long stall_cycles) {
+    if (!net || main_aff < -1 || main_aff > 2 || stall_cycles < 0) return -1;
+    net->main_aff = main_aff;
+    net->stall_side = stall_cycles;
+    return 0;
+}
+
 extern "C" int nnet_set_wgrad_stream(KfNet *net, int on) {
     if (!net) return -1;
     if (!on && net->wg_stream) bridge_gpu_sync();
@@ -2100,6 +2130,7 @@ extern "C" int nnet_weights_changed(KfNet *net) {
 }
 
 extern "C" int nnet_sgd(KfNet *net, float lr, float momentum) {
+    kf_take_pending(__func__);
     if (!on_device(net, "sgd")) return -1;
     if (!ck(kf_sgd_flat(net->master, net->w16, net->grad, net->vel, lr, momentum, net->nparams), "sgd"))
         return -1;

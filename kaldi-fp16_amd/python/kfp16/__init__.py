@@ -30,7 +30,50 @@ def _load(name):
         raise ImportError(
             f"kfp16: {path} is missing — build the HIP libraries first "
             "(python -c 'import __graft_entry__ as g; g.build()'); there is no CPU fallback")
+    if os.environ.get("KF_ERR_TRACE", "0") not in ("", "0"):
+        return _TracedCDLL(path, mode=C.RTLD_GLOBAL)
     return C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
+# KF_ERR_TRACE=1: origin of a HIP error left pending. Every call through the
+# libraries peeks at HIP's pending error (kf_peek_error, not consumed) before and after it:
+# one pending before the call was raised by HIP calls the process made outside kfp16 since
+# its previous call (torch, ctypes users); one pending after it by the call itself. Notes
+# go to stderr and to trace_notes; the libraries' own kf_take_pending checks are unchanged.
+trace_notes: list = []
+
+
+def _trace_note(msg):
+    import sys
+    import traceback
+    where = "".join(traceback.format_stack(limit=5)[:-2]).rstrip()
+    trace_notes.append(msg + "\n" + where)
+    print(f"kfp16 KF_ERR_TRACE: {msg}\n{where}", file=sys.stderr, flush=True)
+
+
+class _TracedCDLL(C.CDLL):
+    def __init__(self, path, mode):
+        super().__init__(path, mode=mode)
+        peek = C.CDLL(os.path.join(LIBDIR, "libkaldi_fp16.so"), mode=mode).kf_peek_error
+        peek.restype, peek.argtypes = C.c_int, []
+        base = self._FuncPtr
+
+        class _Traced(base):
+            _flags_ = base._flags_
+            _restype_ = base._restype_
+
+            def __call__(self, *args):
+                pre = peek()
+                if pre:
+                    _trace_note(f"HIP error {pre} pending before {self.__name__} "
+                                "(raised outside kfp16 since its previous call)")
+                r = base.__call__(self, *args)
+                post = peek()
+                if post and post != pre:
+                    _trace_note(f"HIP error {post} pending after {self.__name__}")
+                return r
+
+        self._FuncPtr = _Traced
 
 
 core = _load("libkaldi_fp16.so")
@@ -52,6 +95,10 @@ def _sig(lib, name, res, *args):
 for _n in ("bridge_last_error", "ops_last_error", "kf_last_error", "nnet_last_error"):
     _sig(core if not _n.startswith("nnet") else nnet, _n, C.c_char_p)
 _sig(core, "bridge_clear_error", None)
+_sig(core, "kf_take_pending", _i, C.c_char_p)
+_sig(core, "kf_pending_log", C.c_char_p)
+_sig(core, "kf_pending_clear", None)
+_sig(core, "kf_peek_error", _i)
 _sig(core, "bridge_gpu_init", _i, _i)
 _sig(core, "bridge_gpu_sync", _i)
 _sig(core, "bridge_gpu_get_free_memory", _i, C.POINTER(_sz), C.POINTER(_sz))
@@ -102,6 +149,8 @@ _sig(nnet, "nnet_dp_plan", _i, _vp, _ll, _i, C.POINTER(_i), C.POINTER(_ll), C.PO
 _sig(nnet, "nnet_dp_debug_early", _i, _vp, _i)
 _sig(nnet, "nnet_set_wgrad_stream", _i, _vp, _i)
 _sig(nnet, "nnet_set_implicit_dz", _i, _vp, _i)
+_sig(nnet, "nnet_debug_backward", _i, _vp, _i, _ll)
+_sig(core, "kf_debug_spin", _i, _vp, _ll)
 _sig(nnet, "nnet_weights_changed", _i, _vp)
 # kf_dp.h (RCCL data parallel)
 _sig(core, "kf_dp_last_error", C.c_char_p)
@@ -135,7 +184,17 @@ def check(rc, what="kfp16"):
     if rc != 0:
         msgs = [m for m in (core.kf_last_error(), core.ops_last_error(), core.bridge_last_error(),
                             nnet.nnet_last_error()) if m]
+        stale = core.kf_pending_log()
+        if stale:   # errors other HIP calls left pending, consumed by the library's entry checks
+            msgs.append(b"[" + stale + b"]")
         raise KfError(f"{what}: " + "; ".join(m.decode() for m in msgs))
+
+
+def pending_log():
+    """kf_pending_log(): errors earlier HIP calls left pending, consumed and logged by the
+    library's entry points (kf_take_pending), or None."""
+    s = core.kf_pending_log()
+    return s.decode() if s else None
 
 
 # ---------------------------------------------------------------- device buffers
@@ -366,6 +425,12 @@ class Network:
         """Weight gradients on their own stream, overlapping the input gradients (default
         on; kf_nnet.h nnet_set_wgrad_stream)."""
         check(nnet.nnet_set_wgrad_stream(self.h, int(on)), "nnet_set_wgrad_stream")
+
+    def debug_backward(self, main_aff: int = -1, stall_cycles: int = 0):
+        """Test hook of the two-stream backward (kf_nnet.h nnet_debug_backward): where the
+        TDNN-F affine weight gradients run, and a spin of `stall_cycles` GPU cycles on the
+        weight-gradient stream before each of its batches of work."""
+        check(nnet.nnet_debug_backward(self.h, int(main_aff), int(stall_cycles)), "nnet_debug_backward")
 
     def set_implicit_dz(self, on: bool):
         """TDNN-F input gradients without the stored dz: consumers read g through the ReLU
