@@ -171,6 +171,7 @@ _sig(core, "kf_prof_enable", None, _i)
 _sig(core, "kf_prof_reserve", _i, _i)
 _sig(core, "kf_prof_collect", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double))
 _sig(core, "kf_prof_reset", None)
+_sig(core, "kf_prof_records", _i, _i, C.POINTER(_i), C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(_i))
 _sig(core, "kf_prof_collect2", _i, _i, C.POINTER(_ll), C.POINTER(C.c_double), C.POINTER(C.c_double),
      C.POINTER(C.c_double))
 
@@ -271,6 +272,18 @@ def prof_collect2(cls: int):
     n, ms, fl, by = _ll(), C.c_double(), C.c_double(), C.c_double()
     core.kf_prof_collect2(cls, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by))
     return n.value, ms.value, fl.value, by.value
+
+
+def prof_records(max_n: int = 4096):
+    """every kf_prof record since the last reset, in issue order: dicts of class, ms,
+    flops, M, N, K and tile (BM * 10000 + BN; 0 for brackets that are not one GEMM)"""
+    cls = (C.c_int * max_n)()
+    ms = (C.c_float * max_n)()
+    fl = (C.c_double * max_n)()
+    mnkt = (C.c_int * (4 * max_n))()
+    n = core.kf_prof_records(max_n, cls, ms, fl, mnkt)
+    return [dict(cls=cls[i], ms=ms[i], flops=fl[i], M=mnkt[4 * i], N=mnkt[4 * i + 1], K=mnkt[4 * i + 2],
+                 tile=mnkt[4 * i + 3]) for i in range(n)]
 
 
 def set_stream(stream_handle) -> None:
@@ -531,5 +544,6 @@ _sig(core, "kf_scale_cols", _i, _vp, _ll, _vp, _vp, _ll, _i, _i)
 _sig(core, "kf_gemm_wgrad_scaled", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i,
      _vp)
 _sig(core, "kf_gemm_debug_kil", None, _i)
+_sig(core, "kf_halo_debug_padded", None, _i)
 _sig(core, "kf_gemm_trace", None, _vp, _i, _i)
 _sig(core, "kf_quant_mxfp8", _i, _vp, _ll, _i, _i, _i, _vp, _ll, _vp, _ll)
