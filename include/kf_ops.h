@@ -320,9 +320,6 @@ void kf_clear_error(void);
  * milliseconds, flops, and per record 4 ints: M, N, K, BM * 10000 + BN; zeros for
  * brackets that are not one GEMM launch); returns the count written (at most max) */
 int kf_prof_records(int max, int *cls, float *ms, double *flops, int *mnkt);
-/* test hook: 1 = the conv halo kernels use the height-padded halo image for every
- * geometry (the r5 layout) instead of the compact one (non-strided 3x3 convs) */
-void kf_halo_debug_padded(int on);
 
 /* Error hygiene across the C-ABI. HIP keeps one pending error per host
  * thread, read and reset by hipGetLastError(). Every entry point of this library that

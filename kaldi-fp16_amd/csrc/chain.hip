@@ -487,21 +487,21 @@ template <typename XT> struct RowPre {
     }
     __device__ __forceinline__ float get(int i, int) const { return v[i]; }
 };
-// fp16 rows: nothing is computed from the loaded values at issue (den_put_exp reads only
-// positions p < P), so the fetch does not wait for its row. The recursions issue it right
-// after the frame's exchange loads (den_consume's `pf`): the exchange loads are then older
-// than the HBM row in the in-order vmcnt and do not wait for it, and the row's latency runs
-// under the consume phase instead of on its own (r6; the r5 form waited for the row between
-// the publish and the exchange wait, ~1.1 us of every frame).
 template <> struct RowPre<h16> {
-    uint32_t v[DEN_MAXPT];
+    uint32_t v[DEN_MAXPT / 2];
     __device__ __forceinline__ void fetch(const h16 *row, int P) {
         const unsigned short *u = reinterpret_cast<const unsigned short *>(row);
 #pragma unroll
-        for (int i = 0; i < DEN_MAXPT; ++i) v[i] = __builtin_nontemporal_load(u + min((int)threadIdx.x + i * DEN_THREADS, P - 1));
+        for (int i = 0; i < DEN_MAXPT / 2; ++i) {
+            int p0 = threadIdx.x + (2 * i) * DEN_THREADS, p1 = p0 + DEN_THREADS;
+            uint32_t lo = __builtin_nontemporal_load(u + min(p0, P - 1));
+            uint32_t hi = __builtin_nontemporal_load(u + min(p1, P - 1));
+            v[i] = (p0 < P ? lo : 0u) | ((p1 < P ? hi : 0u) << 16);
+        }
     }
     __device__ __forceinline__ float get(int i, int) const {
-        return (float)__builtin_bit_cast(h16, (unsigned short)v[i]);
+        unsigned short b = (unsigned short)((i & 1) ? (v[i >> 1] >> 16) : (v[i >> 1] & 0xFFFF));
+        return (float)__builtin_bit_cast(h16, b);
     }
 };
 struct StatePre {  // alpha' row prefetch (S <= DEN_MAXS * DEN_THREADS)
@@ -693,10 +693,9 @@ __device__ __forceinline__ DenV<NS> lds_v(const unsigned char *base, unsigned of
 // f(slice position, values, initp) per position. Only live sequences are loaded (rows[q] of a sequence
 // past its last frame is never read); their values are 0 in f. The partial sums load
 // with the rows, so one round trip serves both.
-template <bool LOC, int NS, class FS, class F, class PF>
+template <bool LOC, int NS, class FS, class F>
 __device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, float *const (&rows)[NS],
-                                            const bool (&live)[NS], int nsl, const float *initp, FS sum, F f,
-                                            PF pf) {
+                                            const bool (&live)[NS], int nsl, const float *initp, FS sum, F f) {
     int tid = threadIdx.x;
     // opaque to the optimiser: the row addresses below are rebuilt every frame instead of
     // being hoisted out of the frame loop as 64-bit values
@@ -724,10 +723,6 @@ __device__ __forceinline__ void den_consume(const DenX &X, int unit, int buf, fl
             for (int m = 0; m < DEN_MAXS; ++m) v[q][m] = 0.0f;
         }
     }
-    // the next frame's row fetch, younger than the exchange loads above (RowPre<h16>)
-    __builtin_amdgcn_sched_barrier(0);
-    pf();
-    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < NS; ++q)
         if (live[q]) sum(q, wave_sum(pv[q]));
@@ -951,7 +946,15 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
         for (int q = 0; q < NS; ++q) ws[q] = wave_sum(pq[q]);
         den_publish<LOC, NS>(X, tail, ws, unit);
         DEN_TP(2);
-        DEN_TP(3);  // (the row prefetch moved into the consume phase: den_consume's pf)
+        // the next frame's output rows: fetched after the publish, so their latency hides
+        // under the exchange wait (fetched at the frame start, the record loads' in-order
+        // vmcnt waits queue behind them)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            on[q] = t + 1 < U.T[q];
+            if (on[q]) pre[q].fetch(nnet + (U.r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
+        }
+        DEN_TP(3);
         if (!den_wait(X, unit, (unsigned)(G * (t + 1)), flag)) return;
         DEN_TP(4);
         float as1[NS];
@@ -964,13 +967,6 @@ __device__ __forceinline__ void den_fwd_body(const DenDev &g, const DenRun &r, c
 #pragma unroll
                                  for (int q = 0; q < NS; ++q) v.x[q] += as1[q] * leaky * ip;
                                  den_put<NS>(va, st, v, live);
-                             },
-                             [&]() {  // the next frame's output rows
-#pragma unroll
-                                 for (int q = 0; q < NS; ++q) {
-                                     on[q] = t + 1 < U.T[q];
-                                     if (on[q]) pre[q].fetch(nnet + (U.r0[q] + (long long)(t + 1) * r.stride) * r.ld, P);
-                                 }
                              });
         DEN_TP(6);
         // past the publish barrier nothing reads this frame's xe
@@ -1119,6 +1115,11 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
 #pragma unroll
         for (int q = 0; q < NS; ++q) ws[q] = wave_sum(pq[q]);
         den_publish<LOC, NS>(X, tail, ws, unit);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {  // as den_fwd_body
+            on[q] = tq[q] > 0;
+            if (on[q]) pre[q].fetch(nnet + (U.r0[q] + (long long)(tq[q] - 1) * r.stride) * r.ld, P);
+        }
         if (!den_wait(X, unit, (unsigned)(G * (it + 1)), flag)) return;
         float tb[NS];
 #pragma unroll
@@ -1132,13 +1133,6 @@ __device__ __forceinline__ void den_bwd_body(const DenDev &g, const DenRun &r, c
 #pragma unroll
                                  for (int q = 0; q < NS; ++q) v.x[q] += tb[q];
                                  den_put<NS>(vb, st, v, live);
-                             },
-                             [&]() {  // as den_fwd_body
-#pragma unroll
-                                 for (int q = 0; q < NS; ++q) {
-                                     on[q] = tq[q] > 0;
-                                     if (on[q]) pre[q].fetch(nnet + (U.r0[q] + (long long)(tq[q] - 1) * r.stride) * r.ld, P);
-                                 }
                              });
         if (gi == 0 && tid == 0) {
 #pragma unroll

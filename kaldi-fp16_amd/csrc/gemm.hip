@@ -649,13 +649,6 @@ struct HaloArgs {
     int nbuf;               // halo images (2 when nch > 1)
     int ctap[KF_MAX_PARTS];
     int bshift[KF_MAX_PARTS];  // BROW: row shift of tap p's weight block (op_wrows)
-    // compact image (r6): hmul = 1, hout = hsrc, |dh| <= 1. No height-padding rows
-    // (hpos = hout, pad = 0), so 16 consecutive output rows read 16 consecutive halo rows
-    // under every tap, across frame boundaries too (halo_off: conflict-free); the rows a
-    // tap reads past a frame's first / last height (another frame's row, or outside the
-    // image) are zeroed in the fragment: cdh[p] = tap p's height offset, -1 / 0 / +1.
-    int compact;
-    int cdh[KF_MAX_PARTS];
     unsigned mhpos;            // ceil(2^32 / hpos): R / hpos = umulhi(R, mhpos)
     unsigned long long *trace;  // diagnostics (kf_halo_trace): block 300 wave 0 stamps, else null
 };
@@ -752,19 +745,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         }
     };
 
-    // per-lane halo row of each 16-row group's row for tap 0 offset 0; compact image: bit I
-    // of hlo / hhi set when row I of this lane is a frame's first / last height
+    // per-lane halo row of each 16-row group's row for tap 0 offset 0
     int rb0[TM];
-    unsigned hlo = 0, hhi = 0;
     static_for<TM>([&](auto I) {
         const int r = wm * WTM + I * 16 + (lane & 15);
         const int m = min(m0 + r, M - 1);
         const int t = m / H.hout, h = m - t * H.hout;
         rb0[I] = (t - tbase + H.dtmin) * H.hpos + h;
-        if (H.compact) {
-            hlo |= (h == 0 ? 1u : 0u) << I;
-            hhi |= (h == H.hout - 1 ? 1u : 0u) << I;
-        }
     });
 
     float4v acc[TM][TN];
@@ -817,15 +804,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         const char *tb = bring + sb_st * B_STAGE;
         sb_st = sb_st + 1 == ST ? 0 : sb_st + 1;
         const int ct = __builtin_amdgcn_readfirstlane(H.ctap[p]);
-        const int cdh = __builtin_amdgcn_readfirstlane(H.cdh[p]);
-        const unsigned zm = cdh < 0 ? hlo : cdh > 0 ? hhi : 0u;  // rows this tap reads as zero
         static_for<BK / 32>([&](auto S) {
             constexpr int s = decltype(S)::value;
             half8 fa[TM], fb[TN];
             static_for<TM>([&](auto I) {
                 const int R = rb0[I] + ct;
                 fa[I] = *reinterpret_cast<const half8 *>(ta + halo_off(R, s * 4 + (lane >> 4)));
-                if ((zm >> I) & 1u) fa[I] = half8{};
             });
             static_for<TN>([&](auto J) { fb[J] = load_frag<BKC, BN>(tb, wn * WTN + J * 16, s, lane); });
             static_for<TM>([&](auto I) {
@@ -1250,10 +1234,6 @@ static int launch(int M, int N, int K, const OpD &A, const OpD &B, const KfEpilo
 // 1 when launched, 0 when not applicable (the caller runs the im2col GEMM), -1 on error.
 // ---------------------------------------------------------------------------
 static unsigned long long *g_halo_trace = nullptr;
-// test hook (kf_ops.h kf_halo_debug_padded): 1 = the padded image for every geometry (the
-// r5 layout), so the compact image can be compared against it
-static int g_halo_padded = 0;
-extern "C" void kf_halo_debug_padded(int on) { g_halo_padded = on != 0; }
 static int g_halo_trace_at = -1, g_halo_launches = 0;
 // diagnostics: stamp block 300 of the conv-halo launch number `at` (counted from this call)
 extern "C" void kf_halo_trace(unsigned long long *buf, int at) {
@@ -1331,12 +1311,9 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     H.hmul = a.hmul;
     H.hsrc = a.hsrc;
     H.pw = a.pw;
-    // compact image (HaloArgs::compact): no height-padding rows
-    const bool compact = a.hmul == 1 && a.hsrc == a.hout && dhmin >= -1 && dhmax <= 1 && !g_halo_padded;
-    H.compact = compact;
-    H.pad = compact ? 0 : std::max(0, -dhmin);
+    H.pad = std::max(0, -dhmin);
     const int maxshp = (a.hout - 1) * a.hmul + dhmax + H.pad;
-    const int HP = compact ? a.hsrc : std::max(a.hsrc + H.pad, maxshp + 1);
+    const int HP = std::max(a.hsrc + H.pad, maxshp + 1);
     const int hpe0 = (HP + a.hmul - 1) / a.hmul;
     H.dtmin = dtmin;
     H.ntaps = a.nparts;
@@ -1371,7 +1348,7 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     // taken when it keeps the image count and the workgroups per CU (80 KB: two)
     // (bounded: with hmul = 2 and an odd hout no pitch qualifies, so no pad is taken)
     int hpe = hpe0;
-    while (!compact && hpe < hpe0 + 8 && (hpe * a.hmul - a.hout) % 8) ++hpe;
+    while (hpe < hpe0 + 8 && (hpe * a.hmul - a.hout) % 8) ++hpe;
     const bool found8 = (hpe * a.hmul - a.hout) % 8 == 0;
     int nb1 = nb0, hb1 = hb0;
     const size_t lds1 = found8 ? geometry(hpe, nb1, hb1) : lds0;
@@ -1392,9 +1369,7 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     H.slice = (H.npieces + H.ntaps - 1) / H.ntaps;
     for (int p = 0; p < a.nparts; ++p) {
         const int x = a.dh[p] + H.pad;
-        H.ctap[p] = compact ? (a.dt[p] - dtmin) * H.hpos + a.dh[p]
-                            : (a.dt[p] - dtmin) * H.hpos + (x % a.hmul) * H.hpe + x / a.hmul;
-        H.cdh[p] = compact ? a.dh[p] : 0;
+        H.ctap[p] = (a.dt[p] - dtmin) * H.hpos + (x % a.hmul) * H.hpe + x / a.hmul;
         H.bshift[p] = brow ? b.dt[p] : 0;
     }
     // (measured and dropped: a 4-stage weight ring at one workgroup per CU, cnn2 517 ->

@@ -544,6 +544,5 @@ _sig(core, "kf_scale_cols", _i, _vp, _ll, _vp, _vp, _ll, _i, _i)
 _sig(core, "kf_gemm_wgrad_scaled", _i, _i, _i, _i, C.POINTER(KfOperand), C.POINTER(KfOperand), _vp, _ll, _vp, _i,
      _vp)
 _sig(core, "kf_gemm_debug_kil", None, _i)
-_sig(core, "kf_halo_debug_padded", None, _i)
 _sig(core, "kf_gemm_trace", None, _vp, _i, _i)
 _sig(core, "kf_quant_mxfp8", _i, _vp, _ll, _i, _i, _i, _vp, _ll, _vp, _ll)

@@ -27,6 +27,9 @@ def main():
     p.add_argument("--one-stream", action="store_true")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--json", default="")
+    p.add_argument("--variants", default="default",
+                   help="comma list of labels run in turn in this process (same-box repeats)")
+    p.add_argument("--quiet", action="store_true", help="per-class sums only")
     a = p.parse_args()
     kfp16.check(kfp16.core.bridge_gpu_init(0))
     T = a.egs * 1500
@@ -38,6 +41,13 @@ def main():
     P = net.layers[-1][3]
     og = kfp16.upload_fp16((np.random.default_rng(11).standard_normal((T, P)) * 0.01).astype(np.float16))
     kfp16.core.kf_prof_reserve(512)
+    for v in a.variants.split(","):
+        print(f"== variant {v}")
+        run(a, net, fb, og, T)
+    net.close()
+
+
+def run(a, net, fb, og, T):
     recs = []
     for s in range(a.steps):
         last = s == a.steps - 1
@@ -56,8 +66,9 @@ def main():
         name = CLS.get(r["cls"], str(r["cls"]))
         tf = r["flops"] / (r["ms"] * 1e-3) / 1e12 if r["ms"] > 0 else 0
         t = r["tile"]
-        print(f"{name:7s} {r['ms'] * 1e3:9.1f} us {tf:7.1f} TF/s  M={r['M']:8d} N={r['N']:5d} K={r['K']:5d} "
-              f"tile={t // 10000}x{t % 10000}")
+        if not a.quiet:
+            print(f"{name:7s} {r['ms'] * 1e3:9.1f} us {tf:7.1f} TF/s  M={r['M']:8d} N={r['N']:5d} K={r['K']:5d} "
+                  f"tile={t // 10000}x{t % 10000}")
         c = tot.setdefault(name, [0, 0.0, 0.0])
         c[0] += 1
         c[1] += r["ms"]
@@ -67,7 +78,6 @@ def main():
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(recs, fh)
-    net.close()
 
 
 if __name__ == "__main__":

@@ -161,39 +161,3 @@ def test_conv_halo_out8_bit_exact(gpu, hin, fin, hout, sub, fout, T):
     np.testing.assert_array_equal(codes, rq)
     np.testing.assert_array_equal(scales, rs)
 
-
-@pytest.mark.parametrize("hin,fin,hout,sub,fout,T", [s for s in SHAPES if s[3] == 1] + [(10, 256, 10, 1, 256, 400)])
-def test_conv_halo_compact_image_bit_identical(gpu, hin, fin, hout, sub, fout, T):
-    """The compact halo image (r6: no height-padding rows, the taps past a frame's first /
-    last height zeroed in the fragment) against the padded image of r5 (kf_halo_debug_padded):
-    forward and input gradient bit-identical — the same products in the same K order."""
-    kf = gpu
-    rng = np.random.default_rng(5 + hin * fin + T)
-    x = _h(rng.standard_normal((T, hin * fin)))
-    W = _h(rng.standard_normal((9 * fin, fout)) / 16)
-    M = T * hout
-    dz = _h(rng.standard_normal((M, fout)))
-    dx, dW, ddz = kf.upload_fp16(x), kf.upload_fp16(W), kf.upload_fp16(dz)
-    res = []
-    for padded in (0, 1):
-        kf.core.kf_halo_debug_padded(padded)
-        try:
-            out = kf.DeviceBuffer(M * fout * 2)
-            a = kf.operand(dx.ptr, hin * fin, M, 9 * fin, 1, nparts=9, part_width=fin, T=T, hout=hout, hsrc=hin,
-                           hmul=1, hdiv=1, tpolicy=0, dt=[o[0] for o in OFFS], dh=[o[1] for o in OFFS])
-            b = kf.operand(dW.ptr, fout, 9 * fin, fout, 0)
-            e = kf.KfEpilogue(out=out.ptr, ldo=fout, alpha=1.0)
-            kf.check(kf.core.kf_gemm_fused(M, fout, 9 * fin, C.byref(a), C.byref(b), C.byref(e)))
-            gx = kf.DeviceBuffer(T * hin * fin * 2)
-            a2 = kf.operand(ddz.ptr, hout * fout, T * hin, 9 * fout, 1, nparts=9, part_width=fout, T=T,
-                            hout=hin, hsrc=hout, hmul=1, hdiv=1, tpolicy=0,
-                            dt=[-o[0] for o in OFFS], dh=[-o[1] for o in OFFS])
-            b2 = kf.operand(dW.ptr, fout, fin, 9 * fout, 1, nparts=9, part_width=fout, T=9 * fin,
-                            dt=[p * fin for p in range(9)])
-            e2 = kf.KfEpilogue(out=gx.ptr, ldo=fin, alpha=1.0)
-            kf.check(kf.core.kf_gemm_fused(T * hin, fin, 9 * fout, C.byref(a2), C.byref(b2), C.byref(e2)))
-            res.append((kf.read_fp16(out.ptr, (M, fout)), kf.read_fp16(gx.ptr, (T * hin, fin))))
-        finally:
-            kf.core.kf_halo_debug_padded(0)
-    assert np.array_equal(res[0][0].view(np.uint16), res[1][0].view(np.uint16))
-    assert np.array_equal(res[0][1].view(np.uint16), res[1][1].view(np.uint16))
