@@ -94,6 +94,10 @@ def parse(argv=None):
                         "(nnet_set_implicit_dz; default: dz stored)")
     p.add_argument("--no-wgrad-stream", action="store_true",
                    help="weight gradients on the main stream (default: their own stream, nnet_set_wgrad_stream)")
+    p.add_argument("--all-rows", action="store_true",
+                   help="train step on every row of every layer (the reference's Network.Forward / "
+                        "Backward over all T rows) instead of the row-subsampled step (nnet_set_row_subsampling: "
+                        "the layers above the conv stack on the rows the chain objective's output rows depend on)")
     p.add_argument("--fp8", action="store_true",
                    help="MXFP8 forward GEMMs (configs[4]; use with --xconfig cnn_tdnn_17f_3072.xconfig)")
     p.add_argument("--mode", choices=("train", "forward"), default="train",
@@ -469,6 +473,16 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
     bucket_bytes = int(a.bucket_mb * (1 << 20))
     if comm is not None and mode == "train":
         net.bind_dp(comm, bucket_bytes)                    # bucketed all-reduce inside backward
+    # row-subsampled train step (kf_nnet.h nnet_set_row_subsampling): the chain objective reads
+    # the output on rows 0 (mod 3) (row0 = 1500 e + 30, frame subsampling 3), so the layers above
+    # the conv stack run on those rows and the clamped-edge tail; the objective then reads the
+    # compact output rows (row c = source row 3c)
+    rsub = mode == "train" and not fp8 and not a.all_rows and not a.implicit_dz
+    if rsub:
+        try:
+            net.set_row_subsampling(3)
+        except kfp16.KfError:   # a topology it does not cover (e.g. attention above the convs)
+            rsub = False
 
     P = net.layers[-1][3]
     # chain supervision: shared den graph, one numerator FST per eg
@@ -486,7 +500,23 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
     row0, nfr, stride = synth.chain_layout(a.egs, FRAMES_PER_EG)
     objective = chain.Chain(dgraph, max_seqs=a.egs, max_frames=int(nfr.max()))
     out_ptr = net.activation("output")[0]
-    gbuf = torch.zeros((T, P), dtype=torch.float16, device="cuda")
+    obj_rows, obj_row0, obj_stride = T, row0, stride
+    if rsub:
+        # the compact row set of this T (one untimed forward), and the objective's layout in it
+        fz = torch.zeros((T, 40), dtype=torch.float16, device="cuda")
+        if ivector_input(xcfg):
+            net.set_row_subsampling(0)
+            rsub = False
+        else:
+            net.forward(fz.data_ptr(), T)
+            tc, tc0, _ = net.row_set()
+            if tc and stride == 3 and np.all(row0 % 3 == 0):
+                obj_rows, obj_row0, obj_stride = tc, row0 // 3, 1
+            else:
+                net.set_row_subsampling(0)
+                rsub = False
+        del fz
+    gbuf = torch.zeros((obj_rows, P), dtype=torch.float16, device="cuda")
     torch.cuda.synchronize()
 
     ivd = ivector_input(xcfg)
@@ -560,7 +590,7 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
             ev_fwd.record(comp)
         if mode == "forward":
             return
-        objective.compute(num, out_ptr, P, T, row0, nfr, stride, gbuf.data_ptr(), P)
+        objective.compute(num, out_ptr, P, obj_rows, obj_row0, nfr, obj_stride, gbuf.data_ptr(), P)
         if h2d:
             ev_obj[sl].record(comp)
             if not inline:
@@ -626,7 +656,8 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
                                   "cuda")
     cpu_issue_ms = [(t_issue[i + 1] - t_issue[i]) * 1e3 for i in range(steps)]
     out = {"T": T, "elapsed": elapsed, "median_ms": median_ms, "step_ms": step_ms, "cpu_issue_ms": cpu_issue_ms, "steps": steps, "prof": prof, "chain_prof": chain_prof, "classes": classes,
-           "xconfig": xconfig, "mode": mode, "h2d": h2d, "input_pool": npool,
+           "xconfig": xconfig, "mode": mode, "h2d": h2d, "input_pool": npool, "rsub": rsub,
+           "obj_rows": obj_rows,
            "stats": stats, "ivd": ivd, "dp": (dp1[0] - dp0[0], dp1[1] - dp0[1]),
            "buckets": len(net.dp_plan(bucket_bytes)) if comm is not None else 0}
     ctx = (xcfg, params, bns, den_g, P) if keep else None
@@ -644,6 +675,7 @@ def describe(r, a, world, mode, fp8, xconfig, peak):
     mean_ms = r["elapsed"] / r["steps"] * 1e3
     value = r["T"] * world * r["steps"] / r["elapsed"]
     d = {"value": round(value, 1), "ms_per_step": round(r["median_ms"], 3), "ms_per_step_mean": round(mean_ms, 3),
+         "row_subsampled": bool(r.get("rsub")),
          "ms_per_step_min_max": [round(min(r["step_ms"]), 3), round(max(r["step_ms"]), 3)],
          "step_ms": [round(x, 2) for x in r["step_ms"]],
          "cpu_issue_ms": [round(x, 2) for x in r["cpu_issue_ms"]]}
@@ -654,6 +686,12 @@ def describe(r, a, world, mode, fp8, xconfig, peak):
         # fp8 share is in roofline.classes): against the 5 PF fp8 peak it would read ~2x
         # low and not compare with the fp16 step
         fpf = mf[1] if r["mode"] == "train" else mf[0]
+        if r.get("rsub") and r["prof"]:
+            # the row-subsampled step executes fewer GEMM FLOPs than the all-rows model count:
+            # price the step by what its GEMMs executed (kf_prof classes)
+            gemm_fl = sum(r["classes"][k][2] for k in ("gemm_fused", "conv_halo", "gemm_wgrad", "conv_wgrad"))
+            fpf = round(gemm_fl / (r["T"] * r["steps"]) / 1e6, 2)
+            d["step_mflop_per_frame_all_rows"] = mf[1]
         d["step_mfma_frac"] = round(value * fpf * 1e6 / (PEAK_FP16_TFLOPS * 1e12), 4)
         d["step_mfma_peak"] = "fp16 dense 2.5 PF"
         d["step_mflop_per_frame"] = fpf
@@ -698,22 +736,27 @@ def sub_results(a, rank, world, prof_on):
     guarded("configs[1]_forward_1536", fwd_1536)
 
     # the 3072 train step in fp16 and in MXFP8, A/B/A/B in this process: each sub-result
-    # is its second run; the speedup compares the means of both runs of each mode
+    # is its second run; the speedup compares the means of both runs of each mode (both on
+    # every row: the MXFP8 step has no row-subsampled form)
+    af = copy.copy(a)
+    af.all_rows = True
+
     def train_3072():
         ms_ab = {False: [], True: []}
         for rep in range(2):
             for f8 in (False, True):
-                r, _ = run_workload(a, "cnn_tdnn_17f_3072.xconfig", "train", f8, rank, world, None, ks, kw, prof_on)
-                d = describe(r, a, world, "train", f8, "", PEAK_FP8_TFLOPS if f8 else PEAK_FP16_TFLOPS)
+                r, _ = run_workload(af, "cnn_tdnn_17f_3072.xconfig", "train", f8, rank, world, None, ks, kw, prof_on)
+                d = describe(r, af, world, "train", f8, "", PEAK_FP8_TFLOPS if f8 else PEAK_FP16_TFLOPS)
                 ms_ab[f8].append(d["ms_per_step"])
                 if rep == 1 and not f8:
                     extra["configs[4]_train_3072_fp16"] = dict(
-                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), fp16 (the MXFP8 step's reference point)",
+                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), fp16, every row (the MXFP8 step's "
+                                 "reference point)",
                         **d)
                 elif rep == 1:
                     extra["configs[4]_train_3072_mxfp8"] = dict(
-                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD): MXFP8 forward GEMMs and strided "
-                                 "TDNN-F affine input gradients, the rest fp16", **d)
+                        workload="cnn_tdnn_17f_3072 train step (fwd+bwd+SGD), every row: MXFP8 forward GEMMs and "
+                                 "strided TDNN-F affine input gradients, the rest fp16", **d)
         m8 = extra["configs[4]_train_3072_mxfp8"]
         m8["ms_per_step_ab"] = {"fp16": ms_ab[False], "mxfp8": ms_ab[True]}
         m16, m8ms = sum(ms_ab[False]) / 2, sum(ms_ab[True]) / 2
@@ -742,6 +785,15 @@ def sub_results(a, rank, world, prof_on):
                      "(nnet_set_wgrad_stream 0): per-launch times of the fused class without co-running work",
             **describe(r, a1, world, "train", False, "cnn_tdnn_17f.xconfig", PEAK_FP16_TFLOPS))
     guarded("train_1536_one_stream", one_stream)
+
+    # the headline step on every row of every layer (the reference's row coverage)
+    def all_rows():
+        r, _ = run_workload(af, "cnn_tdnn_17f.xconfig", "train", False, rank, world, None, ks, kw, prof_on)
+        extra["train_1536_all_rows"] = dict(
+            workload="the headline train step with every layer on all T rows (--all-rows: no row subsampling, "
+                     "the reference's Network.Forward / Backward row coverage)",
+            **describe(r, af, world, "train", False, "cnn_tdnn_17f.xconfig", PEAK_FP16_TFLOPS))
+    guarded("train_1536_all_rows", all_rows)
     return extra, errors
 
 
@@ -814,13 +866,17 @@ def main():
                                   "(kf_num_batch_refill) uploaded, then RNE to fp16 on the GPU; "
                                   f"{head['input_pool']} distinct host minibatches cycled")
                                  if head["h2d"] else "resident in HBM before timing",
-                       "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)"},
+                       "objective": "chain LF-MMI (den S=7052 A=113380, num 250 states/eg, fps 490)",
+                       "rows": ("row-subsampled (nnet_set_row_subsampling 3): tdnnf7 .. output on the "
+                                f"{head['obj_rows']} rows the objective's output rows 0 (mod 3) depend on, "
+                                "the conv stack on all rows; objective and gradients as on all rows"
+                                if head.get("rsub") else "every layer on all T rows")},
         }
         out["ms_per_step_mean"] = d["ms_per_step_mean"]
         out["ms_per_step_min_max"] = d["ms_per_step_min_max"]
         out["step_ms"] = d["step_ms"]
         out["cpu_issue_ms"] = d["cpu_issue_ms"]
-        for k in ("step_mfma_frac", "step_mfma_peak", "step_mflop_per_frame", "objf_per_frame",
+        for k in ("step_mfma_frac", "step_mfma_peak", "step_mflop_per_frame", "step_mflop_per_frame_all_rows", "objf_per_frame",
                   "objective_finite_seqs"):
             if k in d:
                 out[k] = d[k]

@@ -124,6 +124,25 @@ int nnet_dp_debug_early(KfNet *net, int on);
  * caller's stream (the r4 order, A/B and tests). */
 int nnet_set_wgrad_stream(KfNet *net, int on);
 
+/* Row-subsampled train step (r6; default off). stride = 3 declares that the caller reads the
+ * output, and writes output gradients, on rows 0 (mod 3) only (the chain objective with
+ * frame-subsampling-factor 3 and every eg's first supervised row at 0 mod 3, as
+ * chain_layout / TrainStep lay them out). The layers at the top of the output chain whose
+ * row t depends only on rows t and t +- 3 of the layer below (TDNN-F with time stride 0 or
+ * 3, linear, prefinal, output, above a conv-relu-batchnorm layer) then run on the rows
+ * those outputs depend on — Kaldi nnet3's computation of only the indexes an output needs:
+ * the rows 0 (mod 3) and, through the splices' clamp at T - 1, a tail of rows
+ * T-1, T-4, ... — so each of those layers' forward and backward does a third of the work.
+ * Output rows of the set, the objective, every weight gradient and the gradient into the
+ * conv stack are those of the full computation (weight gradients up to the split-K
+ * summation order). After nnet_forward, nnet_row_set gives the compact rows tc (0 = this
+ * forward ran on full rows: fp8, implicit dz or a short T) and tc0: compact row c holds
+ * source row 3c for c < tc0, else (T-1) - 3(tc-1-c); those layers' activations
+ * (nnet_activation: rows = tc) and the output gradient nnet_backward reads are in compact
+ * rows. stride 0 / 1: off. */
+int nnet_set_row_subsampling(KfNet *net, int stride);
+int nnet_row_set(const KfNet *net, int *tc, int *tc0);
+
 /* Implicit dz (default off; fp16 steps): the input-gradient GEMM that produces a TDNN-F
  * layer's output gradient g (layers with a bypass, which store g anyway) does not also
  * store dz = rne(g * bnscale * relu_mask). The layer's affine weight gradient and input

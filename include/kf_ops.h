@@ -221,6 +221,14 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
 int kf_sgd_flat(float *w32, void *w16, const float *g, float *v, float lr, float mom,
                 long long n);
 int kf_f32_to_f16_flat(const float *src, void *dst, long long n);
+/* row sets of the row-subsampled train step (kf_nnet.h nnet_set_row_subsampling): compact
+ * row c is source row 3c for c < tc0, else (T-1) - 3(tc-1-c). row_bytes % 16 == 0.
+ * gather: dst[c] = src[row(c)] for c < tc; scatter: every full row t < T of dst gets the
+ * compact row of src whose source row is t, or zeros */
+int kf_gather_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc);
+int kf_scatter_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc);
+/* edge[c] = rne(sum over rows[0..n) in that order of src[rows[i] * ld + c]), n <= 4 (host array) */
+int kf_rows_sum_list(void *edge, const void *src, long long ld, const int *rows, int n, int cols);
 const char *kf_layers_last_error(void);
 
 /* Kaldi compressed-matrix expansion (egs input, kf_egs.h). One descriptor per stored

@@ -368,6 +368,84 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
     return lay_check("conv_c1_wgrad");
 }
 
+// ---------------------------------------------------------------------------
+// Supervised-row sets of the row-subsampled train step (kf_nnet.h
+// nnet_set_row_subsampling): compact row c of a layer above the conv stack is source row
+// crow(c) = 3c for c < tc0, else (T - 1) - 3 (tc - 1 - c) (the clamped-edge tail). One
+// thread moves 16 bytes; row_bytes % 16 == 0.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ long long crow_of(long long c, int T, int tc0, int tc) {
+    return c < tc0 ? 3 * c : (long long)(T - 1) - 3 * ((long long)tc - 1 - c);
+}
+__global__ __launch_bounds__(256) void k_gather_rows(uint4 *dst, const uint4 *src, long long vpr, int T, int tc0,
+                                                     int tc) {
+    const long long n = (long long)tc * vpr;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const long long c = i / vpr, v = i - c * vpr;
+        dst[i] = src[crow_of(c, T, tc0, tc) * vpr + v];
+    }
+}
+// full rows t < T: the compact row whose source row t is, else zero
+__global__ __launch_bounds__(256) void k_scatter_rows(uint4 *dst, const uint4 *src, long long vpr, int T, int tc0,
+                                                      int tc) {
+    const long long n = (long long)T * vpr;
+    const int nt = tc - tc0, rt = (T - 1) % 3;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const long long t = i / vpr, v = i - t * vpr;
+        long long c = -1;
+        if (t % 3 == 0 && t / 3 < tc0) c = t / 3;
+        else if (nt > 0 && t % 3 == rt && t >= (long long)(T - 1) - 3LL * (nt - 1)) c = tc - 1 - ((T - 1) - t) / 3;
+        dst[i] = c >= 0 ? src[c * vpr + v] : uint4{0u, 0u, 0u, 0u};
+    }
+}
+struct RowList {
+    int n;
+    int row[4];
+};
+// edge[c] = rne(sum over the listed rows, in list order, of src[row][c]) (fp32 sum)
+__global__ __launch_bounds__(256) void k_rows_sum_list(h16 *edge, const h16 *src, long long ld, RowList L, int cols) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= cols) return;
+    float s = 0.f;
+    for (int i = 0; i < L.n; ++i) s += h2f(src[(long long)L.row[i] * ld + c]);
+    edge[c] = f2h(s);
+}
+
+int kf_gather_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc) {
+    kf_take_pending(__func__);
+    if (row_bytes <= 0 || row_bytes % 16 || tc0 < 0 || tc < tc0 || T <= 0 || 3LL * (tc0 - 1) > T - 1) {
+        lay_set_error("gather_rows: bad geometry (row_bytes %lld T %d tc0 %d tc %d)", row_bytes, T, tc0, tc);
+        return -1;
+    }
+    if (tc == 0) return 0;
+    const long long vpr = row_bytes / 16;
+    k_gather_rows<<<kf_blocks((long long)tc * vpr, 256, 16384), 256, 0, kf_stream()>>>((uint4 *)dst, (const uint4 *)src,
+                                                                                    vpr, T, tc0, tc);
+    return lay_check("gather_rows");
+}
+int kf_scatter_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc) {
+    kf_take_pending(__func__);
+    if (row_bytes <= 0 || row_bytes % 16 || tc0 < 0 || tc < tc0 || T <= 0 || 3LL * (tc0 - 1) > T - 1) {
+        lay_set_error("scatter_rows: bad geometry (row_bytes %lld T %d tc0 %d tc %d)", row_bytes, T, tc0, tc);
+        return -1;
+    }
+    const long long vpr = row_bytes / 16;
+    k_scatter_rows<<<kf_blocks((long long)T * vpr, 256, 16384), 256, 0, kf_stream()>>>((uint4 *)dst, (const uint4 *)src,
+                                                                                     vpr, T, tc0, tc);
+    return lay_check("scatter_rows");
+}
+int kf_rows_sum_list(void *edge, const void *src, long long ld, const int *rows, int n, int cols) {
+    kf_take_pending(__func__);
+    if (n < 0 || n > 4 || cols <= 0 || (n && !rows)) {
+        lay_set_error("rows_sum_list: %d rows (at most 4), %d columns", n, cols);
+        return -1;
+    }
+    RowList L{n, {0, 0, 0, 0}};
+    for (int i = 0; i < n; ++i) L.row[i] = rows[i];
+    k_rows_sum_list<<<(cols + 255) / 256, 256, 0, kf_stream()>>>((h16 *)edge, (const h16 *)src, ld, L, cols);
+    return lay_check("rows_sum_list");
+}
+
 int kf_sgd_flat(float *w32, void *w16, const float *g, float *v, float lr, float mom,
                 long long n) {
     kf_take_pending(__func__);

@@ -72,6 +72,7 @@ struct NetLayer {
     void *gdb = nullptr;      // fp16 per-sequence gradient [maxT x dim] (combine backward)
     bool bypass = false;
     bool needs_dx = false;
+    bool compact = false;     // computed on the supervised row set (nnet_set_row_subsampling)
     // MXFP8 forward (nnet_set_fp8): output / aux copies written by the producing
     // GEMM epilogue, and the weights quantised [N][K] with each splice part padded
     Mx a8, x8, w8, w8b;
@@ -226,6 +227,27 @@ struct KfNet {
     // by the masked affine input gradient on the same chain), so off by default.
     int implicit_dz = 0;
     int main_aff = -1;             // nnet_debug_backward (tests): -1 = KF_BWD_MAIN_AFF / 1
+    // Row-subsampled train step (nnet_set_row_subsampling, r6). The chain objective reads the
+    // output on rows 0 (mod 3) only, and every layer from first_c up (TDNN-F with time
+    // stride 0 / 3, linear, prefinal, output) maps row t from rows t, t +- 3 of the layer
+    // below; with the splices' clamp at T - 1 the rows those outputs depend on are the rows
+    // 0 (mod 3) plus a tail of rows T-1, T-4, ... as deep as the layers. Those layers run on
+    // that compact set: compact row c is source row 3c for c < Tc0, else
+    // (T-1) - 3 (Tc-1-c); a splice of +-3 source rows is +-1 compact row. At the boundary
+    // (c = Tc0 - 1 whose +3 row is T-1 = compact Tc-1, and tail row Tc0 whose -3 row is not
+    // in the set) the tail row Tc0 is a scratch slot: after each linear GEMM it receives a
+    // copy of the bottleneck's row Tc - 1, so row Tc0 - 1's +1 neighbour reads row T-1, and
+    // its bottleneck gradient is zeroed after the affine input gradient (its true gradient,
+    // as every row outside the set, is zero). Its own values and those its wrong neighbour
+    // reaches stay more than the tail's depth away from every row with a gradient.
+    int rsub = 0;                  // 3: on
+    int first_c = -1;              // lowest compact layer (its input: a conv, full rows)
+    int rs_nt = 0;                 // tail rows when (T - 1) % 3 != 0
+    int Tc = 0, Tc0 = 0;           // compact rows of the current forward (0: full rows)
+    int maxTc = 0;
+    void *xc = nullptr;            // first_c's input, gathered to compact rows
+    void *dzc = nullptr;           // first_c's input gradient in compact rows
+    uint8_t *mc = nullptr;         // the mask of first_c's input, compact rows
     long long stall_side = 0;      // nnet_debug_backward (tests): spin before side work
     bool dz_imp[2] = {false, false};  // dz[i] was left implicit by the producing epilogue
     bool dz_edge[2] = {false, false}; // row T of dz[i] already holds the strided TDNN-F edge sum
@@ -948,6 +970,17 @@ extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float
     return -1;
 }
 
+// rows a layer's activations / gradients hold in the current forward
+static inline int rows_of(const KfNet *net, int idx) {
+    return (idx >= 0 && net->Tc > 0 && net->layers[idx].compact) ? net->Tc : net->T;
+}
+// compact row of source row t (nnet_set_row_subsampling), or -1 when t is not in the set
+static inline int compact_of(const KfNet *net, int t) {
+    const int T = net->T, nt = net->Tc - net->Tc0;
+    if (t % 3 == 0 && t / 3 < net->Tc0) return t / 3;
+    if (nt > 0 && t % 3 == (T - 1) % 3 && t >= T - 1 - 3 * (nt - 1) && t < T) return net->Tc - 1 - (T - 1 - t) / 3;
+    return -1;
+}
 static const void *act_of(KfNet *net, int idx) {
     if (idx == -2) return net->ivec;
     if (idx < 0) return net->features;
@@ -1219,10 +1252,25 @@ static int forward_impl(KfNet *net, const void *features, int T) {
     }
     net->T = T;
     net->features = features;
+    net->Tc = net->Tc0 = 0;
+    if (net->rsub && net->first_c >= 0 && !net->fp8 && !net->implicit_dz) {
+        const int nt = (T - 1) % 3 == 0 ? 0 : net->rs_nt;
+        const int tc0 = (T - 1) / 3 + 1;
+        if (tc0 >= 4 * nt + 16 && tc0 + nt <= net->maxTc) {
+            net->Tc0 = tc0;
+            net->Tc = tc0 + nt;
+        }
+    }
     for (size_t li = 0; li < net->layers.size(); ++li) {
         NetLayer &nl = net->layers[li];
         const Layer &L = nl.L;
         const void *x = act_of(net, nl.input);
+        if (net->Tc && (int)li == net->first_c) {  // the conv stack's output on the compact rows
+            if (!ck(kf_gather_rows(net->xc, x, (long long)L.in_dim * 2, T, net->Tc0, net->Tc), "row set gather"))
+                return -1;
+            x = net->xc;
+        }
+        const int Tl = rows_of(net, (int)li);
         const int din = L.in_dim, dout = L.out_dim;
         switch (L.type) {
             case LayerType::IDCT:
@@ -1297,7 +1345,8 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 break;
             }
             case LayerType::TDNNF: {
-                const int s = L.time_stride, bn = L.bottleneck;
+                const int T = Tl;  // compact rows (rows_of)
+                const int s = nl.compact && net->Tc ? L.time_stride / 3 : L.time_stride, bn = L.bottleneck;
                 const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
                 const int np = s > 0 ? 2 : 1;
                 const Mx *x8 = in8(net, nl);
@@ -1312,6 +1361,13 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 // force 256x256 tiles onto N = bottleneck (320 of 512 columns used) instead of
                 // 384x160 (3072 model: 331 -> see DESIGN §7)
                 if (!ck(kf_gemm_fused(T, bn, x8 ? nl.w8.ld : klin, &A, &B, &E), "tdnnf linear")) return -1;
+                // compact rows with a tail: row Tc0 - 1's +1 neighbour is row T-1 (the tail's
+                // last row); its copy goes to the scratch row Tc0 (nnet_set_row_subsampling)
+                if (nl.compact && net->Tc > net->Tc0 && s > 0 &&
+                    !ck(ops_copy((char *)nl.aux + (size_t)net->Tc0 * bn * 2,
+                                 (const char *)nl.aux + (size_t)(net->Tc - 1) * bn * 2, bn),
+                        "row set edge copy"))
+                    return -1;
                 if (net->fp8 && nl.x8.q &&
                     !ck(kf_quant_mxfp8(nl.aux, bn, T, bn, 0, nl.x8.q, nl.x8.ld, nl.x8.s, nl.x8.ld / 32),
                         "quantise bottleneck"))
@@ -1342,6 +1398,7 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 break;
             }
             case LayerType::Linear: {
+                const int T = Tl;
                 if (nl.per_seq) {  // ReplaceIndex branch: one row per sequence, any dims (ivector 100)
                     if (!ck(kf_rows_gemm(x, din, wptr(net, nl.pW), dout, nl.act, dout, net->B, din, dout),
                             "ivector linear"))
@@ -1375,6 +1432,7 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 break;
             }
             case LayerType::Prefinal: {
+                const int T = Tl;
                 const int big = L.big_dim, small = L.small_dim;
                 const Mx *x8 = in8(net, nl);
                 KfOperand A = x8 ? op_mx(*x8, T, 1, 0, 0) : op_base(x, din, T, din, 1);
@@ -1407,6 +1465,7 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 break;
             }
             case LayerType::Output: {
+                const int T = Tl;
                 const Mx *x8 = in8(net, nl);
                 KfOperand A = x8 ? op_mx(*x8, T, 1, 0, 0) : op_base(x, din, T, din, 1);
                 KfOperand B = x8 ? op_mxw(nl.w8, dout) : op_base(wptr(net, nl.pW), dout, din, dout, 0);
@@ -1431,7 +1490,7 @@ extern "C" const void *nnet_activation(const KfNet *cnet, const char *layer, int
     KfNet *net = const_cast<KfNet *>(cnet);
     for (size_t i = 0; i < net->layers.size(); ++i)
         if (net->layers[i].L.name == layer) {
-            if (rows) *rows = net->T;
+            if (rows) *rows = rows_of(net, (int)i);  // compact rows above the conv stack (row subsampling)
             if (cols) *cols = net->layers[i].L.out_dim;
             return act_of(net, (int)i);
         }
@@ -1477,7 +1536,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
             }
             // a strided P's clamped-splice edge row (row T of dz: sum of its rows T-1-s .. T-1),
             // summed by the epilogue's last row tile instead of a separate kf_rows_sum launch
-            if (L.time_stride > 0 && di >= 0 && net->T > 0) {
+            if (L.time_stride > 0 && di >= 0 && net->T > 0 && !(net->Tc && pl.compact)) {
                 const int T = net->T;
                 E.edge_out = (char *)dz_out + (size_t)T * w * 2;
                 E.edge_r0 = T - 1 - L.time_stride < 0 ? 0 : T - 1 - L.time_stride;
@@ -1655,17 +1714,37 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     // negative control of the data-parallel tests: exchanging before any producer ran
     if (net->dp && net->dp_early && !dp_issue(net, dp_next, INT_MAX)) return -1;
     to_main();
+    const int Tfull = T;
     for (int li = net->chain_out; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
         NetLayer &nl = net->layers[li];
         const Layer &L = nl.L;
+        const int T = rows_of(net, li);  // compact rows above the conv stack (row subsampling)
+        // the first compact layer's input gradient: in compact rows with the input layer's
+        // mask gathered to them, then scattered to the full rows below (zero elsewhere)
+        const bool to_full = net->Tc && li == net->first_c;
         const int din = L.in_dim, dout = L.out_dim;
-        const void *x = act_of(net, nl.input);
+        // (the first compact layer read its input gathered to the compact rows)
+        const void *x = net->Tc && li == net->first_c ? net->xc : act_of(net, nl.input);
         bool want_dx = nl.needs_dx && nl.input >= 0;
         void *dz_next = net->dz[flip], *g_next = net->g[flip];
         void *const dbott_buf = (nbott & 1) && two ? net->dbott2 : net->dbott;
         net->dz8_layer[flip] = -1;
         KfEpilogue E;
         if (want_dx && !dx_epilogue(net, nl.input, dz_next, g_next, E)) return -1;
+        if (want_dx && to_full) {
+            const NetLayer &pl = net->layers[nl.input];
+            const int w = pl.L.out_dim;
+            if (E.out || !E.out2 || E.edge_out || E.out8 || (E.mask_in && !pl.mask) || (w * 2) % 16 || (w / 8) % 16) {
+                set_err("row subsampling: unsupported input gradient into " + pl.L.name);
+                return -1;
+            }
+            if (E.mask_in) {
+                if (!ck(kf_gather_rows(net->mc, pl.mask, w / 8, Tfull, net->Tc0, net->Tc), "row set mask gather"))
+                    return -1;
+                E.mask_in = net->mc;
+            }
+            E.out2 = net->dzc;
+        }
         // a weight gradient: on side, after what main enqueued so far
         auto wgrad = [&](const std::function<bool()> &f) -> bool {
             if (!to_side()) return false;
@@ -1753,7 +1832,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 break;
             }
             case LayerType::TDNNF: {
-                const int s = L.time_stride, bn = L.bottleneck;
+                const int s = nl.compact && net->Tc ? L.time_stride / 3 : L.time_stride, bn = L.bottleneck;
                 const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
                 // implicit dz (dx_epilogue): the layer's g read through its ReLU mask, the BN
                 // scale applied to the weight gradient's columns and folded into W2 below
@@ -1815,9 +1894,18 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     // sum_{t >= T-1-s} dz[t] (clamped-splice transpose)
                     void *edge = (char *)dzs + (size_t)T * dout * 2;
                     const bool have_edge = !imp && ib >= 0 && net->dz_edge[ib];  // dx_epilogue's
-                    if (!have_edge && !ck(kf_rows_sum_mask(edge, dzs, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout,
-                                                           imp ? nl.mask : nullptr),
-                                          "edge"))
+                    if (nl.compact && net->Tc) {
+                        // compact rows: the source rows T-1-3 .. T-1 that are in the set, in
+                        // source order (the others carry no gradient)
+                        int rows[4], nr = 0;
+                        for (int t = std::max(0, Tfull - 1 - L.time_stride); t < Tfull; ++t) {
+                            const int c = compact_of(net, t);
+                            if (c >= 0 && nr < 4) rows[nr++] = c;
+                        }
+                        if (!ck(kf_rows_sum_list(edge, dzs, dout, rows, nr, dout), "row set edge")) return -1;
+                    } else if (!have_edge && !ck(kf_rows_sum_mask(edge, dzs, dout, T - 1 - s < 0 ? 0 : T - 1 - s, T, dout,
+                                                                  imp ? nl.mask : nullptr),
+                                                 "edge"))
                         return -1;
                     KfOperand B1 = op_wrows(w2, 2, bn, dout);
                     if (net->fp8 && i8 >= 0 && net->dz8_layer[i8] == li && T > 1) {
@@ -1849,6 +1937,10 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         A1.edge_row[1] = T;
                         if (!ck(kf_gemm_fused(T, bn, 2 * dout, &A1, &B1, &E1), "tdnnf affine dgrad"))
                             return -1;
+                        // compact rows: the scratch row Tc0 read row Tc0 - 1's gradient through
+                        // the +1 adjacency; its true gradient is zero
+                        if (nl.compact && net->Tc > net->Tc0)
+                            bridge_gpu_memset((char *)dbott + (size_t)net->Tc0 * bn * 2, 0, (size_t)bn * 2);
                     }
                 } else {
                     KfOperand A1 = masked(op_base(dzs, dout, T, dout, 1));
@@ -2055,6 +2147,11 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 set_err("backward: unsupported layer " + L.name);
                 return -1;
         }
+        if (want_dx && to_full) {
+            const int w = net->layers[nl.input].L.out_dim;
+            if (!ck(kf_scatter_rows(dz_next, net->dzc, (long long)w * 2, Tfull, net->Tc0, net->Tc), "row set scatter"))
+                return -1;
+        }
         // gradient buckets complete at this step go to the communication stream (their
         // gates on side, behind the step's weight gradients)
         if (two) kf_set_stream(net->wg_stream);
@@ -2099,6 +2196,66 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
 extern "C" int nnet_set_implicit_dz(KfNet *net, int on) {
     if (!net) return -1;
     net->implicit_dz = on != 0;
+    return 0;
+}
+
+extern "C" int nnet_set_row_subsampling(KfNet *net, int stride) {
+    if (!on_device(net, "set_row_subsampling")) return -1;
+    if (stride == 0 || stride == 1) {
+        net->rsub = 0;
+        return 0;
+    }
+    if (stride != 3) {
+        set_err("set_row_subsampling: stride " + std::to_string(stride) + " (only 3: chain frame subsampling)");
+        return -1;
+    }
+    // the top of the output chain whose rows are row-local or 3-strided: TDNN-F with time
+    // stride 0 or 3, linear, prefinal, output; consecutive layers, nothing else reads them
+    const int n = (int)net->layers.size();
+    if (net->chain_out != n - 1) {
+        set_err("set_row_subsampling: the chain output must be the last layer");
+        return -1;
+    }
+    int first = -1, n3 = 0;
+    for (int li = net->chain_out; li >= 0; li = net->layers[li].input) {
+        const NetLayer &nl = net->layers[li];
+        const Layer &L = nl.L;
+        const bool ok = (L.type == LayerType::TDNNF && (L.time_stride == 0 || L.time_stride == 3)) ||
+                        (L.type == LayerType::Linear && !nl.per_seq) || L.type == LayerType::Prefinal ||
+                        L.type == LayerType::Output;
+        if (!ok || nl.input != li - 1) break;
+        first = li;
+        if (L.type == LayerType::TDNNF && L.time_stride == 3) ++n3;
+    }
+    if (first < 0 || net->layers[first].input < 0 || net->layers[net->layers[first].input].L.type != LayerType::ConvReluBN) {
+        set_err("set_row_subsampling: needs row-local / 3-strided layers above a conv-relu-batchnorm layer");
+        return -1;
+    }
+    // tail depth: one row per 3-strided layer and a margin (the scratch row's reach)
+    const int nt = n3 + 4;
+    const int maxTc = (net->max_T - 1) / 3 + 1 + nt;
+    const int din = net->layers[first].L.in_dim;
+    if (!net->xc || net->maxTc < maxTc || net->first_c != first) {
+        net->xc = net->dalloc((size_t)maxTc * din * 2);
+        net->dzc = net->dalloc((size_t)(maxTc + 2) * din * 2);
+        net->mc = (uint8_t *)net->dalloc(align_up((size_t)maxTc * din / 8 + 16, 256));
+        if (!net->xc || !net->dzc || !net->mc) {
+            set_err("set_row_subsampling: alloc compact buffers");
+            return -1;
+        }
+    }
+    for (int li = 0; li < n; ++li) net->layers[li].compact = li >= first;
+    net->first_c = first;
+    net->rs_nt = nt;
+    net->maxTc = maxTc;
+    net->rsub = 3;
+    return 0;
+}
+
+extern "C" int nnet_row_set(const KfNet *net, int *tc, int *tc0) {
+    if (!net) return -1;
+    if (tc) *tc = net->Tc;
+    if (tc0) *tc0 = net->Tc0;
     return 0;
 }
 

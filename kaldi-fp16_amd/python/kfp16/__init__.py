@@ -149,6 +149,8 @@ _sig(nnet, "nnet_dp_plan", _i, _vp, _ll, _i, C.POINTER(_i), C.POINTER(_ll), C.PO
 _sig(nnet, "nnet_dp_debug_early", _i, _vp, _i)
 _sig(nnet, "nnet_set_wgrad_stream", _i, _vp, _i)
 _sig(nnet, "nnet_set_implicit_dz", _i, _vp, _i)
+_sig(nnet, "nnet_set_row_subsampling", _i, _vp, _i)
+_sig(nnet, "nnet_row_set", _i, _vp, C.POINTER(_i), C.POINTER(_i))
 _sig(nnet, "nnet_debug_backward", _i, _vp, _i, _ll)
 _sig(core, "kf_debug_spin", _i, _vp, _ll)
 _sig(nnet, "nnet_weights_changed", _i, _vp)
@@ -444,6 +446,22 @@ class Network:
         TDNN-F affine weight gradients run, and a spin of `stall_cycles` GPU cycles on the
         weight-gradient stream before each of its batches of work."""
         check(nnet.nnet_debug_backward(self.h, int(main_aff), int(stall_cycles)), "nnet_debug_backward")
+
+    def set_row_subsampling(self, stride: int):
+        """Row-subsampled train step (kf_nnet.h nnet_set_row_subsampling): 3 = the layers above
+        the conv stack run on the rows the chain objective's output rows 0 (mod 3) depend on;
+        0 = off (full rows)."""
+        check(nnet.nnet_set_row_subsampling(self.h, int(stride)), "nnet_set_row_subsampling")
+
+    def row_set(self):
+        """(tc, tc0, rows) of the last forward: tc compact rows (0: full rows), compact row c is
+        source row rows[c] (3c for c < tc0, then the tail (T-1) - 3(tc-1-c))."""
+        tc, tc0 = _i(), _i()
+        check(nnet.nnet_row_set(self.h, C.byref(tc), C.byref(tc0)), "nnet_row_set")
+        n, n0 = tc.value, tc0.value
+        T = self.T
+        rows = np.array([3 * c if c < n0 else (T - 1) - 3 * (n - 1 - c) for c in range(n)], np.int64)
+        return n, n0, rows
 
     def set_implicit_dz(self, on: bool):
         """TDNN-F input gradients without the stored dz: consumers read g through the ReLU
