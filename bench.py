@@ -648,12 +648,20 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
             chain_prof[name] = classes[name][:3]
         kfp16.core.kf_prof_reset()
     stats = [0.0] * 5
+
+    def probe(where):
+        """attribute a HIP error left pending by the torch call just made (kf_take_pending
+        logs it under `where`; the library's own entry checks would otherwise see it first)"""
+        if kfp16.core.kf_peek_error():
+            kfp16.core.kf_take_pending(("the bench's check after " + where).encode())
     if mode == "train":
         # fails if a den exchange timed out in ANY step since the previous result
         # (warm-up and timed steps): a silently wrong gradient is never reported
         res = objective.result()
+        probe("kf_chain_result")
         stats = dp.sum_over_ranks([res.objf, res.num_logprob, res.den_logprob, res.frames, res.num_ok],
                                   "cuda")
+        probe("dp.sum_over_ranks (torch.tensor on cuda, .tolist())")
     cpu_issue_ms = [(t_issue[i + 1] - t_issue[i]) * 1e3 for i in range(steps)]
     out = {"T": T, "elapsed": elapsed, "median_ms": median_ms, "step_ms": step_ms, "cpu_issue_ms": cpu_issue_ms, "steps": steps, "prof": prof, "chain_prof": chain_prof, "classes": classes,
            "xconfig": xconfig, "mode": mode, "h2d": h2d, "input_pool": npool, "rsub": rsub,
@@ -662,6 +670,7 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
            "buckets": len(net.dp_plan(bucket_bytes)) if comm is not None else 0}
     ctx = (xcfg, params, bns, den_g, P) if keep else None
     torch.cuda.synchronize()
+    probe("torch.cuda.synchronize")
     for nb in (nums if h2d else [nbatch]):
         nb.close()
     objective.close()

@@ -30,6 +30,7 @@ def main():
     p.add_argument("--variants", default="default",
                    help="comma list of labels run in turn in this process (same-box repeats)")
     p.add_argument("--quiet", action="store_true", help="per-class sums only")
+    p.add_argument("--rsub", action="store_true", help="row-subsampled step (nnet_set_row_subsampling 3)")
     a = p.parse_args()
     kfp16.check(kfp16.core.bridge_gpu_init(0))
     T = a.egs * 1500
@@ -39,7 +40,12 @@ def main():
         net.set_wgrad_stream(False)
     fb = kfp16.upload_fp16(synth.make_features(T, 40))
     P = net.layers[-1][3]
-    og = kfp16.upload_fp16((np.random.default_rng(11).standard_normal((T, P)) * 0.01).astype(np.float16))
+    rows = T
+    if a.rsub:
+        net.set_row_subsampling(3)
+        net.forward(fb.ptr, T)
+        rows = net.row_set()[0] or T
+    og = kfp16.upload_fp16((np.random.default_rng(11).standard_normal((rows, P)) * 0.01).astype(np.float16))
     kfp16.core.kf_prof_reserve(512)
     for v in a.variants.split(","):
         print(f"== variant {v}")
