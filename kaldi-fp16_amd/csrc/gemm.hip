@@ -1520,8 +1520,13 @@ static int fused_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     // 215 -> 207 us (rocprof A/B/A/B). Not with an MXFP8 copy: its 48-column wave tiles do
     // not hold whole 32-column blocks (and 32x96 wave tiles overflow the epilogue's LDS).
     if (tile == 6 && K <= 640 && N % 192 == 0 && !E.out8) tile = 7;
+    // N = 160 / 320 with few row blocks (the row-subsampled TDNN-F stack: M = T / 3): 128x160
+    // 4-wave tiles, two workgroups per CU, so that the launch fills the CUs (384x160 at
+    // M = 32,020 is 84 workgroups)
+    if (tile == 5 && (long long)((M + 383) / 384) * ((N + 159) / 160) < 192) tile = 8;
 #define KF_FUSED(BKC_, AM_, BM_)                                                                 \
     do {                                                                                         \
+        if (tile == 8) return launch<128, 160, 2, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 7) return launch<128, 192, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 6) return launch<192, 128, 2, 4, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
         if (tile == 5) return launch<384, 160, 4, 2, true, BKC_, false, 2, AM_, BM_>(M, N, K, a, b, E, G, 1); \
