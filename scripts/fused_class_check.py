@@ -19,7 +19,8 @@ def fused(n):
 
 
 d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows if fused(r["Kernel_Name"])]
-timed = d[warm * per_step:(warm + steps) * per_step]
+skip = line["roofline"].get("priming_launches", 0) + warm * per_step
+timed = d[skip:skip + steps * per_step]
 bench_us = line["roofline"]["kernel_ms_per_step"] * 1e3 / per_step
 print(json.dumps({"launches_timed": len(timed), "rocprof_avg_us": round(sum(timed) / len(timed), 1),
                   "bench_hip_event_avg_us": round(bench_us, 1),
