@@ -76,6 +76,11 @@ typedef struct {
     long long lds;             /* MXFP8: bytes between the scale rows of consecutive source rows */
     const uint8_t *mask;       /* masked operand (above), or NULL */
     int mask_rows;             /* source rows the mask covers */
+    /* time-strided rows (a conv evaluated on a subset of its output frames, the row-
+     * subsampled step's last conv): st = t0 + t*tmul + dt[p] in the rule above. 0 / 0 =
+     * the plain rule. Only the A operand of a kf_gemm_fused convolution that runs on the
+     * halo kernel takes it; other uses fail. */
+    int tmul, t0;
 } KfOperand;
 
 #define KF_FMT_FP16 0
@@ -120,6 +125,11 @@ typedef struct {
     int out8_src;          /* 0: out8 quantises v (out's value); 1: out2's value (needs out2) */
     void *edge_out;        /* fp16 [N], or NULL: column sums of rows [edge_r0, edge_r1) (above) */
     int edge_r0, edge_r1, edge_src;
+    /* grouped output rows: with row_group > 0, GEMM row m addresses row
+     * (m / row_group) * row_stride + m % row_group of every row operand above (out, out2,
+     * resid, mask_out, mask_in, out8): a transposed conv evaluated on every third frame
+     * writes its frames in place. 0 = rows as they are. Not with edge_out. */
+    int row_group, row_stride;
 } KfEpilogue;
 
 /* current stream for every launch made by this library on the calling thread

@@ -1711,6 +1711,7 @@ struct DenXBuf {
     ~DenXBuf() {
         if (buf) hipFree(buf);
         if (cnt) hipFree(cnt);
+        if (h_word) hipHostFree(h_word);
     }
     // nseqs sequences in units of ns, G blocks per unit, over table `tb` (the f table for
     // the forward recursion, b for the backward)
@@ -1778,11 +1779,22 @@ struct DenXBuf {
     unsigned spin_limit = 1u << 21;
     int force_sys = 0;
     // blocks that timed out since the last call (stream-ordered read, then cleared)
+    // (read through a pinned word: a stream-ordered copy into pageable memory left
+    // hipErrorStreamCaptureUnsupported pending on the calling thread in the r6 bench)
+    unsigned *h_word = nullptr;
     unsigned take_timeouts(hipStream_t st) {
         if (!cnt) return 0;
-        unsigned v = 0;
-        hipMemcpyAsync(&v, cnt, 4, hipMemcpyDeviceToHost, st);
+        if (!h_word && hipHostMalloc((void **)&h_word, 64, hipHostMallocDefault) != hipSuccess) {
+            h_word = nullptr;
+            kf_take_pending("DenXBuf::take_timeouts hipHostMalloc");
+            return 0;
+        }
+        *h_word = 0;
+        hipMemcpyAsync(h_word, cnt, 4, hipMemcpyDeviceToHost, st);
+        kf_take_pending("DenXBuf::take_timeouts hipMemcpyAsync");
         hipStreamSynchronize(st);
+        kf_take_pending("DenXBuf::take_timeouts hipStreamSynchronize");
+        const unsigned v = *h_word;
         if (v) {
             hipMemsetAsync(cnt, 0, 4, st);
             hipStreamSynchronize(st);
@@ -2603,6 +2615,7 @@ struct KfChain {
     int max_seqs = 0, max_frames = 0;
     float *alpha_store = nullptr, *beta_store = nullptr, *asum_store = nullptr, *bsum_store = nullptr;
     float *stats = nullptr;
+    float *h_stats = nullptr;     // pinned [max_seqs][8] (kf_chain_result)
     float *num_ab = nullptr;      // numerator alpha/beta
     size_t num_ab_cap = 0;
     float *num_post = nullptr;    // sparse numerator posteriors
@@ -2638,6 +2651,7 @@ struct KfChain {
             }
             if (h_stage[i]) hipHostFree(h_stage[i]);
         }
+        if (h_stats) hipHostFree(h_stats);
         if (side) hipStreamDestroy(side);
         if (ev_in) hipEventDestroy(ev_in);
         if (ev_num) hipEventDestroy(ev_num);
@@ -3122,14 +3136,30 @@ extern "C" const float *kf_chain_seq_stats(const KfChain *c) { return c ? c->sta
 
 extern "C" int kf_chain_result(KfChain *c, KfChainResult *out) {
     if (!c || !out) return -1;
+    kf_take_pending("kf_chain_result");
     const int n = c->last_nseq;
-    std::vector<float> s((size_t)n * 8);
     hipStream_t st = kf_stream();
-    if (n) hipMemcpyAsync(s.data(), c->stats, s.size() * 4, hipMemcpyDeviceToHost, st);
+    // pinned staging (a stream-ordered copy into pageable memory left a spurious
+    // hipErrorStreamCaptureUnsupported pending on the calling thread)
+    if (n && !c->h_stats &&
+        hipHostMalloc((void **)&c->h_stats, (size_t)c->max_seqs * 8 * 4, hipHostMallocDefault) != hipSuccess) {
+        c->h_stats = nullptr;
+        kf_take_pending("kf_chain_result hipHostMalloc");
+        kfc_set_error("kf_chain_result: pinned staging allocation failed");
+        return -1;
+    }
+    if (n && hipMemcpyAsync(c->h_stats, c->stats, (size_t)n * 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess) {
+        kf_take_pending("kf_chain_result hipMemcpyAsync");
+        kfc_set_error("kf_chain_result: statistics copy failed");
+        return -1;
+    }
     if (hipStreamSynchronize(st) != hipSuccess) {
+        kf_take_pending("kf_chain_result hipStreamSynchronize");
         kfc_set_error("kf_chain_result: stream error");
         return -1;
     }
+    kf_take_pending("kf_chain_result after the statistics copy");
+    const float *s = c->h_stats;
     // every compute since the last result: the sticky count is never reset by a launch
     if (const unsigned nt = c->xbuf.take_timeouts(st) + c->xbuf2.take_timeouts(st)) {
         kfc_set_error("kf_chain_result: den cross-workgroup exchange timed out in %u block(s) since the last "

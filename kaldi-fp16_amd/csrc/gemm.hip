@@ -225,7 +225,9 @@ struct EpiMap {
     }
 };
 
-template <int BM, int BN, int WM, int WN>
+// RG: the epilogue honours KfEpilogue.row_group (the conv input-gradient halo kernels only:
+// the row map's registers cost the 80 KB GEMM tiles their second workgroup per CU)
+template <int BM, int BN, int WM, int WN, bool RG = false>
 __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN / WN / 16], char *smem,
                                                const KfEpilogue &E, int M, int N, int m0, int n0,
                                                int tid, int lane, int wave, const EpiPre *pre = nullptr) {
@@ -233,6 +235,13 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;
     const int wm = wave / WN, wn = wave % WN;
+    // grouped output rows (KfEpilogue.row_group): the address row of GEMM row m
+    const int rg = RG ? E.row_group : 0;
+    auto arow = [&](int m) -> long long {
+        if (!RG || rg <= 0) return m;
+        const int g = m / rg;
+        return (long long)g * E.row_stride + (m - g * rg);
+    };
     wait_vmcnt<0>();
     __syncthreads();
     float *prm = reinterpret_cast<float *>(smem);
@@ -271,7 +280,7 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
             const int r = EM::row(k, lane), cg = EM::cg(k, lane);
             const int m = m0 + wm * WTM + icp * 32 + r, n = n0 + wn * WTN + 8 * cg;
             rres[sl][k] = half8{};
-            if (m < M && n < N && E.resid) rres[sl][k] = load_h8((const h16 *)E.resid + (long long)m * E.ldr + n);
+            if (m < M && n < N && E.resid) rres[sl][k] = load_h8((const h16 *)E.resid + arow(m) * E.ldr + n);
         });
     };
     auto prefetch = [&](auto ICc) {
@@ -283,8 +292,8 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
             const bool ok = m < M && n < N;
             cold[sl][k] = half8{};
             mb[sl][k] = 0xFFu;
-            if (ok && E.beta != 0.f) cold[sl][k] = load_h8((const h16 *)E.out + (long long)m * E.ldo + n);
-            if (ok && E.mask_in) mb[sl][k] = E.mask_in[((long long)m * E.ldo2 + n) >> 3];
+            if (ok && E.beta != 0.f) cold[sl][k] = load_h8((const h16 *)E.out + arow(m) * E.ldo + n);
+            if (ok && E.mask_in) mb[sl][k] = E.mask_in[(arow(m) * E.ldo2 + n) >> 3];
         });
     };
     static_for<NSL - 1>([&](auto IC) { prefetch_res(IC); });
@@ -320,7 +329,7 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
                     v[e] = x0[e];
                     v[e + 4] = x1[e];
                 }
-                epilogue8(E, P, m, n, nl, v, cold[sl][k], rres[slr][k], mb[sl][k]);
+                epilogue8(E, P, arow(m), n, nl, v, cold[sl][k], rres[slr][k], mb[sl][k]);
             }
             if constexpr (CG % 4 == 0) {
                 // MXFP8 copy: the 4 lanes l..l+3 (l % 4 == 0) hold one 32-column block
@@ -337,8 +346,9 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
                     for (int e = 0; e < 8; ++e) q[e] = v[e] * inv;
                     const uint2 pk = pack_e4m3x8(q);
                     if (live) {
-                        *reinterpret_cast<uint2 *>((uint8_t *)E.out8 + (long long)m * E.ldo8 + n) = pk;
-                        if ((lane & 3) == 0) E.scale8[(long long)m * (E.ldo8 >> 5) + (n >> 5)] = (uint8_t)(ex + 127);
+                        const long long ma = arow(m);
+                        *reinterpret_cast<uint2 *>((uint8_t *)E.out8 + ma * E.ldo8 + n) = pk;
+                        if ((lane & 3) == 0) E.scale8[ma * (E.ldo8 >> 5) + (n >> 5)] = (uint8_t)(ex + 127);
                     }
                 }
             }
@@ -642,6 +652,7 @@ struct HaloArgs {
     long long ld;
     int T, hout, hmul, hsrc, pw, pad, hpe, hpos, nf, dtmin;
     int ntaps, nch;         // taps, 64-channel chunks per tap
+    int ts, toff;           // output frame t reads source frames ts * t + toff + dt (1 / 0: plain)
     int rows;               // halo rows per chunk image (nf * hpos)
     int npieces;            // 1 KiB LDS-DMA pieces per image (ceil(rows / 8))
     int slice;              // pieces issued per step (ceil(npieces / ntaps))
@@ -714,7 +725,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
     }
     const int mt = tile / n_ntiles, nt = tile - mt * n_ntiles;
     const int m0 = mt * BM, n0 = nt * BN;
-    const int tbase = m0 / H.hout + H.dtmin;
+    const int tbase = H.ts * (m0 / H.hout) + H.toff + H.dtmin;
 
     const bool bwave = wave < NWB;
     SB sb;
@@ -751,7 +762,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         const int r = wm * WTM + I * 16 + (lane & 15);
         const int m = min(m0 + r, M - 1);
         const int t = m / H.hout, h = m - t * H.hout;
-        rb0[I] = (t - tbase + H.dtmin) * H.hpos + h;
+        rb0[I] = (H.ts * t + H.toff - tbase + H.dtmin) * H.hpos + h;
     });
 
     float4v acc[TM][TN];
@@ -822,7 +833,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_halo_kernel(int M, int N
         HALO_TP(2 + 2 * st);
     }
     HALO_TP(126);
-    fused_epilogue<BM, BN, WM, WN>(acc, dsm, E, M, N, m0, n0, tid, lane, wave, &epre);
+    fused_epilogue<BM, BN, WM, WN, BROW>(acc, dsm, E, M, N, m0, n0, tid, lane, wave, &epre);
     HALO_TP(127);
 #undef HALO_TP
 }
@@ -1138,6 +1149,12 @@ static bool to_dev(const KfOperand &d, OpD &o, const char *name) {
         const long long lim = (long long)d.mask_rows * d.ld * 2;
         o.mlim = lim > 0xFFFFFFF0LL ? 0xFFFFFFF0u : (unsigned)lim;
     }
+    if (d.tmul < 0 || d.t0 < 0 || (d.tmul > 1 && (f8 || d.hout < 2))) {
+        kf_set_error("operand %s: time-strided rows (tmul=%d t0=%d) need an fp16 conv operand", name, d.tmul, d.t0);
+        return false;
+    }
+    o.tmul = d.tmul > 1 ? d.tmul : 1;
+    o.t0 = d.t0;
     o.ldb = (unsigned)(d.ld * 2 / u);
     o.pwb = (unsigned)(d.part_width * 2 / u);
     // 32-bit byte offsets (buffer addressing): the largest source row must fit
@@ -1286,6 +1303,7 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
                 b.nparts == a.nparts && b.pw == a.pw;
     for (int p = 0; brow && p < b.nparts; ++p) brow = b.dt[p] >= 0 && b.dt[p] + b.nrows <= b.T;
     if (bkc && !brow) return 0;
+    if (E.row_group && !brow) return 0;  // grouped rows: the input-gradient (BROW) kernels only
     OpD bp = b;
     if (brow) {  // one 64-column chunk of a plain [nrows x ld] matrix, rebased per step
         bp.simple = 1;
@@ -1325,8 +1343,12 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     // gradients (3 or 6 taps; two workgroups per CU): cnn3 461 -> 332 and 588 -> 460 us,
     // cnn5 370 -> 317 and 536 -> 468 us
     const bool residue = brow && a.nparts < 9;
-    const int BM_ = residue ? 128 : 256;
-    H.nf = (BM_ - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
+    // time-strided rows (a.tmul > 1): a tile's output frames read tmul times the source
+    // frames, so 128-row tiles keep the image in LDS
+    const int BM_ = residue || a.tmul > 1 ? 128 : 256;
+    H.ts = a.tmul;
+    H.toff = a.t0;
+    H.nf = H.ts * ((BM_ - 1 + a.hout - 1) / a.hout) + 1 + (dtmax - dtmin);
     const int nw = BN_ == 64 ? 4 : 8;
     const size_t epi = 16 * BN_ + 32 * EpiMap<64>::LDT * 4 * nw;
     // LDS of a halo geometry: two images when there are several channel chunks, else one
@@ -1444,6 +1466,11 @@ static int fused_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
         kf_set_error("kf_gemm_fused: out8_src = 1 needs out2");
         return -1;
     }
+    if (E.row_group < 0 || (E.row_group > 0 && (E.row_stride < E.row_group || E.edge_out || edge))) {
+        kf_set_error("kf_gemm_fused: row_group %d / row_stride %d (row_stride >= row_group > 0, no edge row)",
+                     E.row_group, E.row_stride);
+        return -1;
+    }
     if (E.out8 && (N % 32 || E.ldo8 % 32 || !E.scale8)) {
         kf_set_error("kf_gemm_fused: out8 needs N and ldo8 multiples of 32 and scale8");
         return -1;
@@ -1460,6 +1487,10 @@ static int fused_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     const bool f8 = A->fmt == KF_FMT_MXFP8;
     if (f8 != (B->fmt == KF_FMT_MXFP8)) {
         kf_set_error("kf_gemm_fused: both operands must be MXFP8, or neither");
+        return -1;
+    }
+    if (E.row_group && (f8 || a.mk || b.mk)) {
+        kf_set_error("kf_gemm_fused: grouped output rows (row_group) need an fp16 conv input gradient");
         return -1;
     }
     if (f8) {
@@ -1505,6 +1536,11 @@ static int fused_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     {  // the halo kernel shares fused_epilogue, MXFP8 copy included (BN >= 64)
         const int hr = conv_halo_try(M, N, K, a, b, bm, B->kcontig != 0, E);
         if (hr != 0) return hr < 0 ? -1 : 0;
+    }
+    if (a.tmul > 1 || a.t0 || b.tmul > 1 || b.t0 || E.row_group) {
+        kf_set_error("kf_gemm_fused: time-strided rows (tmul / t0) and grouped output rows (row_group) need a "
+                     "conv on the halo kernel (M=%d N=%d K=%d)", M, N, K);
+        return -1;
     }
     // Tiles: 384x160 8-wave for N = 160 / 320; 256x64 for N <= 64; for
     // N >= 256 192x128 (or 128x192, below) 8-wave tiles (80 KB of LDS: two workgroups share a CU and one's
@@ -1595,6 +1631,10 @@ static int wgrad_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     if (M <= 0 || N <= 0) return 0;
     OpD a, b;
     if (!to_dev(*A, a, "A") || !to_dev(*B, b, "B")) return -1;
+    if (a.tmul > 1 || a.t0 || b.tmul > 1 || b.t0) {
+        kf_set_error("kf_gemm_wgrad: time-strided rows (tmul / t0) are a conv forward operand only");
+        return -1;
+    }
     if (A->kcontig || B->kcontig) {
         kf_set_error("kf_gemm_wgrad: A and B must be reduction-major");
         return -1;

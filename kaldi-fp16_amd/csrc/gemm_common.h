@@ -32,6 +32,7 @@ struct OpD {
     // e.g. an edge row) are unmasked
     const uint8_t *mk;
     unsigned mlim;
+    int tmul, t0;       // time-strided rows (KfOperand.tmul / t0; conv halo forward only)
 };
 
 // compile-time loop: body(I) with I a std::integral_constant (forces full unrolling,
@@ -381,7 +382,7 @@ struct EpiCols {
     const float *bias, *scale, *shift, *scale2;  // LDS, indexed by local column
 };
 
-__device__ __forceinline__ void epilogue8(const KfEpilogue &E, const EpiCols &P, int m, int n,
+__device__ __forceinline__ void epilogue8(const KfEpilogue &E, const EpiCols &P, long long m, int n,
                                           int nl, float v[8], half8 cold, half8 rres,
                                           unsigned mbits) {
 #pragma unroll

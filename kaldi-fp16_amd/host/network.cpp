@@ -242,6 +242,11 @@ struct KfNet {
     // reaches stay more than the tail's depth away from every row with a gradient.
     int rsub = 0;                  // 3: on
     int first_c = -1;              // lowest compact layer (its input: a conv, full rows)
+    // the conv below first_c evaluated on the compact rows only (its output frames 3c and the
+    // tail; time-strided halo operand, kf_ops.h KfOperand.tmul): its activation and mask are
+    // then in compact rows and first_c reads them directly. Its backward stays on full rows
+    // (the input gradient scattered back). KF_RSUB_CONV=0 at nnet_set_row_subsampling: off.
+    int conv_c = 0;
     int rs_nt = 0;                 // tail rows when (T - 1) % 3 != 0
     int Tc = 0, Tc0 = 0;           // compact rows of the current forward (0: full rows)
     int maxTc = 0;
@@ -974,6 +979,14 @@ extern "C" int nnet_set_bn(KfNet *net, const char *layer, int which, const float
 static inline int rows_of(const KfNet *net, int idx) {
     return (idx >= 0 && net->Tc > 0 && net->layers[idx].compact) ? net->Tc : net->T;
 }
+// the conv below the compact layers, evaluated on the compact rows (KfNet.conv_c)
+static inline bool conv_compact(const KfNet *net, int idx) {
+    return net->Tc > 0 && net->conv_c && net->first_c >= 0 && idx >= 0 && idx == net->layers[net->first_c].input;
+}
+// rows a layer's activation holds in the current forward
+static inline int act_rows(const KfNet *net, int idx) {
+    return conv_compact(net, idx) ? net->Tc : rows_of(net, idx);
+}
 // compact row of source row t (nnet_set_row_subsampling), or -1 when t is not in the set
 static inline int compact_of(const KfNet *net, int t) {
     const int T = net->T, nt = net->Tc - net->Tc0;
@@ -1265,7 +1278,7 @@ static int forward_impl(KfNet *net, const void *features, int T) {
         NetLayer &nl = net->layers[li];
         const Layer &L = nl.L;
         const void *x = act_of(net, nl.input);
-        if (net->Tc && (int)li == net->first_c) {  // the conv stack's output on the compact rows
+        if (net->Tc && (int)li == net->first_c && !net->conv_c) {  // the conv stack's output on the compact rows
             if (!ck(kf_gather_rows(net->xc, x, (long long)L.in_dim * 2, T, net->Tc0, net->Tc), "row set gather"))
                 return -1;
             x = net->xc;
@@ -1340,6 +1353,25 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                     E.out8 = nl.a8.q;
                     E.ldo8 = L.fout;
                     E.scale8 = nl.a8.s;
+                }
+                if (conv_compact(net, (int)li)) {
+                    // output frames 3c (c < Tc0), then the tail T-1-3(nt-1) ... T-1 (compact
+                    // rows Tc0 ..): two time-strided launches into compact rows
+                    A.tmul = 3;
+                    A.nrows = net->Tc0 * L.hout;
+                    if (!ck(kf_gemm_fused(net->Tc0 * L.hout, L.fout, K, &A, &B, &E), "conv (compact rows)"))
+                        return -1;
+                    const int nt = net->Tc - net->Tc0;
+                    if (nt > 0) {
+                        const size_t r0 = (size_t)net->Tc0 * L.hout * L.fout;  // elements
+                        A.t0 = T - 1 - 3 * (nt - 1);
+                        A.nrows = nt * L.hout;
+                        E.out = (char *)nl.act + r0 * 2;
+                        E.mask_out = nl.mask + r0 / 8;
+                        if (!ck(kf_gemm_fused(nt * L.hout, L.fout, K, &A, &B, &E), "conv (compact tail rows)"))
+                            return -1;
+                    }
+                    break;
                 }
                 if (!ck(kf_gemm_fused(T * L.hout, L.fout, K, &A, &B, &E), "conv")) return -1;
                 break;
@@ -1490,7 +1522,7 @@ extern "C" const void *nnet_activation(const KfNet *cnet, const char *layer, int
     KfNet *net = const_cast<KfNet *>(cnet);
     for (size_t i = 0; i < net->layers.size(); ++i)
         if (net->layers[i].L.name == layer) {
-            if (rows) *rows = rows_of(net, (int)i);  // compact rows above the conv stack (row subsampling)
+            if (rows) *rows = act_rows(net, (int)i);  // compact rows above the conv stack (row subsampling)
             if (cols) *cols = net->layers[i].L.out_dim;
             return act_of(net, (int)i);
         }
@@ -1712,7 +1744,16 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     for (const auto &r : net->offpath) bridge_gpu_memset(net->grad + r.first, 0, (size_t)r.second * 4);
     (void)n;
     // negative control of the data-parallel tests: exchanging before any producer ran
-    if (net->dp && net->dp_early && !dp_issue(net, dp_next, INT_MAX)) return -1;
+    if (net->dp && net->dp_early) {
+        if (!dp_issue(net, dp_next, INT_MAX)) return -1;
+        // ... and finished before any producer writes (deterministic: left to race with the
+        // backward, a fast one could finish first and hide the early exchange)
+        if (kf_dp_join(net->dp) != 0 ||
+            (two && (kf_event_record(net->ev_side, net->wg_stream) != 0 || kf_stream_wait(mainst, net->ev_side) != 0))) {
+            set_err("backward: early-exchange join");
+            return -1;
+        }
+    }
     to_main();
     const int Tfull = T;
     for (int li = net->chain_out; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
@@ -1724,7 +1765,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         const bool to_full = net->Tc && li == net->first_c;
         const int din = L.in_dim, dout = L.out_dim;
         // (the first compact layer read its input gathered to the compact rows)
-        const void *x = net->Tc && li == net->first_c ? net->xc : act_of(net, nl.input);
+        const void *x = net->Tc && li == net->first_c && !net->conv_c ? net->xc : act_of(net, nl.input);
         bool want_dx = nl.needs_dx && nl.input >= 0;
         void *dz_next = net->dz[flip], *g_next = net->g[flip];
         void *const dbott_buf = (nbott & 1) && two ? net->dbott2 : net->dbott;
@@ -1738,7 +1779,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 set_err("row subsampling: unsupported input gradient into " + pl.L.name);
                 return -1;
             }
-            if (E.mask_in) {
+            if (E.mask_in && !net->conv_c) {  // (a compact conv's mask already is in compact rows)
                 if (!ck(kf_gather_rows(net->mc, pl.mask, w / 8, Tfull, net->Tc0, net->Tc), "row set mask gather"))
                     return -1;
                 E.mask_in = net->mc;
@@ -2042,7 +2083,68 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         set_err("conv " + L.name + ": input gradient of a 1-filter conv not supported");
                         return -1;
                     }
-                    if (L.hsub > 1 && L.hin % L.hsub == 0 && !E.out) {
+                    bool dt3 = noff > 0;  // time offsets exactly {-1, 0, 1}
+                    for (int e = -1; e <= 1 && dt3; ++e) {
+                        bool has = false;
+                        for (int o = 0; o < noff; ++o) has = has || nl.dt[o] == e;
+                        dt3 = has;
+                    }
+                    for (int o = 0; o < noff && dt3; ++o) dt3 = nl.dt[o] >= -1 && nl.dt[o] <= 1;
+                    if (conv_compact(net, li) && dt3 && L.hsub == 1 && E.out2 && !E.out8 && !E.edge_out &&
+                        !E.resid && E.beta == 0.f) {
+                        // the output gradient is non-zero on the compact frames only (net->dzc):
+                        // input frame f = 3c + e receives only the taps with dt = e, from compact
+                        // frame c. One GEMM per residue e over those taps, its rows written to
+                        // frames 3c + e in place (grouped epilogue rows); every nonzero term in
+                        // the full-row kernel's order, so the result is bit-identical. The frames
+                        // the tail reaches (from ws = first tail frame - 1) take the full-row
+                        // kernel on a window of the scattered gradient dz (zero below it).
+                        const int Tc0 = net->Tc0, nt = net->Tc - net->Tc0;
+                        const int ws = nt > 0 ? T - 1 - 3 * (nt - 1) - 1 : T;
+                        const long long fi = (long long)L.hin * L.fin, fo = (long long)L.hout * L.fout;
+                        KfEpilogue Ep = E;
+                        Ep.ldo2 = L.fin;
+                        if (E.out) Ep.ldo = L.fin;
+                        auto at_frame = [&](KfEpilogue &X, long long f) {
+                            X.out2 = (char *)E.out2 + f * fi * 2;
+                            if (E.out) X.out = (char *)E.out + f * fi * 2;
+                            if (E.mask_in) X.mask_in = E.mask_in + f * fi / 8;
+                            if (E.mask_out) X.mask_out = E.mask_out + f * fi / 8;
+                        };
+                        for (int e = -1; e <= 1; ++e) {
+                            const int c_lo = e < 0 ? 1 : 0, c_hi = std::min(Tc0, (ws - 1 - e) / 3 + 1);
+                            if (c_hi <= c_lo) continue;
+                            KfOperand A2 = op_col2im(nl, (const char *)net->dzc + c_lo * fo * 2, c_hi - c_lo);
+                            KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
+                            int np = 0;
+                            for (int o = 0; o < noff; ++o) {
+                                if (nl.dt[o] != e) continue;
+                                A2.dt[np] = 0;
+                                A2.dh[np] = -nl.dh[o];
+                                B2.dt[np] = o * L.fin;
+                                ++np;
+                            }
+                            A2.nparts = B2.nparts = np;
+                            A2.ncols = B2.ncols = np * L.fout;
+                            KfEpilogue Er = Ep;
+                            at_frame(Er, 3LL * c_lo + e);
+                            Er.row_group = L.hin;
+                            Er.row_stride = 3 * L.hin;
+                            if (!ck(kf_gemm_fused((c_hi - c_lo) * L.hin, L.fin, np * L.fout, &A2, &B2, &Er),
+                                    "conv dgrad (compact rows)"))
+                                return -1;
+                        }
+                        if (nt > 0) {
+                            const int tw = T - (ws - 1);
+                            KfOperand A2 = op_col2im(nl, (const char *)dz + (ws - 1) * fo * 2, tw);
+                            KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
+                            KfEpilogue Ew = Ep;
+                            at_frame(Ew, ws - 1);
+                            if (!ck(kf_gemm_fused(tw * L.hin, L.fin, noff * L.fout, &A2, &B2, &Ew),
+                                    "conv dgrad (tail window)"))
+                                return -1;
+                        }
+                    } else if (L.hsub > 1 && L.hin % L.hsub == 0 && !E.out) {
                         // strided conv: input row h' = hsub*j + pi only receives the taps
                         // with (pi - dh) % hsub == 0, so one GEMM per residue pi skips the
                         // (hsub-1)/hsub of the K range the plain col2im reads as zeros
@@ -2246,6 +2348,15 @@ extern "C" int nnet_set_row_subsampling(KfNet *net, int stride) {
     }
     for (int li = 0; li < n; ++li) net->layers[li].compact = li >= first;
     net->first_c = first;
+    {
+        const NetLayer &cl = net->layers[net->layers[first].input];
+        const char *ev = getenv("KF_RSUB_CONV");
+        net->conv_c = cl.L.fin > 1 && !cl.kp && !(ev && ev[0] == '0');
+        for (int li = 0; li < n; ++li)  // first_c must be the conv output's only reader
+            if (li != first && (net->layers[li].input == net->layers[first].input ||
+                                net->layers[li].input2 == net->layers[first].input))
+                net->conv_c = 0;
+    }
     net->rs_nt = nt;
     net->maxTc = maxTc;
     net->rsub = 3;

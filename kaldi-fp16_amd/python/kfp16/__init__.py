@@ -511,7 +511,7 @@ class KfOperand(C.Structure):
                 ("nparts", _i), ("part_width", _i), ("T", _i), ("hout", _i), ("hsrc", _i),
                 ("hmul", _i), ("hdiv", _i), ("tpolicy", _i), ("dt", _i * MAXP), ("dh", _i * MAXP),
                 ("edge_t", _i * MAXP), ("edge_row", _i * MAXP), ("fmt", _i), ("scales", _vp),
-                ("lds", _ll), ("mask", _vp), ("mask_rows", _i)]
+                ("lds", _ll), ("mask", _vp), ("mask_rows", _i), ("tmul", _i), ("t0", _i)]
 
 
 FMT_FP16, FMT_MXFP8 = 0, 1
@@ -522,7 +522,8 @@ class KfEpilogue(C.Structure):
                 ("mask_out", _vp), ("scale", _vp), ("shift", _vp), ("resid", _vp), ("ldr", _ll),
                 ("resid_alpha", _f), ("out2", _vp), ("ldo2", _ll), ("scale2", _vp), ("mask_in", _vp),
                 ("out8", _vp), ("ldo8", _ll), ("scale8", _vp), ("out8_src", _i), ("edge_out", _vp),
-                ("edge_r0", _i), ("edge_r1", _i), ("edge_src", _i)]
+                ("edge_r0", _i), ("edge_r1", _i), ("edge_src", _i),
+                ("row_group", _i), ("row_stride", _i)]
 
 
 def operand(base, ld, rows, cols, kcontig, nparts=1, part_width=None, T=None, hout=1, hsrc=1,

@@ -9,8 +9,9 @@ nnet_set_row_subsampling(3) runs them on that set. Checked here, on the benchmar
 2 egs (T = 3000, T-1 = 2 mod 3: with a tail) and at T = 2998 (T-1 = 0 mod 3: no tail):
 
 - every output row of the set, rows 0 (mod 3), bit-identical to the full forward;
-- the conv stack's activations, masks and every conv weight / bias gradient bit-identical
-  (the gradient into the conv stack is scattered to the same values);
+- the conv stack's activations and every conv weight / bias gradient bit-identical (the
+  gradient into the conv stack is scattered to the same values); cnn6 evaluated on the
+  compact rows only (time-strided conv operand) gives those rows bit-identically;
 - the TDNN-F / prefinal / output weight gradients within 1e-5 (relative Frobenius) of
   the full computation: the same products, summed in another split-K order (fewer rows);
 - the objective's inputs: the supervised output rows equal, so the objective is equal.
@@ -24,13 +25,18 @@ from conftest import rel_fro
 pytestmark = pytest.mark.gpu
 
 
-def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True):
+def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True, conv_rows=True):
+    import os
     from kfp16 import synth
     net = kfp16.Network(xcfg, max_frames=T)
     synth.init_network(net, seed=42)
     net.set_wgrad_stream(two_stream)
     if sub:
-        net.set_row_subsampling(3)
+        os.environ["KF_RSUB_CONV"] = "1" if conv_rows else "0"
+        try:
+            net.set_row_subsampling(3)
+        finally:
+            os.environ.pop("KF_RSUB_CONV", None)
     fb = kfp16.upload_fp16(synth.make_features(T, 40))
     net.forward(fb.ptr, T)
     P = net.layers[-1][3]
@@ -62,13 +68,16 @@ def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True):
     return res
 
 
-@pytest.mark.parametrize("T", [3000, 2998])
-def test_row_subsampled_step_matches_full(gpu, T):
+@pytest.mark.parametrize("T,conv_rows", [(3000, True), (2998, True), (3000, False)])
+def test_row_subsampled_step_matches_full(gpu, T, conv_rows):
+    """conv_rows: cnn6 (the conv below the compact layers) computes only the compact rows
+    (time-strided halo operand, two launches: rows 0 (mod 3) and the tail); else it runs on
+    all rows and tdnnf7 reads its output gathered"""
     kfp16 = gpu
     from kfp16 import synth
     xcfg = synth.load_xconfig("cnn_tdnn_17f.xconfig")
     full = _run(kfp16, xcfg, T, False)
-    sub = _run(kfp16, xcfg, T, True)
+    sub = _run(kfp16, xcfg, T, True, conv_rows=conv_rows)
     tc, tc0, rows = sub["tc"], sub["tc0"], sub["rows"]
     assert tc0 == (T - 1) // 3 + 1
     assert (tc > tc0) == ((T - 1) % 3 != 0)
@@ -77,8 +86,12 @@ def test_row_subsampled_step_matches_full(gpu, T):
     # the supervised rows, through which the objective reads the network
     c_sup = sub["sup"] // 3
     assert np.array_equal(sub["out"][c_sup], full["out"][full["sup"]])
-    # conv stack untouched (full rows), first compact layer on gathered rows
-    assert np.array_equal(sub["acts"]["cnn6"], full["acts"]["cnn6"])
+    # the conv stack: cnn6 on the compact rows (or all rows), the same sums in the same order
+    if conv_rows:
+        assert sub["acts"]["cnn6"].shape[0] == tc
+        assert np.array_equal(sub["acts"]["cnn6"].view(np.uint16), full["acts"]["cnn6"][rows].view(np.uint16))
+    else:
+        assert np.array_equal(sub["acts"]["cnn6"], full["acts"]["cnn6"])
     for name in ("tdnnf7", "tdnnf23", "prefinal-chain"):
         assert np.array_equal(sub["acts"][name][:tc0].view(np.uint16), full["acts"][name][rows[:tc0]].view(np.uint16)), name
     for k, v in full["grads"].items():
