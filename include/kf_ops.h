@@ -237,6 +237,8 @@ int kf_f32_to_f16_flat(const float *src, void *dst, long long n);
  * compact row of src whose source row is t, or zeros */
 int kf_gather_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc);
 int kf_scatter_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc);
+/* kf_scatter_rows for the full rows r0 .. T-1 only, dst row 0 = full row r0 */
+int kf_scatter_rows_from(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc, int r0);
 /* edge[c] = rne(sum over rows[0..n) in that order of src[rows[i] * ld + c]), n <= 4 (host array) */
 int kf_rows_sum_list(void *edge, const void *src, long long ld, const int *rows, int n, int cols);
 const char *kf_layers_last_error(void);

@@ -60,6 +60,7 @@ struct WHalo {
     const h16 *x;        // source [T x hsrc x fin] (row = frame, ld elements)
     long long ld;
     int T, hout, hmul, hsrc, fin, pad, hpe, hpos, nf, dtmin;
+    int ts, toff;        // output frame t reads source frames ts * t + toff + dt (KfOperand.tmul / t0)
     int rows, npieces, halo_bytes;
     int hpw;             // halo pieces issued per wave per K-step (ceil(npieces / waves))
     unsigned inv_hout;   // ceil(2^16 / hout): exact x / hout for x * hout < 2^16
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wgrad_halo_kernel(OpD B,
     const unsigned ldb = (unsigned)(H.ld * 2);
     auto halo_issue = [&](int ks, int img) {
         char *dst = dsm + img * H.halo_bytes;
-        const int tb = (ks * BK) / H.hout + H.dtmin;
+        const int tb = H.ts * ((ks * BK) / H.hout) + H.toff + H.dtmin;
         static_for<HPW_MAX>([&](auto I) {
             constexpr int i = decltype(I)::value;
             if (i < H.hpw) {
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_wgrad_halo_kernel(OpD B,
             static_for<2>([&](auto HI) {
                 const int x = r0 + 32 * S + 8 * g + q4 + 4 * HI;
                 const int df = (int)(((unsigned)x * H.inv_hout) >> 16);
-                base[S][HI] = df * H.hpos + (x - df * H.hout);
+                base[S][HI] = H.ts * df * H.hpos + (x - df * H.hout);
             });
         });
         static_for<BK / 32>([&](auto S) {
@@ -291,8 +292,11 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     H.hpe = (HP + a.hmul - 1) / a.hmul;
     H.hpos = H.hpe * a.hmul;
     H.dtmin = dtmin;
-    // frames a 64-row K-step touches (its first row's frame + the rows' span) + the time taps
-    H.nf = (BK - 1 + a.hout - 1) / a.hout + 1 + (dtmax - dtmin);
+    H.ts = a.tmul;
+    H.toff = a.t0;
+    // frames a 64-row K-step touches (its first row's frame + the rows' span, ts apart) + the
+    // time taps
+    H.nf = H.ts * ((BK - 1 + a.hout - 1) / a.hout) + 1 + (dtmax - dtmin);
     H.rows = H.nf * H.hpos;
     H.npieces = (H.rows + 7) / 8;
     H.halo_bytes = H.npieces * 1024;

@@ -1631,8 +1631,8 @@ static int wgrad_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     if (M <= 0 || N <= 0) return 0;
     OpD a, b;
     if (!to_dev(*A, a, "A") || !to_dev(*B, b, "B")) return -1;
-    if (a.tmul > 1 || a.t0 || b.tmul > 1 || b.t0) {
-        kf_set_error("kf_gemm_wgrad: time-strided rows (tmul / t0) are a conv forward operand only");
+    if (b.tmul > 1 || b.t0) {
+        kf_set_error("kf_gemm_wgrad: time-strided rows (tmul / t0) only on the conv im2col operand A");
         return -1;
     }
     if (A->kcontig || B->kcontig) {
@@ -1648,6 +1648,10 @@ static int wgrad_impl(int M, int N, int K, const KfOperand *A, const KfOperand *
     if (!b.mk) {
         const int hr = kf_conv_wgrad_halo_try(M, N, K, a, b, dW, ldw, bias_grad, accumulate);
         if (hr != 0) return hr < 0 ? -1 : 0;
+    }
+    if (a.tmul > 1 || a.t0) {
+        kf_set_error("kf_gemm_wgrad: time-strided rows (tmul / t0) need a 3x3 conv on the halo kernel");
+        return -1;
     }
     // tiles: 384x160 for N = 160 / 320 (TDNN-F linear); otherwise 64-, 128- or 256-column
     // tiles whose row count (192, 256 or 320) wastes the fewest padded rows of M

@@ -386,12 +386,13 @@ __global__ __launch_bounds__(256) void k_gather_rows(uint4 *dst, const uint4 *sr
     }
 }
 // full rows t < T: the compact row whose source row t is, else zero
+// (rows r0 .. T - 1 only, dst row 0 = full row r0)
 __global__ __launch_bounds__(256) void k_scatter_rows(uint4 *dst, const uint4 *src, long long vpr, int T, int tc0,
-                                                      int tc) {
-    const long long n = (long long)T * vpr;
+                                                      int tc, int r0) {
+    const long long n = (long long)(T - r0) * vpr;
     const int nt = tc - tc0, rt = (T - 1) % 3;
     for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-        const long long t = i / vpr, v = i - t * vpr;
+        const long long t = r0 + i / vpr, v = i % vpr;
         long long c = -1;
         if (t % 3 == 0 && t / 3 < tc0) c = t / 3;
         else if (nt > 0 && t % 3 == rt && t >= (long long)(T - 1) - 3LL * (nt - 1)) c = tc - 1 - ((T - 1) - t) / 3;
@@ -423,16 +424,20 @@ int kf_gather_rows(void *dst, const void *src, long long row_bytes, int T, int t
                                                                                     vpr, T, tc0, tc);
     return lay_check("gather_rows");
 }
-int kf_scatter_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc) {
+int kf_scatter_rows_from(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc, int r0) {
     kf_take_pending(__func__);
-    if (row_bytes <= 0 || row_bytes % 16 || tc0 < 0 || tc < tc0 || T <= 0 || 3LL * (tc0 - 1) > T - 1) {
-        lay_set_error("scatter_rows: bad geometry (row_bytes %lld T %d tc0 %d tc %d)", row_bytes, T, tc0, tc);
+    if (row_bytes <= 0 || row_bytes % 16 || tc0 < 0 || tc < tc0 || T <= 0 || 3LL * (tc0 - 1) > T - 1 || r0 < 0 ||
+        r0 >= T) {
+        lay_set_error("scatter_rows: bad geometry (row_bytes %lld T %d tc0 %d tc %d r0 %d)", row_bytes, T, tc0, tc, r0);
         return -1;
     }
     const long long vpr = row_bytes / 16;
-    k_scatter_rows<<<kf_blocks((long long)T * vpr, 256, 16384), 256, 0, kf_stream()>>>((uint4 *)dst, (const uint4 *)src,
-                                                                                     vpr, T, tc0, tc);
+    k_scatter_rows<<<kf_blocks((long long)(T - r0) * vpr, 256, 16384), 256, 0, kf_stream()>>>(
+        (uint4 *)dst, (const uint4 *)src, vpr, T, tc0, tc, r0);
     return lay_check("scatter_rows");
+}
+int kf_scatter_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc) {
+    return kf_scatter_rows_from(dst, src, row_bytes, T, tc0, tc, 0);
 }
 int kf_rows_sum_list(void *edge, const void *src, long long ld, const int *rows, int n, int cols) {
     kf_take_pending(__func__);

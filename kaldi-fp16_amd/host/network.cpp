@@ -13,6 +13,7 @@
 //     fp32 gradient / fp32 velocity allocation, so the optimiser is one launch
 //     and the data-parallel gradient exchange is one contiguous buffer.
 // Memory comes from the bridge_* ABI, as the Go layer does (internal/gpu/tensor.go).
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -2067,6 +2068,29 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                                       "conv c1 wgrad");
                         }))
                         return -1;
+                } else if (conv_compact(net, li)) {
+                    // output gradient on the compact rows only (net->dzc): the reduction over
+                    // output frames 3c (c < Tc0), then over the tail frames, added
+                    const int nt = net->Tc - net->Tc0;
+                    KfOperand A = op_im2col(nl, x, T, 0);
+                    A.tmul = 3;
+                    A.nrows = net->Tc0 * L.hout;
+                    KfOperand B = op_base(net->dzc, L.fout, net->Tc0 * L.hout, L.fout, 0);
+                    KfOperand At = A, Bt = B;
+                    At.t0 = T - 1 - 3 * (nt - 1);
+                    At.nrows = nt * L.hout;
+                    Bt.base = (const char *)net->dzc + (size_t)net->Tc0 * L.hout * L.fout * 2;
+                    Bt.nrows = Bt.T = nt * L.hout;
+                    if (!wgrad([&] {
+                            return ck(kf_gemm_wgrad(noff * L.fin, L.fout, net->Tc0 * L.hout, &A, &B, gptr(net, nl.pW),
+                                                    L.fout, gptr(net, nl.pb), 0),
+                                      "conv wgrad (compact rows)") &&
+                                   (nt == 0 ||
+                                    ck(kf_gemm_wgrad(noff * L.fin, L.fout, nt * L.hout, &At, &Bt, gptr(net, nl.pW),
+                                                     L.fout, gptr(net, nl.pb), 1),
+                                       "conv wgrad (compact tail rows)"));
+                        }))
+                        return -1;
                 } else {
                     KfOperand A = op_im2col(nl, x, T, 0);
                     KfOperand B = op_base(dz, L.fout, T * L.hout, L.fout, 0);
@@ -2083,15 +2107,11 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         set_err("conv " + L.name + ": input gradient of a 1-filter conv not supported");
                         return -1;
                     }
-                    bool dt3 = noff > 0;  // time offsets exactly {-1, 0, 1}
-                    for (int e = -1; e <= 1 && dt3; ++e) {
-                        bool has = false;
-                        for (int o = 0; o < noff; ++o) has = has || nl.dt[o] == e;
-                        dt3 = has;
-                    }
-                    for (int o = 0; o < noff && dt3; ++o) dt3 = nl.dt[o] >= -1 && nl.dt[o] <= 1;
-                    if (conv_compact(net, li) && dt3 && L.hsub == 1 && E.out2 && !E.out8 && !E.edge_out &&
-                        !E.resid && E.beta == 0.f) {
+                    if (conv_compact(net, li)) {
+                        if (!E.out2 || E.out8 || E.edge_out || E.resid || E.beta != 0.f) {
+                            set_err("row subsampling: unsupported input gradient of " + L.name);
+                            return -1;
+                        }
                         // the output gradient is non-zero on the compact frames only (net->dzc):
                         // input frame f = 3c + e receives only the taps with dt = e, from compact
                         // frame c. One GEMM per residue e over those taps, its rows written to
@@ -2251,8 +2271,19 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         }
         if (want_dx && to_full) {
             const int w = net->layers[nl.input].L.out_dim;
-            if (!ck(kf_scatter_rows(dz_next, net->dzc, (long long)w * 2, Tfull, net->Tc0, net->Tc), "row set scatter"))
+            if (net->conv_c) {
+                // the conv below reads the compact rows (net->dzc); only its tail window
+                // (full rows from ws - 1, conv_dx_window) takes the scattered form
+                const int nt = net->Tc - net->Tc0;
+                const int r0 = Tfull - 1 - 3 * (nt - 1) - 2;
+                if (nt > 0 && !ck(kf_scatter_rows_from((char *)dz_next + (size_t)r0 * w * 2, net->dzc,
+                                                       (long long)w * 2, Tfull, net->Tc0, net->Tc, r0),
+                                  "row set scatter (tail window)"))
+                    return -1;
+            } else if (!ck(kf_scatter_rows(dz_next, net->dzc, (long long)w * 2, Tfull, net->Tc0, net->Tc),
+                           "row set scatter")) {
                 return -1;
+            }
         }
         // gradient buckets complete at this step go to the communication stream (their
         // gates on side, behind the step's weight gradients)
@@ -2351,7 +2382,12 @@ extern "C" int nnet_set_row_subsampling(KfNet *net, int stride) {
     {
         const NetLayer &cl = net->layers[net->layers[first].input];
         const char *ev = getenv("KF_RSUB_CONV");
-        net->conv_c = cl.L.fin > 1 && !cl.kp && !(ev && ev[0] == '0');
+        // time offsets exactly {-1, 0, 1} and no height subsampling: the input gradient's
+        // per-residue GEMMs (backward) cover every input frame
+        bool dt3 = !cl.dt.empty();
+        for (int e = -1; e <= 1 && dt3; ++e) dt3 = std::find(cl.dt.begin(), cl.dt.end(), e) != cl.dt.end();
+        for (int d : cl.dt) dt3 = dt3 && d >= -1 && d <= 1;
+        net->conv_c = cl.L.fin > 1 && !cl.kp && cl.L.hsub == 1 && dt3 && !(ev && ev[0] == '0');
         for (int li = 0; li < n; ++li)  // first_c must be the conv output's only reader
             if (li != first && (net->layers[li].input == net->layers[first].input ||
                                 net->layers[li].input2 == net->layers[first].input))

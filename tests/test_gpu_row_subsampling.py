@@ -12,8 +12,9 @@ nnet_set_row_subsampling(3) runs them on that set. Checked here, on the benchmar
 - the conv stack's activations and every conv weight / bias gradient bit-identical (the
   gradient into the conv stack is scattered to the same values); cnn6 evaluated on the
   compact rows only (time-strided conv operand) gives those rows bit-identically;
-- the TDNN-F / prefinal / output weight gradients within 1e-5 (relative Frobenius) of
-  the full computation: the same products, summed in another split-K order (fewer rows);
+- the TDNN-F / prefinal / output weight gradients (and cnn6's when it runs on the compact
+  rows) within 1e-5 (relative Frobenius) of the full computation: the same products, summed
+  in another split-K order (fewer rows);
 - the objective's inputs: the supervised output rows equal, so the objective is equal.
 """
 import numpy as np
@@ -96,7 +97,7 @@ def test_row_subsampled_step_matches_full(gpu, T, conv_rows):
         assert np.array_equal(sub["acts"][name][:tc0].view(np.uint16), full["acts"][name][rows[:tc0]].view(np.uint16)), name
     for k, v in full["grads"].items():
         w = sub["grads"][k]
-        if k.startswith(("cnn", "idct")):
+        if k.startswith(("cnn", "idct")) and not (conv_rows and k.startswith("cnn6")):
             assert np.array_equal(w, v), k
         else:
             assert rel_fro(w, v) <= 1e-5, (k, rel_fro(w, v))
