@@ -209,14 +209,17 @@ struct KfNet {
     std::vector<ParamRef> params;
     float *master = nullptr, *grad = nullptr, *vel = nullptr;
     void *w16 = nullptr;
-    void *dz[2] = {nullptr, nullptr}, *g[2] = {nullptr, nullptr};
+    // input-gradient ring (three deep: a step's output gradient is not rewritten until the
+    // weight gradients of the step after next have read it)
+    void *dz[3] = {nullptr, nullptr, nullptr}, *g[3] = {nullptr, nullptr, nullptr};
     void *dbott = nullptr, *edge = nullptr;
     // Weight gradients run on their own stream (nnet_set_wgrad_stream, default on): a layer's
     // dW GEMMs hang off the input-gradient chain (dz -> dbott -> dz below) and overlap it.
-    // dbott alternates between two buffers by backward step, so the next layer's affine
-    // input gradient never waits for this layer's linear weight gradient.
-    void *dbott2 = nullptr;
+    // dbott cycles through three buffers by backward step, so the next layers' affine input
+    // gradients never wait for this layer's linear weight gradient.
+    void *dbott2 = nullptr, *dbott3 = nullptr;
     void *wg_stream = nullptr, *ev_go = nullptr, *ev_side = nullptr;
+    void *ev_step[3] = {nullptr, nullptr, nullptr};  // end of a backward step's side work (ring)
     void *hp_stream = nullptr;  // high-priority stream for the input-gradient chain
     int wg_side = 1;
     // Implicit dz (nnet_set_implicit_dz, default off, fp16 step): the input-gradient epilogue
@@ -254,9 +257,13 @@ struct KfNet {
     void *xc = nullptr;            // first_c's input, gathered to compact rows
     void *dzc = nullptr;           // first_c's input gradient in compact rows
     uint8_t *mc = nullptr;         // the mask of first_c's input, compact rows
+    // bottleneck-gradient row mask [maxTc x rm_bn bits]: all ones but the scratch row Tc0
+    // (the TDNN-F affine input gradient zeroes that row in its epilogue)
+    uint8_t *rowmask = nullptr;
+    int rm_bn = 0, rm_tc0 = -1, rm_tc = -1;
     long long stall_side = 0;      // nnet_debug_backward (tests): spin before side work
-    bool dz_imp[2] = {false, false};  // dz[i] was left implicit by the producing epilogue
-    bool dz_edge[2] = {false, false}; // row T of dz[i] already holds the strided TDNN-F edge sum
+    bool dz_imp[3] = {false, false, false};  // dz[i] was left implicit by the producing epilogue
+    bool dz_edge[3] = {false, false, false}; // row T of dz[i] already holds the strided TDNN-F edge sum
     void *w2s = nullptr;              // [kaff x dout] fp16: W2 with the BN scale folded in
     void *dbott_last = nullptr;  // the dbott buffer of the last TDNN-F / prefinal step (tests)
     size_t edge_half = 0;
@@ -264,8 +271,8 @@ struct KfNet {
     int fp8_dgrad = 1;  // nnet_set_fp8(net, 2): MXFP8 forward, fp16 affine input gradients (tests)
     // MXFP8 copies of dz[0] / dz[1] written by the producing input-gradient epilogue
     // (out8_src = 1) for a TDNN-F layer's affine input gradient, and the layer each holds
-    Mx dz8[2];
-    int dz8_layer[2] = {-1, -1};
+    Mx dz8[3];
+    int dz8_layer[3] = {-1, -1, -1};
     bool wt_dirty = true;  // the transposed weight copies need a refresh (NetLayer::wt)
     // data parallel (kf_dp.h): gradient buckets exchanged during the backward
     KfDp *dp = nullptr;
@@ -283,6 +290,7 @@ struct KfNet {
         if (wg_stream) bridge_gpu_sync();
         kf_event_free(ev_go);
         kf_event_free(ev_side);
+        for (void *e : ev_step) kf_event_free(e);
         kf_stream_free(wg_stream);
         kf_stream_free(hp_stream);
         for (void *p : allocs) bridge_gpu_free(p);
@@ -781,12 +789,13 @@ static bool alloc_device(KfNet *net, int max_frames) {
         nl.wt_N = N;
     }
     // gradient buffers carry two spare rows for the splice-transpose edge sums
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < 3; ++i) {
         net->dz[i] = net->dalloc((T + 2) * maxw * 2);
         net->g[i] = net->dalloc((T + 2) * maxw * 2);
     }
     net->dbott = net->dalloc((T + 2) * maxw * 2);
     net->dbott2 = net->dalloc((T + 2) * maxw * 2);
+    net->dbott3 = net->dalloc((T + 2) * maxw * 2);
     {
         size_t w2 = 0;
         for (auto &nl : net->layers)
@@ -800,7 +809,8 @@ static bool alloc_device(KfNet *net, int max_frames) {
     }
     net->edge_half = align_up(maxw * 2, 256);
     net->edge = net->dalloc(net->edge_half * 2);
-    if (!net->dz[0] || !net->dz[1] || !net->g[0] || !net->g[1] || !net->dbott || !net->dbott2 || !net->edge) {
+    if (!net->dz[0] || !net->dz[1] || !net->dz[2] || !net->g[0] || !net->g[1] || !net->g[2] || !net->dbott ||
+        !net->dbott2 || !net->dbott3 || !net->edge) {
         set_err("alloc backward scratch");
         return false;
     }
@@ -808,7 +818,8 @@ static bool alloc_device(KfNet *net, int max_frames) {
     net->hp_stream = kf_stream_new_high();
     net->ev_go = kf_event_new();
     net->ev_side = kf_event_new();
-    if (!net->wg_stream || !net->ev_go || !net->ev_side) {
+    for (auto &e : net->ev_step) e = kf_event_new();
+    if (!net->wg_stream || !net->ev_go || !net->ev_side || !net->ev_step[0] || !net->ev_step[1] || !net->ev_step[2]) {
         set_err("create the weight-gradient stream");
         return false;
     }
@@ -1171,7 +1182,7 @@ extern "C" int nnet_set_fp8(KfNet *net, int on) {
         int dzw = 0;
         for (auto &nl : net->layers)
             if (nl.L.type == LayerType::TDNNF && nl.L.time_stride > 0) dzw = std::max(dzw, nl.L.out_dim);
-        for (int i = 0; first && dzw > 0 && i < 2; ++i)
+        for (int i = 0; first && dzw > 0 && i < 3; ++i)
             if (!mx_alloc(net, net->dz8[i], T, dzw)) {
                 set_err("fp8: alloc dz copies");
                 return -1;
@@ -1385,6 +1396,16 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 const Mx *x8 = in8(net, nl);
                 KfOperand A = x8 ? op_mx(*x8, T, np, -s, 0)
                                  : s > 0 ? op_splice(x, T, din, -s, 0, KF_CLAMP, 1) : op_base(x, din, T, din, 1);
+                // compact rows with a tail: row Tc0 - 1's +1 neighbour in the affine splice is row
+                // T-1 (the tail's last row). The scratch row Tc0 reads the last row's linear inputs
+                // [x(Tc-1-s) | x(Tc-1)] (edge rows), so its bottleneck is that row's, bit for bit
+                // (nnet_set_row_subsampling)
+                const bool scratch = nl.compact && net->Tc > net->Tc0 && s > 0;
+                if (scratch && !x8) {
+                    A.edge_t[0] = A.edge_t[1] = net->Tc0;
+                    A.edge_row[0] = std::max(0, net->Tc - 1 - s);
+                    A.edge_row[1] = net->Tc - 1;
+                }
                 KfOperand B = x8 ? op_mxw(nl.w8, bn) : op_base(wptr(net, nl.pW), bn, klin, bn, 0);
                 KfEpilogue E = epi0();
                 E.out = nl.aux;
@@ -1394,9 +1415,7 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                 // force 256x256 tiles onto N = bottleneck (320 of 512 columns used) instead of
                 // 384x160 (3072 model: 331 -> see DESIGN §7)
                 if (!ck(kf_gemm_fused(T, bn, x8 ? nl.w8.ld : klin, &A, &B, &E), "tdnnf linear")) return -1;
-                // compact rows with a tail: row Tc0 - 1's +1 neighbour is row T-1 (the tail's
-                // last row); its copy goes to the scratch row Tc0 (nnet_set_row_subsampling)
-                if (nl.compact && net->Tc > net->Tc0 && s > 0 &&
+                if (scratch && x8 &&
                     !ck(ops_copy((char *)nl.aux + (size_t)net->Tc0 * bn * 2,
                                  (const char *)nl.aux + (size_t)(net->Tc - 1) * bn * 2, bn),
                         "row set edge copy"))
@@ -1536,6 +1555,13 @@ extern "C" const void *nnet_activation(const KfNet *cnet, const char *layer, int
 // ---------------------------------------------------------------------------
 namespace {
 
+// ring index of an input-gradient buffer, or -1
+int dz_index(const KfNet *net, const void *p) {
+    for (int i = 0; i < 3; ++i)
+        if (p == net->dz[i]) return i;
+    return -1;
+}
+
 // Epilogue of an input-gradient GEMM that produces the gradient of layer P
 // (the input of the layer being back-propagated). v = acc (+ bypass * g_cur):
 //   g_P = rne(v) when P itself has a bypass (its own input gradient needs it)
@@ -1547,7 +1573,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
     const int w = L.out_dim;
     E.ldo2 = w;
     E.out2 = dz_out;
-    const int di = dz_out == net->dz[0] ? 0 : dz_out == net->dz[1] ? 1 : -1;
+    const int di = dz_index(net, dz_out);
     if (di >= 0) net->dz_imp[di] = net->dz_edge[di] = false;
     switch (L.type) {
         case LayerType::TDNNF: {
@@ -1580,7 +1606,7 @@ bool dx_epilogue(KfNet *net, int P, void *dz_out, void *g_out, KfEpilogue &E) {
             // MXFP8 train step: also the e4m3 copy of dz_P for P's affine input gradient; only
             // when the copy's row is exactly w wide (w % 128 == 0), so the dgrad GEMM's K range
             // holds no stale codes from a wider layer's copy
-            const int i = dz_out == net->dz[0] ? 0 : dz_out == net->dz[1] ? 1 : -1;
+            const int i = dz_index(net, dz_out);
             if (net->fp8 && net->fp8_dgrad && i >= 0 && w % 128 == 0 && pl.w8d.q && net->dz8[i].q &&
                 net->dz8[i].ld == w) {
                 E.out8 = net->dz8[i].q;
@@ -1673,9 +1699,9 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     // Two streams: the input-gradient chain on the caller's stream (main), every write into
     // the gradient buffer on the weight-gradient stream (side), which waits for main at each
     // wgrad(): the dW GEMMs of a layer overlap the input gradients below it. Hazards (WAR on
-    // shared scratch) are ordered by events: main waits for all of the previous step's side
-    // work before it overwrites the dz / g ping-pong buffer that work read (dx_wait), and
-    // dbott alternates between two buffers. All gradient writes (and so the data-parallel
+    // shared scratch) are ordered by events: the dz / g / dbott buffers cycle three deep and
+    // main waits for a step's side work before it overwrites what that work read (dx_wait,
+    // side_wait). All gradient writes (and so the data-parallel
     // bucket gates, dp_issue) are on side; main joins side before returning.
     void *const caller = kf_get_stream();
     void *mainst = caller;
@@ -1720,25 +1746,30 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         return true;
     };
     auto to_main = [&]() { kf_set_stream(mainst); };
-    bool side_pending = false;  // side work of the previous step that main has not waited for
-    auto dx_wait = [&]() -> bool {  // main waits for the previous step's side work
-        if (!two || !side_pending) return true;
-        if (kf_stream_wait(mainst, net->ev_side) != 0) {
+    // Steps (layers that hand a gradient down) cycle through three dz / g / dbott buffers.
+    // Before step i rewrites its dz / g buffers, main waits for the side work of step i - 2,
+    // the last reader of what step i - 3 wrote there; before it rewrites its dbott buffer
+    // (earlier in the step), for that of step i - 3. Step i - 1's side work keeps running.
+    // The side stream is in order, so waiting for step j's event covers every step <= j.
+    int stepi = 0, waited = -1;  // side work of steps <= waited: main has waited for it
+    auto side_wait = [&](int upto) -> bool {
+        if (!two || upto <= waited || upto < 0) return true;
+        if (kf_stream_wait(mainst, net->ev_step[upto % 3]) != 0) {
             set_err("backward: weight-gradient stream join");
             return false;
         }
-        side_pending = false;
+        waited = upto;
         return true;
     };
+    auto dx_wait = [&]() -> bool { return side_wait(stepi - 2); };
+    auto joined = [&]() { waited = stepi - 1; };
     // the top layer must be the chain output
     const void *dz = out_grad;  // gradient w.r.t. pre-activation of the current layer
     const void *gcur = out_grad;  // stored gradient w.r.t. the current layer's output
     int flip = 0, done = 0;
-    // dbott alternates by TDNN-F / prefinal step (the steps that write it), not by layer:
-    // step k's affine input gradient writes its buffer before this step's dx_wait, which is
-    // safe because the previous dbott step (k - 1, other buffer) waited for the side work of
-    // step k - 2 (this buffer's readers). A pass-through step in between (Batchnorm) must not
-    // advance the parity, or k would reuse k - 1's buffer while its weight gradient reads it.
+    // dbott cycles by TDNN-F / prefinal step (the steps that write it), not by layer: a
+    // pass-through step in between (Batchnorm) must not advance it, or the next step would
+    // reuse a buffer whose weight gradient may still read it (side_wait covers step i - 3).
     int nbott = 0;
     size_t dp_next = 0;
     if (!to_side()) return -1;
@@ -1756,6 +1787,24 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         }
     }
     to_main();
+    // the bottleneck-gradient row mask of this row set (rebuilt when the set changes, on the
+    // chain stream, which reads it): every 3-strided compact TDNN-F layer of one bottleneck
+    // width zeroes the scratch row through it
+    if (net->Tc > net->Tc0 && net->rowmask) {
+        int bn = 0;
+        for (size_t li = net->first_c; li < net->layers.size(); ++li) {
+            const Layer &q = net->layers[li].L;
+            if (q.type != LayerType::TDNNF || q.time_stride == 0) continue;
+            bn = bn == 0 || bn == q.bottleneck ? q.bottleneck : -1;
+        }
+        if (bn > 0 && bn % 8 == 0 && (net->rm_bn != bn || net->rm_tc0 != net->Tc0 || net->rm_tc != net->Tc)) {
+            bridge_gpu_memset(net->rowmask, 0xFF, (size_t)net->Tc * bn / 8);
+            bridge_gpu_memset(net->rowmask + (size_t)net->Tc0 * bn / 8, 0, (size_t)bn / 8);
+            net->rm_bn = bn;
+            net->rm_tc0 = net->Tc0;
+            net->rm_tc = net->Tc;
+        }
+    }
     const int Tfull = T;
     for (int li = net->chain_out; li >= 0 && done < max_layers; li = net->layers[li].input, ++done) {
         NetLayer &nl = net->layers[li];
@@ -1769,7 +1818,9 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         const void *x = net->Tc && li == net->first_c && !net->conv_c ? net->xc : act_of(net, nl.input);
         bool want_dx = nl.needs_dx && nl.input >= 0;
         void *dz_next = net->dz[flip], *g_next = net->g[flip];
-        void *const dbott_buf = (nbott & 1) && two ? net->dbott2 : net->dbott;
+        // (this step's dbott buffer was last written at step i - 3 or earlier)
+        void *const dbott_buf = !two ? net->dbott : nbott % 3 == 0 ? net->dbott : nbott % 3 == 1 ? net->dbott2 : net->dbott3;
+        if (!side_wait(stepi - 3)) return -1;
         net->dz8_layer[flip] = -1;
         KfEpilogue E;
         if (want_dx && !dx_epilogue(net, nl.input, dz_next, g_next, E)) return -1;
@@ -1878,7 +1929,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 const int klin = s > 0 ? 2 * din : din, kaff = s > 0 ? 2 * bn : bn;
                 // implicit dz (dx_epilogue): the layer's g read through its ReLU mask, the BN
                 // scale applied to the weight gradient's columns and folded into W2 below
-                const int ib = dz == net->dz[0] ? 0 : dz == net->dz[1] ? 1 : -1;
+                const int ib = dz_index(net, dz);
                 const bool imp = ib >= 0 && net->dz_imp[ib];
                 const void *dzs = imp ? gcur : dz;
                 auto masked = [&](KfOperand o) {
@@ -1922,15 +1973,27 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                 KfEpilogue E1 = epi0();
                 E1.out = dbott;
                 E1.ldo = bn;
+                // compact rows with a tail: the scratch row Tc0 read row Tc0 - 1's gradient
+                // through the +1 adjacency; its true gradient is zero (written as zero through
+                // the row mask)
+                bool zero_scratch = nl.compact && net->Tc > net->Tc0 && s > 0;
+                if (zero_scratch && net->rowmask && net->rm_bn == bn && net->rm_tc0 == net->Tc0 &&
+                    net->rm_tc == net->Tc) {
+                    E1.out = nullptr;
+                    E1.out2 = dbott;
+                    E1.ldo2 = bn;
+                    E1.mask_in = net->rowmask;
+                    zero_scratch = false;
+                }
                 if (s > 0 && want_dx) {
                     // the linear input gradient's edge row (row T of dbott: sum of rows 0 .. s),
                     // summed by this GEMM's first row tile
                     E1.edge_out = (char *)dbott + (size_t)T * bn * 2;
                     E1.edge_r0 = 0;
                     E1.edge_r1 = s + 1 < T ? s + 1 : T;
-                    E1.edge_src = 0;
+                    E1.edge_src = E1.out2 ? 1 : 0;
                 }
-                const int i8 = dz == net->dz[0] ? 0 : dz == net->dz[1] ? 1 : -1;
+                const int i8 = dz_index(net, dz);
                 if (s > 0) {
                     // spare row T of dz (of g when dz is implicit: the masked sum) holds
                     // sum_{t >= T-1-s} dz[t] (clamped-splice transpose)
@@ -1979,9 +2042,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         A1.edge_row[1] = T;
                         if (!ck(kf_gemm_fused(T, bn, 2 * dout, &A1, &B1, &E1), "tdnnf affine dgrad"))
                             return -1;
-                        // compact rows: the scratch row Tc0 read row Tc0 - 1's gradient through
-                        // the +1 adjacency; its true gradient is zero
-                        if (nl.compact && net->Tc > net->Tc0)
+                        if (zero_scratch)  // (no row mask for this bottleneck width)
                             bridge_gpu_memset((char *)dbott + (size_t)net->Tc0 * bn * 2, 0, (size_t)bn * 2);
                     }
                 } else {
@@ -2042,7 +2103,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                             set_err("backward: weight-gradient stream join");
                             return -1;
                         }
-                        side_pending = false;
+                        joined();
                         if (E.out || E.mask_in || E.scale2 || !E.out2) {
                             set_err("conv " + L.name + ": small-fin input gradient only into combine-feature-maps");
                             return -1;
@@ -2290,17 +2351,17 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         if (two) kf_set_stream(net->wg_stream);
         if (net->dp && !dp_issue(net, dp_next, done)) return -1;
         if (two) {
-            if (kf_event_record(net->ev_side, net->wg_stream) != 0) {
+            if (kf_event_record(net->ev_step[stepi % 3], net->wg_stream) != 0) {
                 set_err("backward: weight-gradient stream event");
                 return -1;
             }
-            side_pending = true;
         }
         to_main();
         if (!want_dx) break;  // nothing trainable below
         dz = dz_next;
         gcur = g_next;
-        flip ^= 1;
+        ++stepi;
+        flip = stepi % 3;
     }
     // the rest of the buckets, then main waits for side (SGD reads every gradient) and for
     // every bucket
@@ -2372,6 +2433,12 @@ extern "C" int nnet_set_row_subsampling(KfNet *net, int stride) {
         net->xc = net->dalloc((size_t)maxTc * din * 2);
         net->dzc = net->dalloc((size_t)(maxTc + 2) * din * 2);
         net->mc = (uint8_t *)net->dalloc(align_up((size_t)maxTc * din / 8 + 16, 256));
+        int maxbn = 0;
+        for (int li = first; li < n; ++li)
+            if (net->layers[li].L.type == LayerType::TDNNF) maxbn = std::max(maxbn, net->layers[li].L.bottleneck);
+        net->rowmask = maxbn ? (uint8_t *)net->dalloc(align_up((size_t)maxTc * maxbn / 8 + 16, 256)) : nullptr;
+        net->rm_bn = 0;
+        net->rm_tc0 = net->rm_tc = -1;
         if (!net->xc || !net->dzc || !net->mc) {
             set_err("set_row_subsampling: alloc compact buffers");
             return -1;
