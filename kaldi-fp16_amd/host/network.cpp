@@ -220,6 +220,7 @@ struct KfNet {
     void *dbott2 = nullptr, *dbott3 = nullptr;
     void *wg_stream = nullptr, *ev_go = nullptr, *ev_side = nullptr;
     void *ev_step[3] = {nullptr, nullptr, nullptr};  // end of a backward step's side work (ring)
+    void *ev_aux = nullptr;  // side-stream launches main joins on the spot (conv tail rows / window)
     void *hp_stream = nullptr;  // high-priority stream for the input-gradient chain
     int wg_side = 1;
     // Implicit dz (nnet_set_implicit_dz, default off, fp16 step): the input-gradient epilogue
@@ -291,6 +292,7 @@ struct KfNet {
         kf_event_free(ev_go);
         kf_event_free(ev_side);
         for (void *e : ev_step) kf_event_free(e);
+        kf_event_free(ev_aux);
         kf_stream_free(wg_stream);
         kf_stream_free(hp_stream);
         for (void *p : allocs) bridge_gpu_free(p);
@@ -819,7 +821,9 @@ static bool alloc_device(KfNet *net, int max_frames) {
     net->ev_go = kf_event_new();
     net->ev_side = kf_event_new();
     for (auto &e : net->ev_step) e = kf_event_new();
-    if (!net->wg_stream || !net->ev_go || !net->ev_side || !net->ev_step[0] || !net->ev_step[1] || !net->ev_step[2]) {
+    net->ev_aux = kf_event_new();
+    if (!net->wg_stream || !net->ev_go || !net->ev_side || !net->ev_step[0] || !net->ev_step[1] || !net->ev_step[2] ||
+        !net->ev_aux) {
         set_err("create the weight-gradient stream");
         return false;
     }
@@ -1367,21 +1371,43 @@ static int forward_impl(KfNet *net, const void *features, int T) {
                     E.scale8 = nl.a8.s;
                 }
                 if (conv_compact(net, (int)li)) {
-                    // output frames 3c (c < Tc0), then the tail T-1-3(nt-1) ... T-1 (compact
-                    // rows Tc0 ..): two time-strided launches into compact rows
+                    // output frames 3c (c < Tc0), and the tail T-1-3(nt-1) ... T-1 (compact rows
+                    // Tc0 ..): two time-strided launches into compact rows. The tail's few
+                    // workgroups (latency: the whole K loop for ~200 rows) run beside the main
+                    // launch on the weight-gradient stream.
+                    const int nt = net->Tc - net->Tc0;
+                    void *const cst = kf_get_stream();
+                    const bool side = nt > 0 && net->wg_stream;
+                    if (nt > 0) {
+                        const size_t r0 = (size_t)net->Tc0 * L.hout * L.fout;  // elements
+                        KfOperand At = A;
+                        At.tmul = 3;
+                        At.t0 = T - 1 - 3 * (nt - 1);
+                        At.nrows = nt * L.hout;
+                        KfEpilogue Et = E;
+                        Et.out = (char *)nl.act + r0 * 2;
+                        Et.mask_out = nl.mask + r0 / 8;
+                        if (side && (kf_event_record(net->ev_go, cst) != 0 || kf_stream_wait(net->wg_stream, net->ev_go) != 0)) {
+                            set_err("forward: conv tail stream order");
+                            return -1;
+                        }
+                        if (side) kf_set_stream(net->wg_stream);
+                        const bool ok = ck(kf_gemm_fused(nt * L.hout, L.fout, K, &At, &B, &Et), "conv (compact tail rows)");
+                        const bool rec = !side || kf_event_record(net->ev_aux, net->wg_stream) == 0;
+                        kf_set_stream(cst);
+                        if (!ok) return -1;
+                        if (!rec) {
+                            set_err("forward: conv tail event");
+                            return -1;
+                        }
+                    }
                     A.tmul = 3;
                     A.nrows = net->Tc0 * L.hout;
                     if (!ck(kf_gemm_fused(net->Tc0 * L.hout, L.fout, K, &A, &B, &E), "conv (compact rows)"))
                         return -1;
-                    const int nt = net->Tc - net->Tc0;
-                    if (nt > 0) {
-                        const size_t r0 = (size_t)net->Tc0 * L.hout * L.fout;  // elements
-                        A.t0 = T - 1 - 3 * (nt - 1);
-                        A.nrows = nt * L.hout;
-                        E.out = (char *)nl.act + r0 * 2;
-                        E.mask_out = nl.mask + r0 / 8;
-                        if (!ck(kf_gemm_fused(nt * L.hout, L.fout, K, &A, &B, &E), "conv (compact tail rows)"))
-                            return -1;
+                    if (side && kf_stream_wait(cst, net->ev_aux) != 0) {
+                        set_err("forward: conv tail join");
+                        return -1;
                     }
                     break;
                 }
@@ -2082,6 +2108,33 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
             }
             case LayerType::ConvReluBN: {
                 const int noff = (int)nl.dt.size();
+                // compact-row conv (conv_compact): the input gradient of the frames from the
+                // tail's reach up (ws - 1 ..., ws = first tail frame - 1) comes from the full-row
+                // kernel on a window of the scattered output gradient dz (zero below it). It
+                // runs first, on the weight-gradient stream (side = true) beside the residue GEMMs.
+                auto conv_window = [&](bool side) -> bool {
+                    const int nt = net->Tc - net->Tc0, ws = T - 1 - 3 * (nt - 1) - 1, tw = T - (ws - 1);
+                    const long long fi = (long long)L.hin * L.fin, fo = (long long)L.hout * L.fout;
+                    KfOperand A2 = op_col2im(nl, (const char *)dz + (ws - 1) * fo * 2, tw);
+                    KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
+                    KfEpilogue Ew = E;
+                    Ew.ldo2 = L.fin;
+                    Ew.out2 = (char *)E.out2 + (ws - 1) * fi * 2;
+                    if (E.out) {
+                        Ew.ldo = L.fin;
+                        Ew.out = (char *)E.out + (ws - 1) * fi * 2;
+                    }
+                    if (E.mask_in) Ew.mask_in = E.mask_in + (ws - 1) * fi / 8;
+                    if (side && !to_side()) return false;
+                    const bool ok = ck(kf_gemm_fused(tw * L.hin, L.fin, noff * L.fout, &A2, &B2, &Ew),
+                                       "conv dgrad (tail window)");
+                    const bool rec = !side || kf_event_record(net->ev_aux, net->wg_stream) == 0;
+                    if (side) to_main();
+                    if (!rec) set_err("backward: conv window event");
+                    return ok && rec;
+                };
+                if (want_dx && conv_compact(net, li) && net->Tc > net->Tc0 && two && E.out2 && !conv_window(true))
+                    return -1;
                 if (nl.kp) {  // small fin: the forward's im2col is still in nl.im2col
                     // wgrad over the padded K (the pad columns are zero), then the first
                     // ntaps*fin rows into the flat gradient
@@ -2192,8 +2245,14 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                             if (E.mask_in) X.mask_in = E.mask_in + f * fi / 8;
                             if (E.mask_out) X.mask_out = E.mask_out + f * fi / 8;
                         };
+                        // (the tail window, frames ws - 1 .., went to the weight-gradient stream at
+                        // the start of this step, conv_window; the residue GEMMs take frames
+                        // below it, and main joins the window after them)
+                        const bool wside = nt > 0 && two;
+                        if (nt > 0 && !two && !conv_window(false)) return -1;
+                        const int flim = nt > 0 ? ws - 2 : T - 1;  // the last frame of the residues
                         for (int e = -1; e <= 1; ++e) {
-                            const int c_lo = e < 0 ? 1 : 0, c_hi = std::min(Tc0, (ws - 1 - e) / 3 + 1);
+                            const int c_hi = std::min(Tc0, (flim - e) / 3 + 1), c_lo = e < 0 ? 1 : 0;
                             if (c_hi <= c_lo) continue;
                             KfOperand A2 = op_col2im(nl, (const char *)net->dzc + c_lo * fo * 2, c_hi - c_lo);
                             KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
@@ -2215,15 +2274,9 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                                     "conv dgrad (compact rows)"))
                                 return -1;
                         }
-                        if (nt > 0) {
-                            const int tw = T - (ws - 1);
-                            KfOperand A2 = op_col2im(nl, (const char *)dz + (ws - 1) * fo * 2, tw);
-                            KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
-                            KfEpilogue Ew = Ep;
-                            at_frame(Ew, ws - 1);
-                            if (!ck(kf_gemm_fused(tw * L.hin, L.fin, noff * L.fout, &A2, &B2, &Ew),
-                                    "conv dgrad (tail window)"))
-                                return -1;
+                        if (wside && kf_stream_wait(mainst, net->ev_aux) != 0) {
+                            set_err("backward: conv window join");
+                            return -1;
                         }
                     } else if (L.hsub > 1 && L.hin % L.hsub == 0 && !E.out) {
                         // strided conv: input row h' = hsub*j + pi only receives the taps
