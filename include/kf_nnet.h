@@ -154,8 +154,9 @@ int nnet_row_set(const KfNet *net, int *tc, int *tc0);
 int nnet_set_implicit_dz(KfNet *net, int on);
 
 /* diagnostics (tests) of the two-stream backward: main_aff chooses where the TDNN-F
- * affine weight gradients run (-1 = KF_BWD_MAIN_AFF / the default 1: every other one on
- * the input-gradient chain; 0 = all on the weight-gradient stream; 2 = all on the chain);
+ * affine weight gradients run (-1 = KF_BWD_MAIN_AFF / the default 0: all on the
+ * weight-gradient stream; 1 = every other one on the input-gradient chain; 2 = all on the
+ * chain);
  * stall_cycles > 0 queues a spin kernel of that many GPU clock cycles (kf_debug_spin) on
  * the weight-gradient stream before each of its batches of work, so that stream runs far
  * behind the chain and any missing order shows as a wrong gradient. */

@@ -231,7 +231,7 @@ struct KfNet {
     // step-neutral on the MI355X (the linear input gradient's saving is spent
     // by the masked affine input gradient on the same chain), so off by default.
     int implicit_dz = 0;
-    int main_aff = -1;             // nnet_debug_backward (tests): -1 = KF_BWD_MAIN_AFF / 1
+    int main_aff = -1;             // nnet_debug_backward (tests): -1 = KF_BWD_MAIN_AFF / 0
     // Row-subsampled train step (nnet_set_row_subsampling, r6). The chain objective reads the
     // output on rows 0 (mod 3) only, and every layer from first_c up (TDNN-F with time
     // stride 0 / 3, linear, prefinal, output) maps row t from rows t, t +- 3 of the layer
@@ -1977,13 +1977,13 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     return ck(kf_gemm_wgrad(kaff, dout, T, &A, &B, gptr(net, nl.pW2), dout, gptr(net, nl.pb2), 0),
                               "tdnnf affine wgrad");
                 };
-                // Every other TDNN-F layer's affine weight gradient runs on the chain, after its
-                // input gradient: with the edge sums in the epilogues the chain waits for the
-                // weight-gradient stream before each linear input gradient (dx_wait), and this
-                // balances the two (one box: 36.66 / 36.89 -> 36.55 / 36.65 ms; all of them on
-                // the chain 36.95 / 37.01). KF_BWD_MAIN_AFF: 0 = all on the weight-gradient
-                // stream, 2 = all on the chain (A/B).
-                static const int env_main_aff = getenv("KF_BWD_MAIN_AFF") ? atoi(getenv("KF_BWD_MAIN_AFF")) : 1;
+                // The affine weight gradients run on the weight-gradient stream. (r5, with a
+                // two-deep gradient ring, every other one ran on the chain: the chain waited for
+                // the side stream before each linear input gradient, and that balanced the two,
+                // 36.66 / 36.89 -> 36.55 / 36.65 ms. With the three-deep ring, all on side: 24.81 /
+                // 24.89 against 24.96 / 25.13 ms every other, 25.51 / 25.69 all on the chain.)
+                // KF_BWD_MAIN_AFF: 1 = every other on the chain, 2 = all on the chain (A/B).
+                static const int env_main_aff = getenv("KF_BWD_MAIN_AFF") ? atoi(getenv("KF_BWD_MAIN_AFF")) : 0;
                 const int main_aff = net->main_aff >= 0 ? net->main_aff : env_main_aff;
                 const bool aff_on_main = two && (main_aff == 2 || (main_aff == 1 && (done & 1)));
                 if (!aff_on_main && !wgrad(aff_wgrad)) return -1;
