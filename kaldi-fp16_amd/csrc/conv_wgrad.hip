@@ -16,6 +16,7 @@
 // reduction-major stager. Split over the reduction into fp32 slabs like kf_gemm_wgrad;
 // the slab reduce is gemm.hip's.
 #include <algorithm>
+#include <cstdlib>
 
 #include "gemm_common.h"
 
@@ -326,7 +327,9 @@ int kf_conv_wgrad_halo_try(int M, int N, int K, const OpD &a, const OpD &b, floa
     const int tiles = H.ctiles * H.ntiles;
     const int nks = (K + BK - 1) / BK;
     // one workgroup per CU: split the reduction so the grid is about one full wave of CUs
-    const int target = nw == 4 && lds <= 80 * 1024 ? 512 : 256;
+    // (KF_CWGRAD_TARGET: another workgroup target, A/B)
+    static const int env_target = getenv("KF_CWGRAD_TARGET") ? atoi(getenv("KF_CWGRAD_TARGET")) : 0;
+    const int target = env_target > 0 ? env_target : nw == 4 && lds <= 80 * 1024 ? 512 : 256;
     int splits = std::max(1, (target + tiles - 1) / tiles);
     splits = std::min(splits, std::max(1, nks / 8));
     H.kps = (nks + splits - 1) / splits;

@@ -1741,10 +1741,12 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
     // gradient launches 256 workgroups instead of 512. Same-box A/B (bench default, 20
     // steps, median): one stream 38.13 / 38.36 ms, two streams 37.57 / 37.52;
     // the chain's priority is neutral (37.55 without it), 512-workgroup weight gradients
-    // cost 1.2 ms (38.78). (A/B knobs: KF_BWD_HP=0 keeps the chain on the caller's stream,
-    // KF_BWD_WGT=<n> sets the weight gradients' workgroup target)
+    // cost 1.2 ms (38.78). With the row-subsampled step (r6) 160 workgroups: non-den step
+    // time 17.52 ms against 17.81 at 256, 17.57 at 128, 18.15 at 96 (same box, 3 runs each).
+    // (A/B knobs: KF_BWD_HP=0 keeps the chain on the caller's stream, KF_BWD_WGT=<n> sets
+    // the weight gradients' workgroup target)
     static const int env_hp = getenv("KF_BWD_HP") ? atoi(getenv("KF_BWD_HP")) : 1;
-    static const int env_wgt = getenv("KF_BWD_WGT") ? atoi(getenv("KF_BWD_WGT")) : 256;
+    static const int env_wgt = getenv("KF_BWD_WGT") ? atoi(getenv("KF_BWD_WGT")) : 160;
     const bool hp = two && net->hp_stream && env_hp;
     struct Target {
         int old;
