@@ -163,13 +163,14 @@ int nnet_set_implicit_dz(KfNet *net, int on);
 int nnet_debug_backward(KfNet *net, int main_aff, long long stall_cycles);
 
 /* diagnostics (tests): back-propagate through the top n layers only; device
- * pointer of an internal tensor ("dz0", "dz1", "g0", "g1", "dbott" (the buffer of the last
+ * pointer of an internal tensor ("dz0" .. "dz2", "g0" .. "g2": the backward's gradient ring,
+ * "dzlast": the ring buffer the last step wrote, "dbott" (the buffer of the last
  * TDNN-F / prefinal step), "aux", "mask",
  * "bn_scale", "bn2_scale", "dproj" (attention: the gradient of its affine output), and with fp8 on "x8q" / "x8s": the e4m3 values
  * [T x pad128(in_dim)] and E8M0 scales [T x pad128(in_dim)/32] of the MXFP8 input copy
  * the layer's GEMM reads; "w8dq" / "w8ds": a strided TDNN-F layer's e4m3 affine weight rows
  * for its MXFP8 input gradient [bottleneck x 2*pad128(out_dim)]; "dz8q" / "dz8s" with
- * layer = 0 / 1: the e4m3 copy of dz0 / dz1, and "dz8layer": 1 + the layer that copy is
+ * layer = 0 .. 2: the e4m3 copy of dz0 .. dz2, and "dz8layer": 1 + the layer that copy is
  * for, as the returned pointer value (NULL: none); `layer` selects the per-layer ones),
  * NULL if unknown */
 int nnet_backward_n(KfNet *net, const void *out_grad_dev, int n);

@@ -267,6 +267,7 @@ struct KfNet {
     bool dz_edge[3] = {false, false, false}; // row T of dz[i] already holds the strided TDNN-F edge sum
     void *w2s = nullptr;              // [kaff x dout] fp16: W2 with the BN scale folded in
     void *dbott_last = nullptr;  // the dbott buffer of the last TDNN-F / prefinal step (tests)
+    void *dz_last = nullptr;     // the input gradient the last backward step handed down (tests)
     size_t edge_half = 0;
     int fp8 = 0;
     int fp8_dgrad = 1;  // nnet_set_fp8(net, 2): MXFP8 forward, fp16 affine input gradients (tests)
@@ -1687,14 +1688,17 @@ extern "C" int nnet_backward_n(KfNet *net, const void *out_grad, int n) {
 // debugging / tests: device pointers of internal tensors
 extern "C" const void *nnet_debug_tensor(KfNet *net, const char *what, int layer) {
     std::string w = what;
+    if (w == "dzlast") return net->dz_last;
     if (w == "dz0") return net->dz[0];
     if (w == "dz1") return net->dz[1];
+    if (w == "dz2") return net->dz[2];
+    if (w == "g2") return net->g[2];
     if (w == "g0") return net->g[0];
     if (w == "g1") return net->g[1];
     if (w == "dbott") return net->dbott_last ? net->dbott_last : net->dbott;
     // the MXFP8 copies of dz[layer] (layer = buffer 0 / 1) and the layer whose affine input
     // gradient reads it (as an int, through the pointer's low bits: -1 none), MXFP8 train step
-    if ((w == "dz8q" || w == "dz8s" || w == "dz8layer") && (layer == 0 || layer == 1)) {
+    if ((w == "dz8q" || w == "dz8s" || w == "dz8layer") && layer >= 0 && layer <= 2) {
         if (w == "dz8layer") return (const void *)(intptr_t)(net->dz8_layer[layer] + 1);
         return w == "dz8q" ? (const void *)net->dz8[layer].q : (const void *)net->dz8[layer].s;
     }
@@ -2415,6 +2419,7 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
         if (!want_dx) break;  // nothing trainable below
         dz = dz_next;
         gcur = g_next;
+        net->dz_last = dz_next;
         ++stepi;
         flip = stepi % 3;
     }

@@ -115,7 +115,7 @@ def test_attention_backward_in_network_inputs(gpu):
     P = [d for n, _, _, d in net.layers if n == "output"][0]
     og = kf.upload_fp16((np.random.default_rng(7).standard_normal((T, P)) * 0.05).astype(np.float16))
     kf.check(kf.nnet.nnet_backward_n(net.h, og.ptr, 3), "backward_n")   # output, prefinal-chain, prefinal-l
-    dz = kf.read_fp16(kf.nnet.nnet_debug_tensor(net.h, b"dz0", 0), (T, H * od))
+    dz = kf.read_fp16(kf.nnet.nnet_debug_tensor(net.h, b"dzlast", 0), (T, H * od))
     proj = kf.read_fp16(kf.nnet.nnet_debug_tensor(net.h, b"aux", li), (T, H * A))
     kf.check(kf.nnet.nnet_backward_n(net.h, og.ptr, 4), "backward_n")
     got = kf.read_fp16(kf.nnet.nnet_debug_tensor(net.h, b"dproj", li), (T, H * A)).astype(np.float64)
