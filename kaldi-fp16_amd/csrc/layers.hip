@@ -128,16 +128,17 @@ __global__ __launch_bounds__(256) void k_conv_c1_fwd_tile(ConvC1 c, int dtmin, i
 // of the block's rows sit in LDS as fp32 with zero padding (as k_conv_c1_fwd_tile), so
 // the taps are LDS reads, not 2-byte global loads.
 constexpr int C1_UNROLL = 4;
+constexpr int C1_RED = 4 * 32 * 80;  // cross-wave image: 4 waves x (fout / 8 <= 32) lanes x 80 floats
 __global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, int dtmin, int dtmax, int dhmin, int dhmax,
                                                        const h16 *x, const h16 *dz, float *slab,
                                                        int rows_per_block) {
-    extern __shared__ __attribute__((aligned(16))) float red[];  // [256][10*8], then the input tile
+    extern __shared__ __attribute__((aligned(16))) float red[];  // [4 waves x fg][10*8], then the input tile
     const int fg = c.fout / 8;                 // threads per row
     const int lane_f = threadIdx.x % fg, rg = threadIdx.x / fg, nrg = blockDim.x / fg;
     const int rows = c.T * c.hout;             // < 2^31, checked on the host
     const int r0 = blockIdx.x * rows_per_block;
     const int r1 = min(rows, r0 + rows_per_block);
-    float *xs = red + 256 * 80;
+    float *xs = red + C1_RED;
     const int tb = r0 / c.hout, wd = (c.hout - 1) * c.sub + dhmax - dhmin + 1;
     const int nf = (max(r1 - 1, r0) / c.hout - tb + 1) + dtmax - dtmin;
     for (int i = threadIdx.x; i < nf * wd; i += 256) {
@@ -179,20 +180,32 @@ __global__ __launch_bounds__(256) void k_conv_c1_wgrad(ConvC1 c, int dtmin, int 
                 acc[9][e] += gv;
             }
     }
-    float *mine = red + threadIdx.x * 80;
+    // sum over the row groups in a fixed order: first the wave's row groups (lanes
+    // fg apart) by a butterfly over the lane bits above lane_f, then the waves through LDS
+    // (an 80-float image per thread needed 80 KB of LDS and held the kernel to one workgroup
+    // per CU)
 #pragma unroll
     for (int o = 0; o < 10; ++o)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) mine[o * 8 + e] = acc[o][e];
+        for (int e = 0; e < 8; ++e)
+            for (int m = fg; m < 64; m <<= 1) acc[o][e] += __shfl_xor(acc[o][e], m);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane < fg) {
+        float *mine = red + (wave * fg + lane) * 80;
+#pragma unroll
+        for (int o = 0; o < 10; ++o)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) mine[o * 8 + e] = acc[o][e];
+    }
     __syncthreads();
-    // output (o, f): sum over row groups in fixed order
     float *out = slab + (long long)blockIdx.x * (c.noff + 1) * c.fout;
+    const int nw = blockDim.x / 64;
     for (int i = threadIdx.x; i < (c.noff + 1) * c.fout; i += blockDim.x) {
         const int o = i / c.fout, f = i - o * c.fout;
         const int src = o == c.noff ? 9 : o;
         const int tf = f / 8, e = f - tf * 8;
         float s = 0.f;
-        for (int k = 0; k < nrg; ++k) s += red[(k * fg + tf) * 80 + src * 8 + e];
+        for (int k = 0; k < nw; ++k) s += red[(k * fg + tf) * 80 + src * 8 + e];
         out[i] = s;
     }
 }
@@ -358,12 +371,13 @@ int kf_conv_c1_wgrad(int T, int hin, int hout, int sub, int fout, int noff, cons
     // offsets, heights dhmin .. (hout-1)*sub + dhmax
     const size_t tile = (size_t)4 * ((rpb + hout - 1) / hout + 1 + dtmax - dtmin) *
                         ((hout - 1) * sub + dhmax - dhmin + 1);
-    if (256 * 80 * 4 + tile > 160 * 1024) {
+    // (before it: the cross-wave image, C1_RED floats)
+    if (C1_RED * 4 + tile > 160 * 1024) {
         lay_set_error("conv_c1_wgrad: input tile of %zu bytes exceeds the LDS", tile);
         return -1;
     }
-    k_conv_c1_wgrad<<<nblk, 256, 256 * 80 * 4 + tile, kf_stream()>>>(c, dtmin, dtmax, dhmin, dhmax, (const h16 *)x,
-                                                                     (const h16 *)dz, slab, rpb);
+    k_conv_c1_wgrad<<<nblk, 256, C1_RED * 4 + tile, kf_stream()>>>(c, dtmin, dtmax, dhmin, dhmax, (const h16 *)x,
+                                                                   (const h16 *)dz, slab, rpb);
     k_conv_c1_reduce<<<n, 256, 0, kf_stream()>>>(slab, nblk, n, dW, db, noff * fout);
     return lay_check("conv_c1_wgrad");
 }
