@@ -640,7 +640,9 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kfp16.core.kf_prof_enable(0)
+    kfp16.core.kf_take_pending(b"the bench's check after the timed steps (torch.cuda.synchronize)")
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    kfp16.core.kf_take_pending(b"the bench's check after torch.cuda.Event.elapsed_time")
     median_ms = dp.max_over_ranks(float(np.median(step_ms)), "cpu")
     elapsed = dp.max_over_ranks(elapsed, "cpu")
     dp1 = comm.stats() if comm is not None else (0, 0)

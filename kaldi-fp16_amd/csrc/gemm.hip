@@ -1001,13 +1001,16 @@ extern "C" int kf_prof_reserve(int n) {
 }
 // sums per class since the last collect: count, milliseconds, flops, algorithmic bytes
 extern "C" int kf_prof_collect2(int cls, long long *count, double *ms, double *flops, double *bytes) {
+    kf_take_pending(__func__);
     long long c = 0;
     double t = 0, f = 0, by = 0;
     for (auto &r : g_prof_recs) {
         if (r.cls != cls) continue;
         hipEventSynchronize(r.b);
+        kf_take_pending("kf_prof_collect2: hipEventSynchronize");
         float e = 0.f;
         hipEventElapsedTime(&e, r.a, r.b);
+        kf_take_pending("kf_prof_collect2: hipEventElapsedTime");
         c++;
         t += e;
         f += r.flops;
@@ -1069,8 +1072,10 @@ double kf_gemm_alg_bytes(const OpD &a, const OpD &b, const KfEpilogue &E, long l
     return op_src_bytes(a, 0) + op_src_bytes(b, 0) + epi_bytes(E, M, N);
 }
 extern "C" void kf_prof_reset(void) {
+    kf_take_pending(__func__);
     for (auto &r : g_prof_recs) {
         hipEventSynchronize(r.b);
+        kf_take_pending("kf_prof_reset: hipEventSynchronize");
         g_prof_pool.push_back(r.a);
         g_prof_pool.push_back(r.b);
     }
