@@ -1350,7 +1350,9 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     const bool residue = brow && a.nparts < 9;
     // time-strided rows (a.tmul > 1): a tile's output frames read tmul times the source
     // frames, so 128-row tiles keep the image in LDS
-    const int BM_ = residue || a.tmul > 1 ? 128 : 256;
+    // (KF_HALO_BM=128: 128-row tiles for every halo conv, A/B)
+    static const int env_hbm = getenv("KF_HALO_BM") ? atoi(getenv("KF_HALO_BM")) : 256;
+    const int BM_ = residue || a.tmul > 1 || env_hbm == 128 ? 128 : 256;
     H.ts = a.tmul;
     H.toff = a.t0;
     H.nf = H.ts * ((BM_ - 1 + a.hout - 1) / a.hout) + 1 + (dtmax - dtmin);
