@@ -360,7 +360,11 @@ __device__ __forceinline__ void fused_epilogue(float4v (&acc)[BM / WM / 16][BN /
     // edge row (KfEpilogue.edge_out): the row tile that holds rows [edge_r0, edge_r1) sums the
     // values it just stored, per column in row order (kf_rows_sum's order and rounding), once
     // every wave's stores are visible to the workgroup. The host falls back to kf_rows_sum when
-    // the rows span two tiles (launch<>).
+    // the rows span two tiles (launch<>). Visibility rests on CU mode with the write-through
+    // L1 (the workgroup-scope release / acquire below) and on no earlier read of out / out2
+    // in this kernel (a beta accumulation reads out, but only rows it then overwrites, and
+    // edge_src = 1 sums out2, which nothing reads before); a change to either needs a
+    // different source, e.g. the fp32 staging rounded as stored.
     if (E.edge_out && E.edge_r0 >= m0 && E.edge_r1 <= m0 + BM && E.edge_r1 <= M && E.edge_r0 < E.edge_r1) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
