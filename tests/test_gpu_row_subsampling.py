@@ -26,7 +26,7 @@ from conftest import rel_fro
 pytestmark = pytest.mark.gpu
 
 
-def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True, conv_rows=True):
+def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True, conv_rows=True, ivec=0):
     import os
     from kfp16 import synth
     net = kfp16.Network(xcfg, max_frames=T)
@@ -39,7 +39,13 @@ def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True, conv_rows=True):
         finally:
             os.environ.pop("KF_RSUB_CONV", None)
     fb = kfp16.upload_fp16(synth.make_features(T, 40))
-    net.forward(fb.ptr, T)
+    if ivec:   # Kaldi's ivector front end: one ivector per 1500-frame eg
+        B = (T + 1499) // 1500
+        iv = kfp16.upload_fp16((np.random.default_rng(5).standard_normal((B, ivec)) * 2).astype(np.float16))
+        seq = np.minimum(np.arange(B + 1) * 1500, T).astype(np.int32)
+        net.forward_ivector(fb.ptr, T, iv.ptr, seq)
+    else:
+        net.forward(fb.ptr, T)
     P = net.layers[-1][3]
     # output gradient on the supervised rows only (2 egs' chain layout: row0 = 1500 e + 30)
     g = np.zeros((T, P), np.float16)
@@ -69,16 +75,19 @@ def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True, conv_rows=True):
     return res
 
 
-@pytest.mark.parametrize("T,conv_rows", [(3000, True), (2998, True), (3000, False)])
-def test_row_subsampled_step_matches_full(gpu, T, conv_rows):
+@pytest.mark.parametrize("T,conv_rows,model", [(3000, True, "plain"), (2998, True, "plain"), (3000, False, "plain"),
+                                               (3000, True, "ivec")])
+def test_row_subsampled_step_matches_full(gpu, T, conv_rows, model):
     """conv_rows: cnn6 (the conv below the compact layers) computes only the compact rows
     (time-strided halo operand, two launches: rows 0 (mod 3) and the tail); else it runs on
-    all rows and tdnnf7 reads its output gathered"""
+    all rows and tdnnf7 reads its output gathered. model ivec: Kaldi's ivector front end
+    (cnn_tdnn_17f_ivec, nnet_forward_ivector) under the same TDNN-F stack"""
     kfp16 = gpu
     from kfp16 import synth
-    xcfg = synth.load_xconfig("cnn_tdnn_17f.xconfig")
-    full = _run(kfp16, xcfg, T, False)
-    sub = _run(kfp16, xcfg, T, True, conv_rows=conv_rows)
+    xcfg = synth.load_xconfig("cnn_tdnn_17f_ivec.xconfig" if model == "ivec" else "cnn_tdnn_17f.xconfig")
+    ivec = 100 if model == "ivec" else 0
+    full = _run(kfp16, xcfg, T, False, ivec=ivec)
+    sub = _run(kfp16, xcfg, T, True, conv_rows=conv_rows, ivec=ivec)
     tc, tc0, rows = sub["tc"], sub["tc0"], sub["rows"]
     assert tc0 == (T - 1) // 3 + 1
     assert (tc > tc0) == ((T - 1) % 3 != 0)
@@ -97,7 +106,7 @@ def test_row_subsampled_step_matches_full(gpu, T, conv_rows):
         assert np.array_equal(sub["acts"][name][:tc0].view(np.uint16), full["acts"][name][rows[:tc0]].view(np.uint16)), name
     for k, v in full["grads"].items():
         w = sub["grads"][k]
-        if k.startswith(("cnn", "idct")) and not (conv_rows and k.startswith("cnn6")):
+        if k.startswith(("cnn", "idct", "ivector")) and not (conv_rows and k.startswith("cnn6")):
             assert np.array_equal(w, v), k
         else:
             assert rel_fro(w, v) <= 1e-5, (k, rel_fro(w, v))
