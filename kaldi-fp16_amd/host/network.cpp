@@ -2464,27 +2464,38 @@ extern "C" int nnet_set_row_subsampling(KfNet *net, int stride) {
         return -1;
     }
     // the top of the output chain whose rows are row-local or 3-strided: TDNN-F with time
-    // stride 0 or 3, linear, prefinal, output; consecutive layers, nothing else reads them
+    // stride 0 or 3, linear, prefinal, output; consecutive layers. Every layer after the
+    // first of them is such a layer too (e.g. Kaldi's xent branch, prefinal-xent and
+    // output-xent on prefinal-l), and nothing below reads them.
     const int n = (int)net->layers.size();
-    if (net->chain_out != n - 1) {
-        set_err("set_row_subsampling: the chain output must be the last layer");
-        return -1;
-    }
+    auto row_local = [&](const NetLayer &nl) {
+        const Layer &L = nl.L;
+        return (L.type == LayerType::TDNNF && (L.time_stride == 0 || L.time_stride == 3)) ||
+               (L.type == LayerType::Linear && !nl.per_seq) || L.type == LayerType::Prefinal ||
+               L.type == LayerType::Output;
+    };
     int first = -1, n3 = 0;
     for (int li = net->chain_out; li >= 0; li = net->layers[li].input) {
         const NetLayer &nl = net->layers[li];
-        const Layer &L = nl.L;
-        const bool ok = (L.type == LayerType::TDNNF && (L.time_stride == 0 || L.time_stride == 3)) ||
-                        (L.type == LayerType::Linear && !nl.per_seq) || L.type == LayerType::Prefinal ||
-                        L.type == LayerType::Output;
-        if (!ok || nl.input != li - 1) break;
+        if (!row_local(nl) || nl.input != li - 1) break;
         first = li;
-        if (L.type == LayerType::TDNNF && L.time_stride == 3) ++n3;
+        if (nl.L.type == LayerType::TDNNF && nl.L.time_stride == 3) ++n3;
     }
     if (first < 0 || net->layers[first].input < 0 || net->layers[net->layers[first].input].L.type != LayerType::ConvReluBN) {
         set_err("set_row_subsampling: needs row-local / 3-strided layers above a conv-relu-batchnorm layer");
         return -1;
     }
+    for (int li = first; li < n; ++li)
+        if (!row_local(net->layers[li]) || (net->layers[li].input >= 0 && net->layers[li].input < first - 1) ||
+            net->layers[li].input2 > -100) {
+            set_err("set_row_subsampling: layer " + net->layers[li].L.name + " above the row set is not row-local");
+            return -1;
+        }
+    for (int li = 0; li < first; ++li)
+        if (net->layers[li].input >= first || net->layers[li].input2 >= first) {
+            set_err("set_row_subsampling: layer " + net->layers[li].L.name + " reads a layer of the row set");
+            return -1;
+        }
     // tail depth: one row per 3-strided layer and a margin (the scratch row's reach)
     const int nt = n3 + 4;
     const int maxTc = (net->max_T - 1) / 3 + 1 + nt;

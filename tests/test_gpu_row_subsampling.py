@@ -66,7 +66,8 @@ def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True, conv_rows=True, ivec
         assert tc == 0
         gb = kfp16.upload_fp16(g)
     out = net.read_activation("output").astype(np.float32)
-    acts = {n: net.read_activation(n) for n in ("cnn6", "tdnnf7", "tdnnf23", "prefinal-chain")}
+    names = ["cnn6", "tdnnf7", "tdnnf23", "prefinal-chain"] + [n for n, *_ in net.layers if n == "output-xent"]
+    acts = {n: net.read_activation(n) for n in names}
     net.backward(gb.ptr)
     torch.cuda.synchronize()
     grads = net.read_grads()
@@ -76,16 +77,18 @@ def _run(kfp16, xcfg, T, sub, seed_grad=3, two_stream=True, conv_rows=True, ivec
 
 
 @pytest.mark.parametrize("T,conv_rows,model", [(3000, True, "plain"), (2998, True, "plain"), (3000, False, "plain"),
-                                               (3000, True, "ivec")])
+                                               (3000, True, "ivec"), (3000, True, "kaldi")])
 def test_row_subsampled_step_matches_full(gpu, T, conv_rows, model):
     """conv_rows: cnn6 (the conv below the compact layers) computes only the compact rows
     (time-strided halo operand, two launches: rows 0 (mod 3) and the tail); else it runs on
     all rows and tdnnf7 reads its output gathered. model ivec: Kaldi's ivector front end
-    (cnn_tdnn_17f_ivec, nnet_forward_ivector) under the same TDNN-F stack"""
+    (cnn_tdnn_17f_ivec, nnet_forward_ivector) under the same TDNN-F stack; kaldi: the recipe
+    topology (ivector front end and the xent branch on prefinal-l, also on the row set)"""
     kfp16 = gpu
     from kfp16 import synth
-    xcfg = synth.load_xconfig("cnn_tdnn_17f_ivec.xconfig" if model == "ivec" else "cnn_tdnn_17f.xconfig")
-    ivec = 100 if model == "ivec" else 0
+    xcfg = synth.load_xconfig({"ivec": "cnn_tdnn_17f_ivec.xconfig", "kaldi": "cnn_tdnn_17f_kaldi.xconfig"}
+                              .get(model, "cnn_tdnn_17f.xconfig"))
+    ivec = 100 if model in ("ivec", "kaldi") else 0
     full = _run(kfp16, xcfg, T, False, ivec=ivec)
     sub = _run(kfp16, xcfg, T, True, conv_rows=conv_rows, ivec=ivec)
     tc, tc0, rows = sub["tc"], sub["tc0"], sub["rows"]
@@ -102,7 +105,7 @@ def test_row_subsampled_step_matches_full(gpu, T, conv_rows, model):
         assert np.array_equal(sub["acts"]["cnn6"].view(np.uint16), full["acts"]["cnn6"][rows].view(np.uint16))
     else:
         assert np.array_equal(sub["acts"]["cnn6"], full["acts"]["cnn6"])
-    for name in ("tdnnf7", "tdnnf23", "prefinal-chain"):
+    for name in [n for n in full["acts"] if n != "cnn6"]:
         assert np.array_equal(sub["acts"][name][:tc0].view(np.uint16), full["acts"][name][rows[:tc0]].view(np.uint16)), name
     for k, v in full["grads"].items():
         w = sub["grads"][k]
