@@ -553,6 +553,15 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         ev_fwd = torch.cuda.Event()   # this step's forward done: the den recursion runs next
         for nb in nums:   # the first refill frees the create-time upload (one device sync), untimed
             nb.refill(packs[0], copy.cuda_stream)
+        # setup, untimed: every host minibatch once through each device slot (the copy
+        # engine's first transfers from a pinned buffer ran slow: with three warm-up steps the
+        # first three timed steps took 27.2 / 26.8 / 26.0 ms against 24.5, and none with the
+        # inputs resident)
+        for b in range(npool):
+            for sl in range(2):
+                with torch.cuda.stream(copy):
+                    f32[sl].copy_(host[b], non_blocking=True)
+                nums[sl].refill(packs[b], copy.cuda_stream)
         torch.cuda.synchronize()
         state = {"i": 0}
 
