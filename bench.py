@@ -542,7 +542,14 @@ def run_workload(a, xconfig, mode, fp8, rank, world, comm, steps, warmup, prof_o
         # fp32 features (pinned host) and numerator FSTs (kf_num_batch_refill) go up on a copy
         # stream while step i computes; the step then rounds its features to fp16 (RNE,
         # fp16.go:12-70) on the GPU. Two device slots; events order reuse.
-        copy = comp if inline else torch.cuda.Stream()
+        if inline:
+            copy = comp
+        else:
+            # a NON-BLOCKING copy stream (kf_stream_new): torch's streams are blocking ones,
+            # which the legacy default stream the step runs on synchronises with implicitly
+            import ctypes
+            kfp16.core.kf_stream_new.restype = ctypes.c_void_p
+            copy = torch.cuda.ExternalStream(kfp16.core.kf_stream_new())
         host = [torch.from_numpy(f).pin_memory() for f in feats_pool]
         f32 = [torch.empty((T, 40), dtype=torch.float32, device="cuda") for _ in range(2)]
         fbufs = [torch.empty((T, 40), dtype=torch.float16, device="cuda") for _ in range(2)]
