@@ -1075,11 +1075,12 @@ static double epi_bytes(const KfEpilogue &E, long long M, long long N) {
 double kf_gemm_alg_bytes(const OpD &a, const OpD &b, const KfEpilogue &E, long long M, long long N) {
     return op_src_bytes(a, 0) + op_src_bytes(b, 0) + epi_bytes(E, M, N);
 }
+// (no hipEventSynchronize here: a record of a stream destroyed since, e.g. a closed network's
+// weight-gradient stream, made it fail with hipErrorStreamCaptureUnsupported; re-recording an
+// event, also one still in flight, is what the next launch does anyway)
 extern "C" void kf_prof_reset(void) {
     kf_take_pending(__func__);
     for (auto &r : g_prof_recs) {
-        hipEventSynchronize(r.b);
-        kf_take_pending("kf_prof_reset: hipEventSynchronize");
         g_prof_pool.push_back(r.a);
         g_prof_pool.push_back(r.b);
     }
