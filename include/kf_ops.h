@@ -239,6 +239,9 @@ int kf_gather_rows(void *dst, const void *src, long long row_bytes, int T, int t
 int kf_scatter_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc);
 /* kf_scatter_rows for the full rows r0 .. T-1 only, dst row 0 = full row r0 */
 int kf_scatter_rows_from(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc, int r0);
+/* dst block b (block_bytes each, % 16) = src block map[b], or zeros where map[b] < 0;
+ * nblocks <= 32, map a host array (the merged weight rows of a strided conv's input gradient) */
+int kf_copy_blocks(void *dst, const void *src, long long block_bytes, const int *map, int nblocks);
 /* edge[c] = rne(sum over rows[0..n) in that order of src[rows[i] * ld + c]), n <= 4 (host array) */
 int kf_rows_sum_list(void *edge, const void *src, long long ld, const int *rows, int n, int cols);
 const char *kf_layers_last_error(void);

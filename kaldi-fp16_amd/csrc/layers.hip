@@ -419,6 +419,19 @@ __global__ __launch_bounds__(256) void k_scatter_rows(uint4 *dst, const uint4 *s
         dst[i] = c >= 0 ? src[c * vpr + v] : uint4{0u, 0u, 0u, 0u};
     }
 }
+struct BlockMap {
+    int n;
+    int src[32];
+};
+// dst block b = src block M.src[b], or zeros where M.src[b] < 0 (blocks of vpb uint4)
+__global__ __launch_bounds__(256) void k_copy_blocks(uint4 *dst, const uint4 *src, long long vpb, BlockMap M) {
+    const long long n = (long long)M.n * vpb;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const int b = (int)(i / vpb);
+        const int sb = M.src[b];
+        dst[i] = sb >= 0 ? src[sb * vpb + (i - b * vpb)] : uint4{0u, 0u, 0u, 0u};
+    }
+}
 struct RowList {
     int n;
     int row[4];
@@ -458,6 +471,21 @@ int kf_scatter_rows_from(void *dst, const void *src, long long row_bytes, int T,
 }
 int kf_scatter_rows(void *dst, const void *src, long long row_bytes, int T, int tc0, int tc) {
     return kf_scatter_rows_from(dst, src, row_bytes, T, tc0, tc, 0);
+}
+int kf_copy_blocks(void *dst, const void *src, long long block_bytes, const int *map, int nblocks) {
+    kf_take_pending(__func__);
+    if (block_bytes <= 0 || block_bytes % 16 || nblocks < 0 || nblocks > 32 || (nblocks && !map)) {
+        lay_set_error("copy_blocks: bad geometry (block_bytes %lld nblocks %d)", block_bytes, nblocks);
+        return -1;
+    }
+    if (!nblocks) return 0;
+    BlockMap M;
+    M.n = nblocks;
+    for (int b = 0; b < 32; ++b) M.src[b] = b < nblocks ? map[b] : -1;
+    const long long vpb = block_bytes / 16;
+    k_copy_blocks<<<kf_blocks((long long)nblocks * vpb, 256, 4096), 256, 0, kf_stream()>>>((uint4 *)dst,
+                                                                                       (const uint4 *)src, vpb, M);
+    return lay_check("copy_blocks");
 }
 int kf_rows_sum_list(void *edge, const void *src, long long ld, const int *rows, int n, int cols) {
     kf_take_pending(__func__);

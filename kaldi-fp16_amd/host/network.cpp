@@ -85,6 +85,12 @@ struct NetLayer {
     // fused GEMM's k-contiguous B; refreshed from w16 before a forward after any change
     void *wt = nullptr;
     int wt_pi = -1, wt_K = 0, wt_N = 0;
+    // strided conv (height-subsample-out > 1), input gradient as one GEMM over every residue:
+    // the merged weight rows [np * hsub * fin x fout] (block (p, pi) = tap wm_map[p*hsub+pi]'s
+    // fin rows of W, or zeros), the parts' (dt, dh') in wm_dt / wm_dh
+    void *wm = nullptr;
+    int wm_np = -1;
+    std::vector<int> wm_map, wm_dt, wm_dh;
 };
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -1003,6 +1009,54 @@ static inline bool conv_compact(const KfNet *net, int idx) {
 // rows a layer's activation holds in the current forward
 static inline int act_rows(const KfNet *net, int idx) {
     return conv_compact(net, idx) ? net->Tc : rows_of(net, idx);
+}
+// strided conv input gradient as one GEMM over every residue (KF_HSUB_MERGE: the largest
+// merged width hsub * fin that takes it, default 128; 0 = one GEMM per residue). The merged
+// parts (dt, dh') are ordered by dt, then dh' descending, and taken only when every residue's
+// taps then keep their o order. Computed and allocated on first use.
+static bool hsub_merge(KfNet *net, NetLayer &nl) {
+    const char *e = getenv("KF_HSUB_MERGE");
+    const int lim = e ? atoi(e) : 128;
+    const Layer &L = nl.L;
+    if (L.hsub * L.fin > lim) return false;
+    if (nl.wm_np >= 0) return nl.wm_np > 0;
+    nl.wm_np = 0;
+    const int noff = (int)nl.dt.size(), hs = L.hsub;
+    std::vector<std::pair<int, int>> keys;  // (dt, -dh')
+    for (int pi = 0; pi < hs; ++pi)
+        for (int o = 0; o < noff; ++o) {
+            const int r = pi - nl.dh[o];
+            if (((r % hs) + hs) % hs) continue;
+            keys.push_back({nl.dt[o], -(r / hs)});
+        }
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    const int np = (int)keys.size();
+    if (np == 0 || np * hs > 32) return false;
+    std::vector<int> map(np * hs, -1);
+    for (int pi = 0; pi < hs; ++pi) {
+        int last = -1;
+        for (int o = 0; o < noff; ++o) {
+            const int r = pi - nl.dh[o];
+            if (((r % hs) + hs) % hs) continue;
+            const int p = (int)(std::lower_bound(keys.begin(), keys.end(), std::make_pair(nl.dt[o], -(r / hs))) -
+                                keys.begin());
+            if (p <= last || map[p * hs + pi] >= 0) return false;  // the residue's tap order not kept
+            map[p * hs + pi] = o;
+            last = p;
+        }
+    }
+    nl.wm = net->dalloc((size_t)np * hs * L.fin * L.fout * 2);
+    if (!nl.wm) return false;
+    nl.wm_map = map;
+    nl.wm_dt.resize(np);
+    nl.wm_dh.resize(np);
+    for (int p = 0; p < np; ++p) {
+        nl.wm_dt[p] = keys[p].first;
+        nl.wm_dh[p] = -keys[p].second;
+    }
+    nl.wm_np = np;
+    return true;
 }
 // compact row of source row t (nnet_set_row_subsampling), or -1 when t is not in the set
 static inline int compact_of(const KfNet *net, int t) {
@@ -2284,6 +2338,36 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                             set_err("backward: conv window join");
                             return -1;
                         }
+                    } else if (L.hsub > 1 && L.hin % L.hsub == 0 && !E.out && hsub_merge(net, nl)) {
+                        // strided conv, every residue in one GEMM of N = hsub * fin columns: the
+                        // output row (t, j) holds input rows h' = hsub*j + pi, pi < hsub, which is
+                        // the [(t,h) x fin] gradient itself. Part p = (dt, dh') of the merged list;
+                        // the weight block of (p, pi) is the tap o with dh_o = pi - hsub*dh', or
+                        // zeros. Each residue's taps keep their order in K (hsub_merge), and the
+                        // zero blocks add exact zeros, so every column sums the per-residue
+                        // GEMM's terms in its order.
+                        const int np = nl.wm_np;
+                        if (!ck(kf_copy_blocks(nl.wm, wptr(net, nl.pW), (long long)L.fin * L.fout * 2, nl.wm_map.data(),
+                                               np * L.hsub),
+                                "conv dgrad (strided, merged weights)"))
+                            return -1;
+                        KfOperand A2 = op_col2im(nl, dz, T);
+                        KfOperand B2 = op_wrows(nl.wm, np, L.hsub * L.fin, L.fout);
+                        for (int p = 0; p < np; ++p) {
+                            A2.dt[p] = -nl.wm_dt[p];
+                            A2.dh[p] = nl.wm_dh[p];
+                        }
+                        A2.nparts = B2.nparts = np;
+                        A2.ncols = B2.ncols = np * L.fout;
+                        A2.hout = L.hin / L.hsub;
+                        A2.hmul = 1;
+                        A2.hdiv = 1;
+                        A2.nrows = T * A2.hout;
+                        KfEpilogue Ep = E;
+                        Ep.ldo2 = (long long)L.hsub * L.fin;
+                        if (!ck(kf_gemm_fused(T * A2.hout, L.hsub * L.fin, np * L.fout, &A2, &B2, &Ep),
+                                "conv dgrad (strided, merged)"))
+                            return -1;
                     } else if (L.hsub > 1 && L.hin % L.hsub == 0 && !E.out) {
                         // strided conv: input row h' = hsub*j + pi only receives the taps
                         // with (pi - dh) % hsub == 0, so one GEMM per residue pi skips the
