@@ -1011,12 +1011,13 @@ static inline int act_rows(const KfNet *net, int idx) {
     return conv_compact(net, idx) ? net->Tc : rows_of(net, idx);
 }
 // strided conv input gradient as one GEMM over every residue (KF_HSUB_MERGE: the largest
-// merged width hsub * fin that takes it, default 128; 0 = one GEMM per residue). The merged
+// merged width hsub * fin that takes it; default 0 = one GEMM per residue: merged, the zero
+// blocks' third more MFMA work cost what the wider tiles gain). The merged
 // parts (dt, dh') are ordered by dt, then dh' descending, and taken only when every residue's
 // taps then keep their o order. Computed and allocated on first use.
 static bool hsub_merge(KfNet *net, NetLayer &nl) {
     const char *e = getenv("KF_HSUB_MERGE");
-    const int lim = e ? atoi(e) : 128;
+    const int lim = e ? atoi(e) : 0;
     const Layer &L = nl.L;
     if (L.hsub * L.fin > lim) return false;
     if (nl.wm_np >= 0) return nl.wm_np > 0;
