@@ -90,6 +90,8 @@ struct NetLayer {
     // fin rows of W, or zeros), the parts' (dt, dh') in wm_dt / wm_dh
     void *wm = nullptr;
     int wm_np = -1;
+    // conv input gradient, per-tap transposed weight blocks [fout x fin] (dgrad_wt)
+    void *wtd = nullptr;
     std::vector<int> wm_map, wm_dt, wm_dh;
 };
 
@@ -1058,6 +1060,33 @@ static bool hsub_merge(KfNet *net, NetLayer &nl) {
     }
     nl.wm_np = np;
     return true;
+}
+// conv input gradient with the weights as a plain [taps * fout x fin] B, N contiguous (the
+// forward's B layout): block i = (tap taps[i]'s fin rows of W)^T, one batched transpose per
+// layer and step. The shifted k-contiguous weight rows (op_wrows, the BROW halo kernels) ran
+// cnn4's input gradient at half the forward's rate. KF_DGRAD_WT=0: op_wrows. The K order is
+// the same either way, so the result is bit-identical.
+static bool dgrad_wt_on() {
+    const char *e = getenv("KF_DGRAD_WT");
+    return !(e && e[0] == '0');
+}
+static void *dgrad_wt(KfNet *net, NetLayer &nl, const std::vector<int> &taps) {
+    const Layer &L = nl.L;
+    const size_t blk = (size_t)L.fin * L.fout * 2;
+    if ((int)taps.size() > KF_TRANSPOSE_MAX || taps.size() > nl.dt.size()) return nullptr;
+    if (!nl.wtd) nl.wtd = net->dalloc(nl.dt.size() * blk);
+    if (!nl.wtd) return nullptr;
+    std::vector<const void *> src;
+    std::vector<void *> dst;
+    std::vector<int> M, N;
+    for (size_t i = 0; i < taps.size(); ++i) {
+        src.push_back((const char *)wptr(net, nl.pW) + taps[i] * blk);
+        dst.push_back((char *)nl.wtd + i * blk);
+        M.push_back(L.fin);
+        N.push_back(L.fout);
+    }
+    if (kf_transpose_batch((int)taps.size(), src.data(), dst.data(), M.data(), N.data()) != 0) return nullptr;
+    return nl.wtd;
 }
 // compact row of source row t (nnet_set_row_subsampling), or -1 when t is not in the set
 static inline int compact_of(const KfNet *net, int t) {
@@ -2373,6 +2402,17 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                         // strided conv: input row h' = hsub*j + pi only receives the taps
                         // with (pi - dh) % hsub == 0, so one GEMM per residue pi skips the
                         // (hsub-1)/hsub of the K range the plain col2im reads as zeros
+                        const bool twt = dgrad_wt_on();
+                        std::vector<int> taps;  // every residue's taps, residue by residue
+                        for (int pi = 0; pi < L.hsub; ++pi)
+                            for (int o = 0; o < noff; ++o)
+                                if (!((((pi - nl.dh[o]) % L.hsub) + L.hsub) % L.hsub)) taps.push_back(o);
+                        char *wt = nullptr;
+                        if (twt && !(wt = (char *)dgrad_wt(net, nl, taps))) {
+                            set_err("conv dgrad (strided): transposed weights of " + L.name);
+                            return -1;
+                        }
+                        int tap0 = 0;  // the residue's first block in wt
                         for (int pi = 0; pi < L.hsub; ++pi) {
                             KfOperand A2 = op_col2im(nl, dz, T);
                             KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
@@ -2388,6 +2428,8 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                             if (!np) continue;
                             A2.nparts = B2.nparts = np;
                             A2.ncols = B2.ncols = np * L.fout;
+                            if (twt) B2 = op_base(wt + (size_t)tap0 * L.fin * L.fout * 2, L.fin, np * L.fout, L.fin, 0);
+                            tap0 += np;
                             A2.hout = L.hin / L.hsub;
                             A2.hmul = 1;
                             A2.hdiv = 1;
@@ -2403,6 +2445,16 @@ static int backward_impl(KfNet *net, const void *out_grad, int max_layers) {
                     } else {
                         KfOperand A2 = op_col2im(nl, dz, T);
                         KfOperand B2 = op_wrows(wptr(net, nl.pW), noff, L.fin, L.fout);
+                        if (dgrad_wt_on()) {
+                            std::vector<int> taps(noff);
+                            for (int o = 0; o < noff; ++o) taps[o] = o;
+                            void *wt = dgrad_wt(net, nl, taps);
+                            if (!wt) {
+                                set_err("conv dgrad: transposed weights of " + L.name);
+                                return -1;
+                            }
+                            B2 = op_base(wt, L.fin, noff * L.fout, L.fin, 0);
+                        }
                         E.ldo2 = L.fin;  // dz of the input conv layer viewed as [(t,h) x fin]
                         if (E.out) E.ldo = L.fin;
                         if (!ck(kf_gemm_fused(T * L.hin, L.fin, noff * L.fout, &A2, &B2, &E), "conv dgrad"))
