@@ -1352,7 +1352,8 @@ static int conv_halo_try(int M, int N, int K, const OpD &a, const OpD &b, int bm
     // 256-row tiles, except 128-row tiles for the strided convs' per-residue input
     // gradients (3 or 6 taps; two workgroups per CU): cnn3 461 -> 332 and 588 -> 460 us,
     // cnn5 370 -> 317 and 536 -> 468 us
-    const bool residue = a.nparts < 9;  // (B as shifted weight rows or a transposed copy)
+    static const int env_rbm = getenv("KF_HALO_RES_BM") ? atoi(getenv("KF_HALO_RES_BM")) : 128;
+    const bool residue = a.nparts < 9 && env_rbm != 256;  // (B as shifted weight rows or a transposed copy)
     // time-strided rows (a.tmul > 1): a tile's output frames read tmul times the source
     // frames, so 128-row tiles keep the image in LDS
     // (KF_HALO_BM=128: 128-row tiles for every halo conv, A/B)
